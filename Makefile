@@ -1,0 +1,41 @@
+# fantoch_amd build (no cmake/ninja needed).  `make` builds the product
+# library and the oracle; both are plain in-tree .so files so they travel to
+# the GPU box with the repo snapshot.
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+ARCH ?= gfx950
+JOBS ?= 8
+
+LIB := fantoch_amd/libfantoch_amd.so
+ORACLE := oracle/build/liboracle.so
+CPPTEST := tests/cpp/build/test_graph_executor
+
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
+            -Iinclude -Ifantoch_amd/csrc
+SRCS := fantoch_amd/csrc/graph_exec.hip fantoch_amd/csrc/executor_host.cpp
+HDRS := include/fantoch_amd.h include/fantoch_amd.hpp fantoch_amd/csrc/fx_synth.h fantoch_amd/csrc/fx_internal.h
+
+all: $(LIB) $(ORACLE) $(CPPTEST)
+
+$(LIB): $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+
+$(ORACLE): oracle/graph_oracle.cpp include/fantoch_amd.h
+	@mkdir -p oracle/build
+	$(CXX) -O2 -std=c++17 -fPIC -shared -Wall -o $@ oracle/graph_oracle.cpp -lpthread
+
+# C++ port of the reference's graph unit tests against the C++ Executor mirror
+$(CPPTEST): tests/cpp/test_graph_executor.cpp include/fantoch_amd.hpp include/fantoch_amd.h $(LIB)
+	@mkdir -p tests/cpp/build
+	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ tests/cpp/test_graph_executor.cpp \
+	  -Lfantoch_amd -lfantoch_amd -Wl,-rpath,'$$ORIGIN/../../../fantoch_amd'
+
+# kernel resource usage (VGPR/SGPR/LDS/occupancy) for DESIGN.md / tuning
+resource-usage:
+	$(HIPCC) $(HIPFLAGS) -c -o /tmp/fx_ge.o fantoch_amd/csrc/graph_exec.hip \
+	  -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|SGPRs:|ScratchSize|Occupancy|LDS Size"
+
+clean:
+	rm -f $(LIB) $(ORACLE) $(CPPTEST)
+
+.PHONY: all clean resource-usage

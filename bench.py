@@ -1,0 +1,279 @@
+#!/usr/bin/env python3
+"""bench.py — executed commands/s of the batched GPU GraphExecutor (BASELINE.json configs[1]).
+
+Workload (per GPU; weak scaling): EPaxos n=5, 4096 seeds x conflict rates
+{0,2,10,50,100}% = 20,480 instances, 1 client per process x 1,000 commands
+-> 5 commit streams of 5,000 Adds per instance (102,400 streams, 512M Adds).
+Streams are seeded synthetic Atlas/EPaxos commit streams generated on the GPU
+(fantoch_amd/csrc/fx_synth.h) before the timed region.
+
+One step = one pass of the hot path over the resident batch:
+  fx_batch_execute (GraphExecutor::handle over every Add of every stream)
+  + fx_batch_metrics (ChainSize / ExecutionDelay histograms)
+  + all-reduce of the histograms over ranks (RCCL) when N > 1.
+
+Launch: python bench.py --gpus N --steps K --warmup W   (N > 1 via torch.distributed.run)
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "executed cmds/sec (node) for batched Atlas/EPaxos sims; % of HBM roofline"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--seeds", type=int, default=4096)
+    ap.add_argument("--conflicts", type=str, default="0,2,10,50,100")
+    ap.add_argument("--n", type=int, default=5)
+    ap.add_argument("--cmds", type=int, default=1000)
+    ap.add_argument("--window", type=int, default=8)
+    ap.add_argument("--cycle-pct", type=int, default=30)
+    ap.add_argument("--seed", type=int, default=20250213)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", type=str, default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from fantoch_amd import _lib
+    from fantoch_amd import streams as fs
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    lib = _lib.load()
+    if lib.fx_device_count() <= 0:
+        raise SystemExit("no GPU visible to libfantoch_amd")
+
+    conflicts = [int(c) for c in args.conflicts.split(",")]
+    instances = args.seeds * len(conflicts)
+    p = fs.synth_params(seed=args.seed, instances=instances, n=args.n, cmds=args.cmds,
+                        window=args.window, cycle_pct=args.cycle_pct, conflicts=conflicts,
+                        instance_base=rank * instances)
+    S, steps, dmax = fs.synth_shape(p)
+    pw = _lib.plane_words(S, steps)
+    stream = torch.cuda.current_stream(dev)
+    hs = ctypes.c_void_p(stream.cuda_stream)
+
+    def buf(words):
+        return torch.empty(words, dtype=torch.int32, device=dev)
+
+    dot, hdr, deps = buf(pw), buf(pw), buf(pw * dmax)
+    order, release = buf(pw), buf(pw)
+    nexec, err = buf(S), buf(S)
+    NBC, NBD = 64, 4096
+    chain = torch.zeros(NBC, dtype=torch.int64, device=dev)
+    delay = torch.zeros(NBD, dtype=torch.int64, device=dev)
+
+    t0 = time.time()
+    _lib.check(lib.fx_synth_generate(ctypes.byref(p), dot.data_ptr(), hdr.data_ptr(),
+                                     deps.data_ptr(), hs), "fx_synth_generate")
+    torch.cuda.synchronize(dev)
+    gen_s = time.time() - t0
+    inb = _lib.StreamBatch(dot.data_ptr(), hdr.data_ptr(), deps.data_ptr(), None, S, steps, dmax,
+                           args.n)
+    outb = _lib.OrderBatch(order.data_ptr(), release.data_ptr(), nexec.data_ptr(), err.data_ptr())
+    hb = _lib.HistBatch(chain.data_ptr(), NBC, delay.data_ptr(), NBD)
+
+    # algorithmic bytes of one executor launch: read dot + hdr + the used dep
+    # words of every Add, write one order word + one release word per command
+    nd_total = int(((hdr >> 24) & 31).sum(dtype=torch.int64).item())
+    n_adds = S * steps
+    alg_bytes = 16 * n_adds + 4 * nd_total
+
+    tiered = [False]
+    tier_counts = (ctypes.c_uint32 * _lib.FX_NUM_TIERS)()
+
+    def step():
+        chain.zero_()
+        delay.zero_()
+        if tiered[0]:
+            st = lib.fx_batch_run_tiered(ctypes.byref(inb), ctypes.byref(outb), 0, hs, tier_counts)
+        else:
+            st = lib.fx_batch_execute(ctypes.byref(inb), ctypes.byref(outb), 0, None, S, None, 0,
+                                      steps, _lib.FX_FLAG_INIT, None, hs)
+        _lib.check(st, "executor")
+        _lib.check(lib.fx_batch_metrics(ctypes.byref(inb), ctypes.byref(outb), ctypes.byref(hb), hs),
+                   "metrics")
+        if world > 1:
+            dist.all_reduce(chain)
+            dist.all_reduce(delay)
+
+    # warmup (+ decide whether any stream needs a tier rerun)
+    for w in range(max(args.warmup, 1)):
+        step()
+        torch.cuda.synchronize(dev)
+        if w == 0:
+            bad = int((err != 0).sum().item())
+            if bad:
+                tiered[0] = True
+                step()
+                torch.cuda.synchronize(dev)
+    if int((err != 0).sum().item()) != 0:
+        raise SystemExit("streams failed: %s" % torch.unique(err).tolist())
+    executed_local = int(nexec.sum(dtype=torch.int64).item())
+
+    lib.fx_profile_enable(1)
+    kernel_ms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        if not tiered[0]:
+            ms = ctypes.c_float()
+            # events were recorded on `hs` around the executor kernel; reading
+            # them after the step keeps the next launch queued behind this one
+            if lib.fx_profile_last_exec_ms(ctypes.byref(ms)) == 0:
+                kernel_ms.append(ms.value)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lib.fx_profile_enable(0)
+
+    stats = torch.tensor([elapsed, executed_local, nd_total, n_adds], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = stats[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats[1:].clone()
+        dist.all_reduce(sm)
+        elapsed = float(mx.item())
+        executed_total, nd_all, adds_all = [float(x) for x in sm.tolist()]
+    else:
+        executed_total, nd_all, adds_all = float(executed_local), float(nd_total), float(n_adds)
+
+    value = executed_total * args.steps / elapsed
+    edges = nd_all * args.steps / elapsed
+    kavg = sum(kernel_ms) / len(kernel_ms) if kernel_ms else None
+
+    result = None
+    if rank == 0:
+        roof = None
+        if kavg:
+            achieved = alg_bytes / (kavg * 1e-3) / 1e9
+            traffic = None
+            if os.path.exists(args.traffic_json):
+                try:
+                    tj = json.load(open(args.traffic_json))
+                    if tj.get("workload_key") == workload_key(args):
+                        traffic = tj.get("hbm_bytes_per_launch")
+                except Exception:
+                    traffic = None
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                    "traffic": traffic, "kernel": "k_graph_exec<Tier0>",
+                    "kernel_ms_avg": round(kavg, 4), "alg_bytes_per_launch": alg_bytes,
+                    "alg_bytes_per_cmd": round(alg_bytes / n_adds, 3)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args, lib, dot, hdr, deps, order, release, nexec, S, steps, dmax, pw)
+        result = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "cmds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded Atlas/EPaxos-like commit streams generated on device)",
+            "config": {
+                "workload": "EPaxos n=%d, %d seeds x conflict {%s}%%, %d cmds/process, 1 client/region "
+                            "(BASELINE configs[1])" % (args.n, args.seeds, args.conflicts, args.cmds),
+                "instances_per_gpu": instances, "streams_per_gpu": S, "adds_per_stream": steps,
+                "window": args.window, "cycle_pct": args.cycle_pct, "seed": args.seed,
+                "parallelism": "instances sharded over %d GPU(s), one wavefront lane per stream" % world,
+            },
+            "edges_per_s": round(edges, 1),
+            "executed_per_step": int(executed_total),
+            "tier_reruns": bool(tiered[0]),
+            "gen_seconds": round(gen_s, 3),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+def workload_key(args):
+    return "n%d_s%d_c%s_m%d_w%d_y%d_seed%d" % (args.n, args.seeds, args.conflicts.replace(",", "-"),
+                                              args.cmds, args.window, args.cycle_pct, args.seed)
+
+
+def cpu_baseline(args, lib, dot, hdr, deps, order, release, nexec, S, steps, dmax, pw):
+    """Times the CPU oracle (C++ restatement of the reference GraphExecutor) on a
+    bounded prefix of the same batch, with std::threads over streams like the
+    reference's rayon par_iter, and checks that prefix against the GPU output."""
+    import numpy as np
+    from fantoch_amd import streams as fs
+    from oracle import oracle_lib
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    # calibrate: ~2M Adds/s per thread -> pick whole tiles of 64 streams
+    budget_adds = args.cpu_baseline_seconds * 2.0e6 * threads
+    tiles = int(max(1, min((S + 63) // 64, budget_adds // (64 * steps))))
+    Ss = min(S, tiles * 64)
+    steps4 = (steps + 3) // 4
+    words = tiles * steps4 * 256
+    to_np = lambda t, off, cnt: t[off:off + cnt].cpu().numpy().view(np.uint32)
+    planes = fs.Planes(Ss, steps, dmax, args.n)
+    planes.dot[:] = to_np(dot, 0, words)[:planes.plane]
+    planes.hdr[:] = to_np(hdr, 0, words)[:planes.plane]
+    for j in range(dmax):
+        planes.deps[j * planes.plane:(j + 1) * planes.plane] = to_np(deps, j * pw, words)[:planes.plane]
+    t0 = time.perf_counter()
+    o_order, o_rel, o_nexec, o_err = oracle_lib.batch_execute(planes, threads=threads)
+    dt = time.perf_counter() - t0
+    executed = int(o_nexec.sum())
+    g_order = to_np(order, 0, words)
+    g_rel = to_np(release, 0, words)
+    g_nexec = nexec[:Ss].cpu().numpy().view(np.uint32)
+    parity = bool(np.array_equal(g_nexec, o_nexec))
+    if parity:
+        for s in range(Ss):
+            idx = fs.index(np.arange(int(o_nexec[s])), s, steps)
+            if not np.array_equal(g_order[idx], o_order[idx]):
+                parity = False
+                break
+        ridx = np.concatenate([fs.index(np.arange(steps), s, steps) for s in range(Ss)])
+        parity = parity and bool(np.array_equal(g_rel[ridx], o_rel[ridx]))
+    return {"value": round(executed / dt, 1), "unit": "cmds/s", "cores": threads, "kind": "port",
+            "sample": "first %d streams (%d Adds) of the same batch, %.2f s wall on %d threads; "
+                      "GPU output on the sample %s the oracle bit-for-bit"
+                      % (Ss, Ss * steps, dt, threads, "matches" if parity else "DIFFERS FROM"),
+            "sample_parity": parity}
+
+
+if __name__ == "__main__":
+    main()

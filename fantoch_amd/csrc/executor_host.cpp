@@ -1,0 +1,524 @@
+// executor_host.cpp — the `Executor` trait (fantoch/src/executor/mod.rs:27-89)
+// as a C-ABI handle over the HIP batch kernel, plus Histogram statistics.
+//
+// A handle owns one commit stream.  handle_add appends the Add to a host log
+// (mirrored in the tiled plane layout); pulling results (to_clients, drain,
+// metrics, monitor, pending) runs the new steps on the GPU, resuming from the
+// executor state saved by the previous launch, and converts the executed order
+// into ExecutorResults exactly like GraphExecutor::fetch_commands_to_execute +
+// execute (executor.rs:126-138,184-188) -> Command::execute (command.rs:147-162)
+// -> KVStore::execute + ExecutionOrderMonitor::add (kvs.rs:53-65, monitor.rs:21-31).
+// There is no CPU execution path: without a GPU the constructor fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <vector>
+
+#include "fantoch_amd.h"
+#include "fx_internal.h"
+
+namespace {
+
+struct Cmd {
+  fx_rifl rifl;
+  std::vector<uint32_t> keys;  // ascending (canonical C11)
+  uint32_t read_only;
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  bool ensure(size_t b) {
+    if (bytes >= b) return true;
+    release();
+    if (hipMalloc(&p, b) != hipSuccess) {
+      p = nullptr;
+      return false;
+    }
+    bytes = b;
+    return true;
+  }
+  uint32_t* u32() const { return static_cast<uint32_t*>(p); }
+};
+
+constexpr uint32_t kDmaxDev = 31;
+
+}  // namespace
+
+struct fx_graph_executor {
+  uint8_t process_id = 0;
+  uint64_t shard_id = 0;
+  fx_config cfg{};
+  uint32_t executor_index = 0;
+  hipStream_t stream = nullptr;
+
+  // host log (arrival order)
+  std::vector<uint32_t> dots, hdrs;
+  std::vector<std::vector<uint32_t>> deps;
+  std::vector<Cmd> cmds;
+  bool have_base = false;
+  uint64_t t_base = 0;
+  uint32_t init_frontier[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool use_frontier = false;
+
+  // device mirror
+  uint32_t cap = 0;      // plane rows
+  uint32_t dmax = 0;     // dep planes in use
+  uint32_t uploaded = 0; // rows present on the device
+  DevBuf d_dot, d_hdr, d_deps, d_order, d_release, d_nexec, d_err, d_state;
+  uint32_t tier = 0;
+  uint32_t processed = 0;  // steps executed by the device state
+  uint32_t consumed = 0;   // order entries already converted
+
+  // outputs
+  std::deque<fx_executor_result> to_clients;
+  std::deque<std::pair<uint32_t, bool>> executed;  // (packed dot, scc start)
+  std::map<uint64_t, uint64_t> chain_size, execution_delay;
+  std::map<uint32_t, std::vector<fx_rifl>> monitor;
+  std::vector<uint32_t> release_host;
+  int sticky = FX_OK;
+};
+
+namespace {
+
+int upload_all(fx_graph_executor* ex, uint32_t new_cap, uint32_t new_dmax) {
+  const size_t plane = fx_plane_words(1, new_cap);
+  if (!ex->d_dot.ensure(plane * 4) || !ex->d_hdr.ensure(plane * 4) ||
+      !ex->d_deps.ensure(plane * 4 * std::max<uint32_t>(new_dmax, 1)) ||
+      !ex->d_order.ensure(plane * 4) || !ex->d_release.ensure(plane * 4) ||
+      !ex->d_nexec.ensure(4) || !ex->d_err.ensure(4))
+    return FX_ERR_HIP;
+  std::vector<uint32_t> hd(plane, 0), hh(plane, 0), hp(plane * std::max<uint32_t>(new_dmax, 1), 0);
+  const uint32_t N = (uint32_t)ex->dots.size();
+  for (uint32_t i = 0; i < N; ++i) {
+    const size_t at = fx_index(i, 0, new_cap);
+    hd[at] = ex->dots[i];
+    hh[at] = ex->hdrs[i];
+    for (uint32_t j = 0; j < ex->deps[i].size(); ++j) hp[j * plane + at] = ex->deps[i][j];
+  }
+  if (hipMemcpyAsync(ex->d_dot.p, hd.data(), plane * 4, hipMemcpyHostToDevice, ex->stream) ||
+      hipMemcpyAsync(ex->d_hdr.p, hh.data(), plane * 4, hipMemcpyHostToDevice, ex->stream) ||
+      hipMemcpyAsync(ex->d_deps.p, hp.data(), hp.size() * 4, hipMemcpyHostToDevice, ex->stream) ||
+      hipStreamSynchronize(ex->stream))
+    return FX_ERR_HIP;
+  ex->cap = new_cap;
+  ex->dmax = new_dmax;
+  ex->uploaded = N;
+  return FX_OK;
+}
+
+// Copies rows [from, N) of the single-stream planes to the device.
+int upload_tail(fx_graph_executor* ex) {
+  const uint32_t N = (uint32_t)ex->dots.size();
+  if (ex->uploaded >= N) return FX_OK;
+  const uint32_t r0 = ex->uploaded & ~3u;
+  const uint32_t r1 = (N + 3) & ~3u;
+  const size_t w0 = fx_index(r0, 0, ex->cap), words = (size_t)(r1 - r0) / 4 * 256;
+  const size_t plane = fx_plane_words(1, ex->cap);
+  std::vector<uint32_t> hd(words, 0), hh(words, 0), hp(words * ex->dmax, 0);
+  for (uint32_t i = r0; i < N; ++i) {
+    const size_t at = fx_index(i, 0, ex->cap) - w0;
+    hd[at] = ex->dots[i];
+    hh[at] = ex->hdrs[i];
+    for (uint32_t j = 0; j < ex->deps[i].size(); ++j) hp[j * words + at] = ex->deps[i][j];
+  }
+  if (hipMemcpyAsync(ex->d_dot.u32() + w0, hd.data(), words * 4, hipMemcpyHostToDevice, ex->stream) ||
+      hipMemcpyAsync(ex->d_hdr.u32() + w0, hh.data(), words * 4, hipMemcpyHostToDevice, ex->stream))
+    return FX_ERR_HIP;
+  for (uint32_t j = 0; j < ex->dmax; ++j)
+    if (hipMemcpyAsync(ex->d_deps.u32() + j * plane + w0, hp.data() + j * words, words * 4,
+                       hipMemcpyHostToDevice, ex->stream))
+      return FX_ERR_HIP;
+  if (hipStreamSynchronize(ex->stream)) return FX_ERR_HIP;
+  ex->uploaded = N;
+  return FX_OK;
+}
+
+// Runs the steps not yet executed; converts new order entries.
+int flush(fx_graph_executor* ex) {
+  if (ex->sticky) return ex->sticky;
+  const uint32_t N = (uint32_t)ex->dots.size();
+  if (ex->processed >= N) return FX_OK;
+  uint32_t need_dmax = ex->dmax;
+  for (uint32_t i = ex->uploaded; i < N; ++i) need_dmax = std::max<uint32_t>(need_dmax, (uint32_t)ex->deps[i].size());
+  if (N > ex->cap || need_dmax > ex->dmax) {
+    uint32_t nc = std::max<uint32_t>(64, ex->cap);
+    while (nc < N) nc *= 2;
+    int st = upload_all(ex, nc, std::max<uint32_t>(need_dmax, 1));
+    if (st) return ex->sticky = st;
+  } else {
+    int st = upload_tail(ex);
+    if (st) return ex->sticky = st;
+  }
+  fx_stream_batch in{};
+  in.dot = ex->d_dot.u32();
+  in.hdr = ex->d_hdr.u32();
+  in.deps = ex->d_deps.u32();
+  in.lengths = nullptr;
+  in.num_streams = 1;
+  in.steps = ex->cap;
+  in.dmax = ex->dmax;
+  in.n = ex->cfg.n;
+  fx_order_batch out{ex->d_order.u32(), ex->d_release.u32(), ex->d_nexec.u32(), ex->d_err.u32()};
+  uint32_t nexec = 0, err = 0;
+  while (true) {
+    if (!ex->d_state.ensure(fx_batch_state_bytes(ex->tier, ex->cfg.n, 1))) return ex->sticky = FX_ERR_HIP;
+    uint32_t flags = FX_FLAG_SAVE_STATE;
+    if (ex->processed == 0) flags |= FX_FLAG_INIT;
+    if (ex->cfg.execute_at_commit) flags |= FX_FLAG_EXECUTE_AT_COMMIT;
+    DevBuf d_front;
+    const uint32_t* front = nullptr;
+    if (ex->processed == 0 && ex->use_frontier) {
+      if (!d_front.ensure(32) ||
+          hipMemcpyAsync(d_front.p, ex->init_frontier, 32, hipMemcpyHostToDevice, ex->stream))
+        return ex->sticky = FX_ERR_HIP;
+      front = d_front.u32();
+    }
+    int st = fx_batch_execute(&in, &out, ex->tier, nullptr, 1, ex->d_state.p, ex->processed, N, flags,
+                              front, ex->stream);
+    if (st) return ex->sticky = st;
+    if (hipMemcpyAsync(&nexec, ex->d_nexec.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
+        hipMemcpyAsync(&err, ex->d_err.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
+        hipStreamSynchronize(ex->stream))
+      return ex->sticky = FX_ERR_HIP;
+    if (err == FX_ERR_CAPACITY && ex->tier + 1 < FX_NUM_TIERS) {
+      // rerun the whole log one tier up; the already-consumed prefix of the
+      // (deterministic) order is skipped below
+      ex->tier += 1;
+      ex->processed = 0;
+      continue;
+    }
+    break;
+  }
+  if (err) return ex->sticky = (int)err;
+  ex->processed = N;
+  if (nexec <= ex->consumed) return FX_OK;
+  // read back the new order entries and the release steps they need
+  std::vector<uint32_t> order(nexec - ex->consumed);
+  const uint32_t k0 = ex->consumed;
+  {
+    const uint32_t r0 = k0 & ~3u, r1 = (nexec + 3) & ~3u;
+    std::vector<uint32_t> rows((size_t)(r1 - r0) / 4 * 256);
+    if (hipMemcpyAsync(rows.data(), ex->d_order.u32() + fx_index(r0, 0, ex->cap), rows.size() * 4,
+                       hipMemcpyDeviceToHost, ex->stream) ||
+        hipStreamSynchronize(ex->stream))
+      return ex->sticky = FX_ERR_HIP;
+    for (uint32_t k = k0; k < nexec; ++k) order[k - k0] = rows[fx_index(k, 0, ex->cap) - fx_index(r0, 0, ex->cap)];
+  }
+  {
+    const uint32_t r1 = (N + 3) & ~3u;
+    std::vector<uint32_t> rows((size_t)r1 / 4 * 256);
+    if (hipMemcpyAsync(rows.data(), ex->d_release.p, rows.size() * 4, hipMemcpyDeviceToHost, ex->stream) ||
+        hipStreamSynchronize(ex->stream))
+      return ex->sticky = FX_ERR_HIP;
+    ex->release_host.resize(N);
+    for (uint32_t i = 0; i < N; ++i) ex->release_host[i] = rows[fx_index(i, 0, ex->cap)];
+  }
+  // convert (fetch_commands_to_execute -> execute), collecting metrics
+  for (size_t x = 0; x < order.size(); ++x) {
+    const uint32_t o = order[x];
+    const uint32_t rec = FX_ORDER_REC(o);
+    const bool start = (o & FX_ORDER_SCC_START) != 0;
+    if (start && !ex->cfg.execute_at_commit) {
+      uint64_t size = 1;
+      while (x + size < order.size() && !(order[x + size] & FX_ORDER_SCC_START)) ++size;
+      ex->chain_size[size] += 1;  // ChainSize (mod.rs:492-493)
+    }
+    if (!ex->cfg.execute_at_commit) {
+      const uint32_t rs = ex->release_host[rec];
+      const uint64_t delay = (uint64_t)FX_HDR_T(ex->hdrs[rs]) - FX_HDR_T(ex->hdrs[rec]);
+      ex->execution_delay[delay] += 1;  // ExecutionDelay (mod.rs:514-518)
+    }
+    ex->executed.emplace_back(ex->dots[rec], start);
+    const Cmd& c = ex->cmds[rec];
+    for (uint32_t key : c.keys) {
+      ex->to_clients.push_back(fx_executor_result{c.rifl, key, c.read_only});
+      if (ex->cfg.executor_monitor_execution_order && !c.read_only) ex->monitor[key].push_back(c.rifl);
+    }
+  }
+  ex->consumed = nexec;
+  return FX_OK;
+}
+
+int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys, uint32_t nkeys,
+           uint32_t read_only, const fx_dot* deps, uint32_t ndeps, uint64_t now_ms, uint32_t kind) {
+  if (!ex) return FX_ERR_INVALID_ARG;
+  if (ex->sticky) return ex->sticky;
+  if (ex->executor_index != 0) return FX_ERR_INVALID_ARG;  // mod.rs:220 assert_eq!(executor_index, 0)
+  if (dot.source < 1 || dot.source > ex->cfg.n || dot.seq < 1 || dot.seq > FX_SEQ_MASK) return FX_ERR_DOT_RANGE;
+  if (ndeps && !deps) return FX_ERR_INVALID_ARG;
+  if (nkeys && !keys) return FX_ERR_INVALID_ARG;
+  if (!ex->have_base) {
+    ex->have_base = true;
+    ex->t_base = now_ms;
+  }
+  if (now_ms < ex->t_base || now_ms - ex->t_base > 0x00FFFFFFull) return FX_ERR_TIME_RANGE;
+  std::vector<uint32_t> dv;
+  dv.reserve(ndeps);
+  for (uint32_t j = 0; j < ndeps; ++j) {
+    if (deps[j].source < 1 || deps[j].source > 255 || deps[j].seq < 1 || deps[j].seq > FX_SEQ_MASK)
+      return FX_ERR_DOT_RANGE;
+    dv.push_back(FX_PACK_DOT(deps[j].source, deps[j].seq));
+  }
+  std::sort(dv.begin(), dv.end());  // canonical C1 (executor.rs:76 iterates a HashSet)
+  dv.erase(std::unique(dv.begin(), dv.end()), dv.end());
+  if (dv.size() > kDmaxDev) return FX_ERR_INVALID_ARG;
+  if (ex->dots.size() + 1 >= (1u << 26)) return FX_ERR_INVALID_ARG;
+  Cmd c;
+  c.rifl = rifl;
+  c.keys.assign(keys, keys + nkeys);
+  std::sort(c.keys.begin(), c.keys.end());
+  c.keys.erase(std::unique(c.keys.begin(), c.keys.end()), c.keys.end());
+  c.read_only = read_only;
+  ex->dots.push_back(FX_PACK_DOT(dot.source, dot.seq));
+  ex->hdrs.push_back(FX_MAKE_HDR((uint32_t)(now_ms - ex->t_base), (uint32_t)dv.size(), kind));
+  ex->deps.push_back(std::move(dv));
+  ex->cmds.push_back(std::move(c));
+  return FX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+fx_graph_executor* fx_graph_executor_new(uint8_t process_id, uint64_t shard_id, const fx_config* config) {
+  if (!config || config->n < 1 || config->n > 8 || config->shard_count != 1) return nullptr;
+  if (fx_device_count() <= 0) return nullptr;  // no CPU fallback
+  auto* ex = new fx_graph_executor();
+  ex->process_id = process_id;
+  ex->shard_id = shard_id;
+  ex->cfg = *config;
+  if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ex;
+    return nullptr;
+  }
+  return ex;
+}
+
+void fx_graph_executor_free(fx_graph_executor* ex) {
+  if (!ex) return;
+  hipStream_t s = ex->stream;
+  delete ex;  // DevBufs free first
+  if (s) (void)hipStreamDestroy(s);
+}
+
+int fx_graph_executor_set_executor_index(fx_graph_executor* ex, uint32_t index) {
+  if (!ex) return FX_ERR_INVALID_ARG;
+  ex->executor_index = index;
+  return FX_OK;
+}
+
+int fx_graph_executor_handle_add(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys,
+                                 uint32_t nkeys, uint32_t read_only, const fx_dot* deps, uint32_t ndeps,
+                                 uint64_t now_ms) {
+  return append(ex, dot, rifl, keys, nkeys, read_only, deps, ndeps, now_ms, FX_KIND_ADD);
+}
+
+int fx_graph_executor_index_only(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys,
+                                 uint32_t nkeys, const fx_dot* deps, uint32_t ndeps, uint64_t now_ms) {
+  return append(ex, dot, rifl, keys, nkeys, 0, deps, ndeps, now_ms, FX_KIND_INDEX_ONLY);
+}
+
+int fx_graph_executor_set_executed_frontier(fx_graph_executor* ex, const uint64_t* frontier, uint32_t n) {
+  if (!ex || !frontier || n > 8 || n > ex->cfg.n) return FX_ERR_INVALID_ARG;
+  if (ex->processed > 0) return FX_ERR_INVALID_ARG;
+  for (uint32_t p = 0; p < n; ++p) {
+    if (frontier[p] > FX_SEQ_MASK) return FX_ERR_DOT_RANGE;
+    ex->init_frontier[p] = (uint32_t)frontier[p];
+  }
+  ex->use_frontier = true;
+  return FX_OK;
+}
+
+int fx_graph_executor_to_clients(fx_graph_executor* ex, fx_executor_result* out, uint32_t cap, uint32_t* n_out) {
+  if (!ex || (cap && !out) || !n_out) return FX_ERR_INVALID_ARG;
+  int st = flush(ex);
+  if (st) return st;
+  uint32_t c = 0;
+  while (c < cap && !ex->to_clients.empty()) {
+    out[c++] = ex->to_clients.front();
+    ex->to_clients.pop_front();
+  }
+  *n_out = c;
+  return FX_OK;
+}
+
+int fx_graph_executor_drain_dots(fx_graph_executor* ex, fx_dot* out, uint8_t* scc_start, uint32_t cap,
+                                 uint32_t* n_out) {
+  if (!ex || (cap && !out) || !n_out) return FX_ERR_INVALID_ARG;
+  int st = flush(ex);
+  if (st) return st;
+  uint32_t c = 0;
+  while (c < cap && !ex->executed.empty()) {
+    const auto e = ex->executed.front();
+    ex->executed.pop_front();
+    out[c] = fx_dot{FX_DOT_SRC(e.first), FX_DOT_SEQ(e.first)};
+    if (scc_start) scc_start[c] = e.second ? 1 : 0;
+    ++c;
+  }
+  *n_out = c;
+  return FX_OK;
+}
+
+int fx_graph_executor_metrics(fx_graph_executor* ex, uint32_t kind, uint64_t* values, uint64_t* counts,
+                              uint32_t cap, uint32_t* n_out) {
+  if (!ex || !n_out || kind > 1 || (cap && (!values || !counts))) return FX_ERR_INVALID_ARG;
+  int st = flush(ex);
+  if (st) return st;
+  const auto& h = kind == 0 ? ex->execution_delay : ex->chain_size;
+  uint32_t c = 0;
+  for (const auto& kv : h) {
+    if (c < cap) {
+      values[c] = kv.first;
+      counts[c] = kv.second;
+    }
+    ++c;
+  }
+  *n_out = c;
+  return FX_OK;
+}
+
+int fx_graph_executor_monitor(fx_graph_executor* ex, uint32_t key, fx_rifl* out, uint32_t cap, uint32_t* n_out) {
+  if (!ex || !n_out || (cap && !out)) return FX_ERR_INVALID_ARG;
+  if (!ex->cfg.executor_monitor_execution_order) return FX_ERR_INVALID_ARG;  // monitor() = None
+  int st = flush(ex);
+  if (st) return st;
+  auto it = ex->monitor.find(key);
+  uint32_t c = 0;
+  if (it != ex->monitor.end()) {
+    for (const auto& r : it->second) {
+      if (c < cap) out[c] = r;
+      ++c;
+    }
+  }
+  *n_out = c;
+  return FX_OK;
+}
+
+int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiting_on, uint32_t cap,
+                              uint32_t* n_out) {
+  if (!ex || !n_out || (cap && (!dots || !waiting_on))) return FX_ERR_INVALID_ARG;
+  int st = flush(ex);
+  if (st) return st;
+  *n_out = 0;
+  if (ex->processed == 0) return FX_OK;
+  fx_tier_info ti;
+  fx_tier_query(ex->tier, ex->cfg.n, &ti);
+  std::vector<uint32_t> block((size_t)ti.state_words * 64);
+  if (hipMemcpyAsync(block.data(), ex->d_state.p, block.size() * 4, hipMemcpyDeviceToHost, ex->stream) ||
+      hipStreamSynchronize(ex->stream))
+    return FX_ERR_HIP;
+  std::vector<uint32_t> d(64), w(64);
+  const uint32_t c = fx::decode_pending(ex->tier, block.data(), 0, d.data(), w.data(), 64);
+  std::vector<std::pair<uint32_t, uint32_t>> pw;
+  for (uint32_t i = 0; i < c && i < 64; ++i) pw.emplace_back(d[i], w[i]);
+  std::sort(pw.begin(), pw.end());
+  uint32_t m = 0;
+  for (const auto& e : pw) {
+    if (m < cap) {
+      dots[m] = fx_dot{FX_DOT_SRC(e.first), FX_DOT_SEQ(e.first)};
+      waiting_on[m] = fx_dot{FX_DOT_SRC(e.second), FX_DOT_SEQ(e.second)};
+    }
+    ++m;
+  }
+  *n_out = m;
+  return FX_OK;
+}
+
+int fx_graph_executor_parallel(void) { return 1; }
+
+// ------------------------------------------------------------ histogram
+// histogram.rs:172-235
+int fx_hist_stats_compute(const uint64_t* values, const uint64_t* counts, uint32_t n, fx_hist_stats* out) {
+  if (!out || (n && (!values || !counts))) return FX_ERR_INVALID_ARG;
+  uint64_t sum = 0, cnt = 0;
+  double mn = NAN, mx = NAN;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (i && values[i] <= values[i - 1]) return FX_ERR_INVALID_ARG;
+    if (!counts[i]) continue;
+    sum += values[i] * counts[i];
+    cnt += counts[i];
+    if (std::isnan(mn)) mn = (double)values[i];
+    mx = (double)values[i];
+  }
+  const double count = (double)cnt;
+  const double mean = (double)sum / count;
+  double var_acc = 0.0, dist_acc = 0.0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!counts[i]) continue;
+    const double x = (double)values[i], xc = (double)counts[i];
+    const double diff = mean - x;
+    var_acc += (diff * diff) * xc;
+    dist_acc += std::fabs(diff) * xc;
+  }
+  const double stddev = std::sqrt(var_acc / (count - 1.0));  // corrected (n - 1)
+  out->count = count;
+  out->mean = mean;
+  out->stddev = stddev;
+  out->cov = stddev / mean;
+  out->mdtm = dist_acc / count;
+  out->min = mn;
+  out->max = mx;
+  return FX_OK;
+}
+
+// histogram.rs:111-170
+int fx_hist_percentile(const uint64_t* values, const uint64_t* counts, uint32_t n, double p, double* out) {
+  if (!out || p < 0.0 || p > 1.0 || (n && (!values || !counts))) return FX_ERR_INVALID_ARG;
+  std::vector<std::pair<uint64_t, uint64_t>> data;
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (counts[i]) {
+      data.emplace_back(values[i], counts[i]);
+      total += counts[i];
+    }
+  if (data.empty()) {
+    *out = 0.0;
+    return FX_OK;
+  }
+  const double index = p * (double)total;
+  const double index_rounded = std::round(index);  // Rust f64::round: half away from zero
+  const bool whole = std::fabs(index - index_rounded) == 0.0;
+  uint64_t idx = (uint64_t)index_rounded;
+  size_t pos = 0;
+  double left = 0.0, right = 0.0;
+  bool have_right = false;
+  while (true) {
+    if (pos >= data.size()) return FX_ERR_INVALID_ARG;  // "there should a next histogram value"
+    const uint64_t value = data[pos].first, count = data[pos].second;
+    ++pos;
+    if (idx == count) {
+      left = (double)value;
+      if (pos < data.size()) {
+        right = (double)data[pos].first;
+        have_right = true;
+      }
+      break;
+    } else if (idx < count) {
+      left = (double)value;
+      right = left;
+      have_right = true;
+      break;
+    }
+    idx -= count;
+  }
+  if (whole) {
+    if (!have_right) return FX_ERR_INVALID_ARG;  // "there should be a right value"
+    *out = (left + right) / 2.0;
+  } else {
+    *out = left;
+  }
+  return FX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+"""`GraphExecutor`: the reference's Executor trait over the C-ABI (runs on the GPU).
+
+Mirrors fantoch_ps/src/executor/graph/executor.rs:31-114 (trait surface in
+fantoch/src/executor/mod.rs:27-89): `handle(Add)`, `to_clients()`,
+`to_clients_iter()`, `metrics()`, `monitor()`, `parallel()`.  Keys are u32
+ids (canonical C7); a reference panic is an FxError here.
+"""
+import ctypes
+
+from . import _lib
+from ._lib import CDot, CRifl, check
+
+EXECUTION_DELAY = 0
+CHAIN_SIZE = 1
+
+
+class GraphExecutor:
+    def __init__(self, process_id, shard_id, n, f=1, execute_at_commit=False, monitor=True):
+        lib = _lib.load()
+        cfg = _lib.Config(n, f, 1, 1 if execute_at_commit else 0, 1 if monitor else 0)
+        h = lib.fx_graph_executor_new(process_id, shard_id, ctypes.byref(cfg))
+        if not h:
+            raise _lib.FxError(_lib.FX_ERR_NO_DEVICE if lib.fx_device_count() <= 0
+                               else _lib.FX_ERR_INVALID_ARG, "fx_graph_executor_new")
+        self._h = h
+        self.n = n
+
+    def close(self):
+        if self._h:
+            _lib.load().fx_graph_executor_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def parallel():
+        return bool(_lib.load().fx_graph_executor_parallel())
+
+    def set_executor_index(self, index):
+        check(_lib.load().fx_graph_executor_set_executor_index(self._h, index))
+
+    def handle_add(self, dot, rifl, keys, deps, time_ms, read_only=False):
+        """handle(GraphExecutionInfo::Add{dot, cmd, deps}, time)."""
+        keys = list(keys)
+        karr = (ctypes.c_uint32 * max(len(keys), 1))(*keys)
+        deps = list(deps)
+        darr = (CDot * max(len(deps), 1))(*[CDot(int(s), int(q)) for s, q in deps])
+        check(_lib.load().fx_graph_executor_handle_add(
+            self._h, CDot(*dot), CRifl(*rifl), karr, len(keys), 1 if read_only else 0, darr,
+            len(deps), int(time_ms)), "handle_add")
+
+    def index_only(self, dot, rifl, keys, deps, time_ms=0):
+        keys = list(keys)
+        karr = (ctypes.c_uint32 * max(len(keys), 1))(*keys)
+        deps = list(deps)
+        darr = (CDot * max(len(deps), 1))(*[CDot(int(s), int(q)) for s, q in deps])
+        check(_lib.load().fx_graph_executor_index_only(
+            self._h, CDot(*dot), CRifl(*rifl), karr, len(keys), darr, len(deps), int(time_ms)),
+            "index_only")
+
+    def set_executed_frontier(self, frontier):
+        arr = (ctypes.c_uint64 * len(frontier))(*frontier)
+        check(_lib.load().fx_graph_executor_set_executed_frontier(self._h, arr, len(frontier)))
+
+    def to_clients_iter(self):
+        """Drains ExecutorResults: list of (rifl, key)."""
+        out = []
+        buf = (_lib.ExecutorResultC * 256)()
+        got = ctypes.c_uint32()
+        while True:
+            check(_lib.load().fx_graph_executor_to_clients(self._h, buf, 256, ctypes.byref(got)),
+                  "to_clients")
+            for i in range(got.value):
+                r = buf[i]
+                out.append(((r.rifl.source, r.rifl.seq), r.key))
+            if got.value < 256:
+                return out
+
+    def drain_dots(self):
+        """Executed dots in execution order: list of ((source, seq), scc_start)."""
+        out = []
+        buf = (CDot * 256)()
+        start = (ctypes.c_uint8 * 256)()
+        got = ctypes.c_uint32()
+        while True:
+            check(_lib.load().fx_graph_executor_drain_dots(self._h, buf, start, 256,
+                                                           ctypes.byref(got)), "drain_dots")
+            for i in range(got.value):
+                out.append(((buf[i].source, buf[i].seq), bool(start[i])))
+            if got.value < 256:
+                return out
+
+    def metrics(self, kind):
+        """{value: count} of ExecutionDelay (0) or ChainSize (1)."""
+        got = ctypes.c_uint32()
+        lib = _lib.load()
+        check(lib.fx_graph_executor_metrics(self._h, kind, None, None, 0, ctypes.byref(got)))
+        n = got.value
+        v = (ctypes.c_uint64 * max(n, 1))()
+        c = (ctypes.c_uint64 * max(n, 1))()
+        check(lib.fx_graph_executor_metrics(self._h, kind, v, c, n, ctypes.byref(got)))
+        return {int(v[i]): int(c[i]) for i in range(n)}
+
+    def monitor(self, key):
+        got = ctypes.c_uint32()
+        lib = _lib.load()
+        check(lib.fx_graph_executor_monitor(self._h, key, None, 0, ctypes.byref(got)))
+        n = got.value
+        buf = (CRifl * max(n, 1))()
+        check(lib.fx_graph_executor_monitor(self._h, key, buf, n, ctypes.byref(got)))
+        return [(buf[i].source, buf[i].seq) for i in range(n)]
+
+    def pending(self):
+        """[(dot, waiting_on)] of the pending vertices, ascending."""
+        buf = (CDot * 64)()
+        wb = (CDot * 64)()
+        got = ctypes.c_uint32()
+        check(_lib.load().fx_graph_executor_pending(self._h, buf, wb, 64, ctypes.byref(got)))
+        return [((buf[i].source, buf[i].seq), (wb[i].source, wb[i].seq))
+                for i in range(min(got.value, 64))]

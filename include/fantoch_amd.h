@@ -1,0 +1,303 @@
+/*
+ * fantoch_amd.h — C-ABI drop-in boundary of the MI355X-native GraphExecutor.
+ *
+ * The reference has no FFI: its boundary is the Rust trait
+ * `fantoch::executor::Executor` (fantoch/src/executor/mod.rs:27-89) implemented by
+ * `GraphExecutor` (fantoch_ps/src/executor/graph/executor.rs:31-114) on top of
+ * `DependencyGraph` (fantoch_ps/src/executor/graph/mod.rs:45-677).  Every entry
+ * point below names the reference item it replaces.  Plain pointers and sizes
+ * only; HIP streams are passed as `void*` (a `hipStream_t`); no torch types.
+ *
+ * Two surfaces:
+ *   1. fx_graph_executor_*  — one executor handle, the `Executor` trait 1:1
+ *      (handle -> to_clients -> metrics -> monitor).  Adds are buffered on the
+ *      host and executed on the GPU when results are pulled.
+ *   2. fx_batch_*           — thousands of independent commit streams (one per
+ *      (instance, process) executor) executed by one kernel launch; the form
+ *      the batched simulator and bench use.  Buffers are device pointers.
+ *
+ * Errors: the reference panics on invariant violations (mod.rs:220,234-237,258,
+ * 263; tarjan.rs:245,255).  Here every entry point returns an `int` status
+ * (FX_OK = 0); batched launches also fill a per-stream error word.
+ */
+#ifndef FANTOCH_AMD_H
+#define FANTOCH_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- status */
+#define FX_OK 0
+#define FX_ERR_INVALID_ARG 1   /* bad pointer/size/config                      */
+#define FX_ERR_CAPACITY 2      /* per-stream pending table / clock window full:
+                                  rerun the stream at a larger tier            */
+#define FX_ERR_DOUBLE_INDEX 3  /* mod.rs:233-237 "tried to index already indexed" */
+#define FX_ERR_DEPS_UNSORTED 4 /* deps plane not strictly ascending (canonical C1) */
+#define FX_ERR_DOT_RANGE 5     /* source 0 / > n, or seq >= 2^24               */
+#define FX_ERR_HIP 6           /* HIP runtime error (no device, launch failed) */
+#define FX_ERR_UNSUPPORTED 7   /* shard_count > 1 request/reply path (out of scope) */
+#define FX_ERR_ORDER_OVERFLOW 8/* more executions than order-plane rows        */
+#define FX_ERR_TIME_RANGE 9    /* t_ms >= 2^24 relative to the stream base     */
+#define FX_ERR_NO_DEVICE 10    /* no GPU visible: the product never falls back */
+
+/* ------------------------------------------------- packed stream format */
+/* A dot (fantoch/src/id.rs:21-27, Id<u8>{source, sequence}, derived Ord) is
+ * packed as (source << 24) | seq; the packed u32 orders exactly like the
+ * reference's (source, sequence) tuple. */
+#define FX_SEQ_BITS 24u
+#define FX_SEQ_MASK 0x00FFFFFFu
+#define FX_PACK_DOT(src, seq) ((((uint32_t)(src)) << FX_SEQ_BITS) | ((uint32_t)(seq) & FX_SEQ_MASK))
+#define FX_DOT_SRC(d) ((uint32_t)(d) >> FX_SEQ_BITS)
+#define FX_DOT_SEQ(d) ((uint32_t)(d) & FX_SEQ_MASK)
+
+/* Record header word: t_ms (24 bits) | ndeps (5 bits) | kind (3 bits). */
+#define FX_HDR_T(h) ((uint32_t)(h) & 0x00FFFFFFu)
+#define FX_HDR_ND(h) (((uint32_t)(h) >> 24) & 31u)
+#define FX_HDR_KIND(h) ((uint32_t)(h) >> 29)
+#define FX_MAKE_HDR(t, nd, kind) \
+  (((uint32_t)(t) & 0x00FFFFFFu) | (((uint32_t)(nd) & 31u) << 24) | (((uint32_t)(kind) & 7u) << 29))
+#define FX_KIND_ADD 0u        /* GraphExecutionInfo::Add -> handle_add (mod.rs:213-275) */
+#define FX_KIND_INDEX_ONLY 1u /* VertexIndex::index without a search (index.rs:33-37);
+                                 the hook the reference's sccs_found_and_missing_dep test uses */
+
+/* Order-plane word: arrival index of the executed command | SCC-start flag. */
+#define FX_ORDER_SCC_START 0x80000000u
+#define FX_ORDER_REC(o) ((uint32_t)(o) & 0x7FFFFFFFu)
+#define FX_RELEASE_NONE 0xFFFFFFFFu
+
+/* Batch flags */
+#define FX_FLAG_INIT 1u              /* start from an empty executor (else resume from state) */
+#define FX_FLAG_EXECUTE_AT_COMMIT 2u /* Config::execute_at_commit (executor.rs:72-73)    */
+#define FX_FLAG_SAVE_STATE 4u        /* write the executor state back for a later resume */
+
+/* Plane layout.  Every per-(step, stream) array ("plane") is tiled in tiles
+ * of 64 streams x 4 steps (1 KiB): element (step, stream) lives at
+ *   fx_index(step, stream, steps) =
+ *     ((stream / 64) * ceil(steps / 4) + step / 4) * 256 + (stream % 64) * 4 + step % 4
+ * so one 16-byte load per lane fetches 4 consecutive steps of that lane's
+ * stream and the 64 lanes of a wavefront (= 64 streams) read 1 KiB contiguous
+ * per plane per 4 steps.  A plane holds fx_plane_words(S, steps) u32 words
+ * (S rounded up to 64, steps to 4).  dep j of (step, stream) lives at
+ * deps[j * fx_plane_words(S, steps) + fx_index(step, stream, steps)]; the
+ * deps of one record are strictly ascending by packed dot (canonical C1,
+ * replacing the hash order of executor.rs:76). */
+#define FX_TILE_STREAMS 64u
+#define FX_TILE_STEPS 4u
+#if defined(__HIPCC__)
+#define FX_INLINE __host__ __device__ static inline
+#else
+#define FX_INLINE static inline
+#endif
+FX_INLINE size_t fx_plane_words(uint32_t num_streams, uint32_t steps) {
+  return (size_t)((num_streams + 63u) / 64u) * 64u * (size_t)((steps + 3u) / 4u) * 4u;
+}
+FX_INLINE size_t fx_index(uint32_t step, uint32_t stream, uint32_t steps) {
+  return ((size_t)(stream >> 6) * ((steps + 3u) >> 2) + (step >> 2)) * 256u +
+         ((stream & 63u) << 2) + (step & 3u);
+}
+typedef struct fx_stream_batch {
+  const uint32_t* dot;      /* plane: packed dot of the Add                */
+  const uint32_t* hdr;      /* plane: FX_MAKE_HDR(t_ms, ndeps, kind)       */
+  const uint32_t* deps;     /* dmax planes: packed dep dots, ascending     */
+  const uint32_t* lengths;  /* [S] valid steps per stream, or NULL = steps */
+  uint32_t num_streams;     /* S                                           */
+  uint32_t steps;           /* rows per plane                              */
+  uint32_t dmax;            /* number of dep planes                        */
+  uint32_t n;               /* processes per instance (sources 1..n)       */
+} fx_stream_batch;
+
+typedef struct fx_order_batch {
+  uint32_t* order;    /* plane, row k: k-th executed command: arrival index | SCC_START */
+  uint32_t* release;  /* plane, row a: step at which arrival a was executed, or NONE   */
+  uint32_t* nexec;    /* [S] number of executed commands                            */
+  uint32_t* err;      /* [S] FX_* status of the stream                              */
+} fx_order_batch;
+
+/* Dense histograms (fantoch/src/metrics/histogram.rs:14-59 keeps an exact
+ * BTreeMap; values here are small integers so a dense array is exact as long
+ * as every value < nbins; the last bin counts values >= nbins-1). */
+typedef struct fx_hist_batch {
+  uint64_t* chain_size;       /* ExecutorMetricsKind::ChainSize (mod.rs:492-493)      */
+  uint32_t nbins_chain;
+  uint64_t* execution_delay;  /* ExecutorMetricsKind::ExecutionDelay (mod.rs:514-518) */
+  uint32_t nbins_delay;
+} fx_hist_batch;
+
+/* Executor tiers: capacity of the per-stream pending table and of the
+ * executed-clock window above each source's frontier.  A stream that exceeds
+ * its tier stops with FX_ERR_CAPACITY and is rerun at the next tier. */
+#define FX_TIER_LDS_SMALL 0 /* LDS-resident state, occupancy-sized   */
+#define FX_TIER_LDS_LARGE 1 /* LDS-resident state, one wave per CU    */
+#define FX_TIER_GLOBAL 2    /* HBM-resident state, deep capacities    */
+#define FX_NUM_TIERS 3
+
+typedef struct fx_tier_info {
+  uint32_t max_sources;    /* n supported                                   */
+  uint32_t pending_cap;    /* vertices pending at once                       */
+  uint32_t window_bits;    /* executed-clock exceptions above the frontier  */
+  uint32_t state_words;    /* 32-bit state words per stream                  */
+} fx_tier_info;
+
+/* ---------------------------------------------------- batched executor */
+
+/* Capacity of a tier for n processes. Replaces nothing in the reference (its
+ * HashMap/DashMap indexes are unbounded, index.rs:18-51,145-208). */
+int fx_tier_query(uint32_t tier, uint32_t n, fx_tier_info* out);
+
+/* Bytes of resumable executor state for num_streams streams at a tier. */
+size_t fx_batch_state_bytes(uint32_t tier, uint32_t n, uint32_t num_streams);
+
+/* Run GraphExecutor::handle(Add) (executor.rs:69-93) for steps
+ * [step_begin, step_end) of every stream, i.e. DependencyGraph::handle_add
+ * (mod.rs:213-275) -> find_scc (409-486) -> TarjanSCCFinder::strong_connect
+ * (tarjan.rs:96-316) -> save_scc (488-523) -> index_pending/check_pending/
+ * try_pending (525-642), with canonical iteration C1 (deps ascending) and C2
+ * (waiters ascending).
+ *   stream_map: NULL, or [num_lanes] stream indices to run (tier reruns)
+ *   state:      device buffer of fx_batch_state_bytes(tier, n, num_lanes)
+ *               (NULL allowed with FX_FLAG_INIT and without FX_FLAG_SAVE_STATE)
+ *   init_frontier: NULL, or [num_streams][8] executed-clock frontiers to start
+ *               from (AboveExSet::from_events(1..=f), mod.rs:1309-1315),
+ *               indexed by stream (not lane)
+ * All pointers are device pointers; the call is asynchronous on hip_stream. */
+int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out,
+                     uint32_t tier, const uint32_t* stream_map, uint32_t num_lanes,
+                     void* state, uint32_t step_begin, uint32_t step_end,
+                     uint32_t flags, const uint32_t* init_frontier, void* hip_stream);
+
+/* Fold the executor metrics of a finished batch into dense histograms
+ * (Metrics::collect, fantoch/src/metrics/mod.rs:34-48): one ChainSize sample
+ * per SCC and one ExecutionDelay = t(release) - t(add) sample per executed
+ * command.  Histogram buffers are accumulated into (zero them first). */
+int fx_batch_metrics(const fx_stream_batch* in, const fx_order_batch* out,
+                     const fx_hist_batch* hists, void* hip_stream);
+
+/* Synchronous convenience driver: runs every stream at tier 0 and reruns the
+ * streams that report FX_ERR_CAPACITY at tiers 1 and 2.  Device pointers.
+ * Returns FX_OK when every stream finished with FX_OK. */
+int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out,
+                        uint32_t flags, void* hip_stream, uint32_t* tier_counts);
+
+/* --------------------------------------- synthetic Atlas/EPaxos streams */
+/* Commit streams of `instances` independent simulated instances; instance i
+ * has n processes, each coordinating cmds_per_process commands; conflict rate
+ * conflict_pct[i % num_conflicts] percent (fantoch/src/client/key_gen.rs:96-128
+ * semantics with a counter-based RNG, canonical C6); delivery order per process is a
+ * seeded windowed shuffle; concurrent same-key commands of the same round see
+ * each other with probability cycle_pct (2-/k-cycles). */
+typedef struct fx_synth_params {
+  uint64_t seed;
+  uint32_t instances;
+  uint32_t instance_base;    /* global index of the first instance (multi-GPU) */
+  uint32_t n;
+  uint32_t cmds_per_process;
+  uint32_t window;           /* delivery jitter window (generation units)   */
+  uint32_t cycle_pct;
+  uint32_t horizon;          /* rounds searched back for the latest conflict */
+  uint32_t num_conflicts;
+  uint32_t conflict_pct[8];
+} fx_synth_params;
+
+/* Planes of the synthetic batch: S = instances * n, steps = n * cmds, dmax = n. */
+int fx_synth_shape(const fx_synth_params* p, uint32_t* num_streams, uint32_t* steps, uint32_t* dmax);
+/* Generate into device planes (dot/hdr/deps of `out`, caller allocated). */
+int fx_synth_generate(const fx_synth_params* p, uint32_t* dot, uint32_t* hdr, uint32_t* deps, void* hip_stream);
+/* Same generator on the host (identical bytes). */
+int fx_synth_generate_host(const fx_synth_params* p, uint32_t* dot, uint32_t* hdr, uint32_t* deps);
+
+/* ---------------------------------------------- single executor handle */
+/* Config (fantoch/src/config.rs:5-45), the fields this path reads. */
+typedef struct fx_config {
+  uint32_t n;
+  uint32_t f;
+  uint32_t shard_count;                      /* must be 1 (partial replication out of scope) */
+  uint32_t execute_at_commit;                /* config.rs execute_at_commit  */
+  uint32_t executor_monitor_execution_order; /* config.rs: KVStore monitor (kvs.rs:29-39) */
+} fx_config;
+
+typedef struct fx_dot { uint32_t source; uint32_t seq; } fx_dot;       /* Dot  = Id<u8>  */
+typedef struct fx_rifl { uint64_t source; uint64_t seq; } fx_rifl;     /* Rifl = Id<u64> */
+
+/* ExecutorResult (fantoch/src/executor/mod.rs:169-174) with keys as u32 ids
+ * (canonical C7) and payloads dropped. */
+typedef struct fx_executor_result {
+  fx_rifl rifl;
+  uint32_t key;
+  uint32_t read_only;
+} fx_executor_result;
+
+typedef struct fx_graph_executor fx_graph_executor;
+
+/* Executor::new (executor.rs:34-51). NULL on bad config or no GPU. */
+fx_graph_executor* fx_graph_executor_new(uint8_t process_id, uint64_t shard_id, const fx_config* config);
+/* Drop. */
+void fx_graph_executor_free(fx_graph_executor* ex);
+/* Executor::set_executor_index (executor.rs:53-56); only index 0 handles Adds. */
+int fx_graph_executor_set_executor_index(fx_graph_executor* ex, uint32_t index);
+/* Executor::handle(GraphExecutionInfo::Add{dot, cmd, deps}) (executor.rs:69-80).
+ * keys: ids of the command's keys on this shard; deps in any order (the ABI
+ * canonicalises to ascending, C1, and drops duplicates); now_ms = SysTime::millis(). */
+int fx_graph_executor_handle_add(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl,
+                                 const uint32_t* keys, uint32_t nkeys, uint32_t read_only,
+                                 const fx_dot* deps, uint32_t ndeps, uint64_t now_ms);
+/* Test hook mirroring `queue.vertex_index.index(Vertex::new(..))` (mod.rs:1164-1306). */
+int fx_graph_executor_index_only(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl,
+                                 const uint32_t* keys, uint32_t nkeys,
+                                 const fx_dot* deps, uint32_t ndeps, uint64_t now_ms);
+/* Test hook mirroring `queue.executed_clock = AEClock::from(..)` (mod.rs:1309-1315):
+ * frontier[i] = highest contiguous executed seq of source i+1. Only before the first Add. */
+int fx_graph_executor_set_executed_frontier(fx_graph_executor* ex, const uint64_t* frontier, uint32_t n);
+/* Executor::to_clients (executor.rs:95-97): pops up to cap results in execution order. */
+int fx_graph_executor_to_clients(fx_graph_executor* ex, fx_executor_result* out, uint32_t cap, uint32_t* n_out);
+/* Execution order as dots (DependencyGraph::commands_to_execute in the tests, mod.rs:158-160):
+ * pops up to cap executed dots; scc_start[i] = 1 if out[i] opens a new SCC. */
+int fx_graph_executor_drain_dots(fx_graph_executor* ex, fx_dot* out, uint8_t* scc_start, uint32_t cap, uint32_t* n_out);
+/* Executor::metrics (executor.rs:107-109): histogram as (value, count) pairs
+ * sorted by value; kind 0 = ExecutionDelay, 1 = ChainSize.  Returns pair count in *n_out. */
+int fx_graph_executor_metrics(fx_graph_executor* ex, uint32_t kind, uint64_t* values,
+                              uint64_t* counts, uint32_t cap, uint32_t* n_out);
+/* Executor::monitor (executor.rs:111-113): the rifls executed on `key`, in order. */
+int fx_graph_executor_monitor(fx_graph_executor* ex, uint32_t key, fx_rifl* out, uint32_t cap, uint32_t* n_out);
+/* Pending vertices and the dot each waits on (0 source = none), ascending; debug/tests
+ * (VertexIndex::monitor_pending, index.rs:53-103, reports the same information). */
+int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiting_on, uint32_t cap, uint32_t* n_out);
+/* Executor::parallel (executor.rs:103-105). */
+int fx_graph_executor_parallel(void);
+
+/* ------------------------------------------------- histogram statistics */
+/* Histogram stats (histogram.rs:61-235) over (value, count) pairs sorted by value. */
+typedef struct fx_hist_stats {
+  double count, mean, stddev, cov, mdtm, min, max;
+} fx_hist_stats;
+int fx_hist_stats_compute(const uint64_t* values, const uint64_t* counts, uint32_t n, fx_hist_stats* out);
+/* Histogram::percentile (histogram.rs:111-170). */
+int fx_hist_percentile(const uint64_t* values, const uint64_t* counts, uint32_t n, double p, double* out);
+
+/* ------------------------------------------------------------- runtime */
+/* Number of visible GPUs; 0 means every compute entry point returns FX_ERR_NO_DEVICE. */
+int fx_device_count(void);
+/* Minimal device-memory plumbing for hosts without their own GPU runtime
+ * bindings (a Rust/cgo/ctypes caller); torch callers may pass their own
+ * device pointers and hipStream_t instead. */
+int fx_dev_alloc(void** ptr, size_t bytes);
+int fx_dev_free(void* ptr);
+int fx_dev_memset(void* ptr, int value, size_t bytes, void* hip_stream);
+int fx_dev_h2d(void* dst, const void* src, size_t bytes, void* hip_stream);
+int fx_dev_d2h(void* dst, const void* src, size_t bytes, void* hip_stream);
+int fx_dev_synchronize(void* hip_stream);
+/* Elapsed milliseconds of the last fx_batch_execute launch on hip_stream,
+ * measured with HIP events recorded on that stream around the kernel when
+ * fx_profile_enable(1) is set (bench roofline; 0 disables the events). */
+int fx_profile_enable(int on);
+int fx_profile_last_exec_ms(float* ms);
+const char* fx_status_string(int status);
+const char* fx_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FANTOCH_AMD_H */

@@ -1,0 +1,187 @@
+// fantoch_amd.hpp — C++ host mirror of the reference's executor surface over
+// the C-ABI (fantoch_amd.h).  Names, argument meaning and error behaviour
+// follow the Rust items (a panic there is an exception here):
+//   Dot / Rifl ............. fantoch/src/id.rs:7-27
+//   Config ................. fantoch/src/config.rs:5-102 (fields this path reads)
+//   Command ................ fantoch/src/command.rs:12-72 (keys as u32 ids, C7)
+//   Dependency ............. fantoch_ps/src/protocol/common/graph/deps/keys/mod.rs:18-35
+//   GraphExecutionInfo::add  fantoch_ps/src/executor/graph/executor.rs:197-218
+//   ExecutorResult ......... fantoch/src/executor/mod.rs:169-184
+//   GraphExecutor .......... fantoch_ps/src/executor/graph/executor.rs:19-114
+//                            (the `Executor` trait, fantoch/src/executor/mod.rs:27-89)
+#pragma once
+#include <cstdint>
+#include <map>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "fantoch_amd.h"
+
+namespace fantoch_amd {
+
+using ProcessId = uint8_t;
+using ShardId = uint64_t;
+using Key = uint32_t;
+
+struct Dot {
+  ProcessId source = 0;
+  uint64_t sequence = 0;
+  Dot() = default;
+  Dot(ProcessId s, uint64_t q) : source(s), sequence(q) {}
+  bool operator<(const Dot& o) const {
+    return source != o.source ? source < o.source : sequence < o.sequence;
+  }
+  bool operator==(const Dot& o) const { return source == o.source && sequence == o.sequence; }
+};
+
+struct Rifl {
+  uint64_t source = 0;
+  uint64_t sequence = 0;
+  Rifl() = default;
+  Rifl(uint64_t s, uint64_t q) : source(s), sequence(q) {}
+  bool operator==(const Rifl& o) const { return source == o.source && sequence == o.sequence; }
+  bool operator<(const Rifl& o) const {
+    return source != o.source ? source < o.source : sequence < o.sequence;
+  }
+};
+
+struct Config {
+  uint32_t n = 0, f = 0, shard_count = 1;
+  bool execute_at_commit = false;
+  bool executor_monitor_execution_order = false;
+  Config(uint32_t n_, uint32_t f_) : n(n_), f(f_) {}  // Config::new (config.rs:52-102)
+};
+
+struct Command {
+  Rifl rifl;
+  std::vector<Key> keys;
+  bool read_only = false;
+  // Command::from(rifl, [(key, op)]) with the payloads dropped (C7)
+  static Command from(Rifl r, std::vector<Key> ks, bool read_only = false) {
+    Command c;
+    c.rifl = r;
+    c.keys = std::move(ks);
+    c.read_only = read_only;
+    return c;
+  }
+};
+
+struct Dependency {
+  Dot dot;
+};
+
+struct GraphExecutionInfo {
+  Dot dot;
+  Command cmd;
+  std::vector<Dependency> deps;
+  static GraphExecutionInfo add(Dot d, Command c, std::vector<Dependency> deps) {
+    return GraphExecutionInfo{d, std::move(c), std::move(deps)};
+  }
+};
+
+struct ExecutorResult {
+  Rifl rifl;
+  Key key;
+};
+
+enum class ExecutorMetricsKind : uint32_t { ExecutionDelay = 0, ChainSize = 1 };
+
+class Error : public std::runtime_error {
+ public:
+  int status;
+  explicit Error(int s) : std::runtime_error(fx_status_string(s)), status(s) {}
+};
+
+inline void check(int s) {
+  if (s != FX_OK) throw Error(s);
+}
+
+class GraphExecutor {
+ public:
+  // Executor::new (executor.rs:34-51)
+  GraphExecutor(ProcessId process_id, ShardId shard_id, const Config& config) {
+    fx_config c{config.n, config.f, config.shard_count, config.execute_at_commit ? 1u : 0u,
+                config.executor_monitor_execution_order ? 1u : 0u};
+    h_ = fx_graph_executor_new(process_id, shard_id, &c);
+    if (!h_) throw Error(fx_device_count() <= 0 ? FX_ERR_NO_DEVICE : FX_ERR_INVALID_ARG);
+  }
+  GraphExecutor(const GraphExecutor&) = delete;
+  GraphExecutor& operator=(const GraphExecutor&) = delete;
+  ~GraphExecutor() { fx_graph_executor_free(h_); }
+
+  void set_executor_index(uint32_t index) { check(fx_graph_executor_set_executor_index(h_, index)); }
+
+  // Executor::handle (executor.rs:69-93); only Add exists with shard_count == 1
+  void handle(const GraphExecutionInfo& info, uint64_t time_ms) {
+    std::vector<fx_dot> deps;
+    for (const auto& d : info.deps) deps.push_back(fx_dot{d.dot.source, (uint32_t)d.dot.sequence});
+    check(fx_graph_executor_handle_add(h_, fx_dot{info.dot.source, (uint32_t)info.dot.sequence},
+                                       fx_rifl{info.cmd.rifl.source, info.cmd.rifl.sequence},
+                                       info.cmd.keys.data(), (uint32_t)info.cmd.keys.size(),
+                                       info.cmd.read_only ? 1u : 0u, deps.data(),
+                                       (uint32_t)deps.size(), time_ms));
+  }
+
+  // Executor::to_clients (executor.rs:95-97)
+  std::optional<ExecutorResult> to_clients() {
+    fx_executor_result r;
+    uint32_t got = 0;
+    check(fx_graph_executor_to_clients(h_, &r, 1, &got));
+    if (!got) return std::nullopt;
+    return ExecutorResult{Rifl(r.rifl.source, r.rifl.seq), r.key};
+  }
+
+  // Executor::to_clients_iter (mod.rs:58-60)
+  std::vector<ExecutorResult> to_clients_iter() {
+    std::vector<ExecutorResult> v;
+    while (auto r = to_clients()) v.push_back(*r);
+    return v;
+  }
+
+  // DependencyGraph::commands_to_execute as dots (mod.rs:158-160)
+  std::vector<std::pair<Dot, bool>> drain_dots() {
+    std::vector<std::pair<Dot, bool>> v;
+    fx_dot buf[256];
+    uint8_t start[256];
+    while (true) {
+      uint32_t got = 0;
+      check(fx_graph_executor_drain_dots(h_, buf, start, 256, &got));
+      for (uint32_t i = 0; i < got; ++i) v.emplace_back(Dot((ProcessId)buf[i].source, buf[i].seq), start[i] != 0);
+      if (got < 256) break;
+    }
+    return v;
+  }
+
+  static bool parallel() { return fx_graph_executor_parallel() != 0; }
+
+  // Executor::metrics (executor.rs:107-109): collected histogram of a kind
+  std::map<uint64_t, uint64_t> metrics(ExecutorMetricsKind kind) {
+    uint32_t n = 0;
+    check(fx_graph_executor_metrics(h_, (uint32_t)kind, nullptr, nullptr, 0, &n));
+    std::vector<uint64_t> v(n), c(n);
+    check(fx_graph_executor_metrics(h_, (uint32_t)kind, v.data(), c.data(), n, &n));
+    std::map<uint64_t, uint64_t> m;
+    for (uint32_t i = 0; i < n; ++i) m[v[i]] = c[i];
+    return m;
+  }
+
+  // Executor::monitor -> ExecutionOrderMonitor::get_order(key) (monitor.rs:44-46)
+  std::vector<Rifl> monitor_order(Key key) {
+    uint32_t n = 0;
+    check(fx_graph_executor_monitor(h_, key, nullptr, 0, &n));
+    std::vector<fx_rifl> r(n);
+    check(fx_graph_executor_monitor(h_, key, r.data(), n, &n));
+    std::vector<Rifl> out;
+    for (const auto& x : r) out.emplace_back(x.source, x.seq);
+    return out;
+  }
+
+  fx_graph_executor* raw() { return h_; }
+
+ private:
+  fx_graph_executor* h_ = nullptr;
+};
+
+}  // namespace fantoch_amd

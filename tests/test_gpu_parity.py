@@ -1,0 +1,275 @@
+"""Parity of the HIP path (through the C-ABI) with the CPU oracle.  GPU only.
+
+Integer/index work: everything is compared bit-exactly — the order plane
+(executed arrival index + SCC-start flag, row by row), the release plane,
+nexec and the per-stream status — on the same seeded inputs."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import kat_shapes as K
+from fantoch_amd import _lib
+from fantoch_amd import device as fd
+from fantoch_amd import streams as fs
+from fantoch_amd.executor import GraphExecutor, CHAIN_SIZE, EXECUTION_DELAY
+from oracle import oracle_lib
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def valid_rows(order, nexec, S, steps):
+    idx = []
+    for s in range(S):
+        idx.append(_lib.index(np.arange(int(nexec[s])), s, steps))
+    return np.concatenate(idx) if idx else np.zeros(0, np.int64)
+
+
+def release_rows(lengths, S, steps):
+    idx = []
+    for s in range(S):
+        L = steps if lengths is None else int(lengths[s])
+        idx.append(_lib.index(np.arange(L), s, steps))
+    return np.concatenate(idx) if idx else np.zeros(0, np.int64)
+
+
+def assert_parity(planes, res, execute_at_commit=False, init_frontier=None):
+    o_order, o_rel, o_nexec, o_err = oracle_lib.batch_execute(
+        planes, execute_at_commit=execute_at_commit, init_frontier=init_frontier, threads=8)
+    assert np.array_equal(res.err, o_err), (np.unique(res.err), np.unique(o_err))
+    assert np.array_equal(res.nexec, o_nexec)
+    rows = valid_rows(res.order, res.nexec, planes.S, planes.steps)
+    assert np.array_equal(res.order[rows], o_order[rows])
+    rrows = release_rows(planes.lengths, planes.S, planes.steps)
+    assert np.array_equal(res.release[rrows], o_rel[rrows])
+    return o_order, o_rel, o_nexec
+
+
+def oracle_hists(planes, order, release, nexec, nbc, nbd):
+    chain = np.zeros(nbc, np.uint64)
+    delay = np.zeros(nbd, np.uint64)
+    t = planes.hdr & 0xFFFFFF
+    for s in range(planes.S):
+        k = int(nexec[s])
+        if not k:
+            continue
+        o = order[_lib.index(np.arange(k), s, planes.steps)]
+        rec = (o & 0x7FFFFFFF).astype(np.int64)
+        start = (o & _lib.FX_ORDER_SCC_START) != 0
+        rel = release[_lib.index(rec, s, planes.steps)].astype(np.int64)
+        d = t[_lib.index(rel, s, planes.steps)].astype(np.int64) - t[_lib.index(rec, s, planes.steps)]
+        np.add.at(delay, np.minimum(d, nbd - 1), 1)
+        starts = np.flatnonzero(start)
+        sizes = np.diff(np.append(starts, k))
+        np.add.at(chain, np.minimum(sizes, nbc - 1), 1)
+    return chain, delay
+
+
+# ------------------------------------------------------------ synthetic
+SYNTH_CASES = [
+    dict(n=5, instances=40, cmds=200, window=8, cycle_pct=30),
+    dict(n=3, instances=64, cmds=150, window=6, cycle_pct=50),
+    dict(n=7, instances=20, cmds=120, window=8, cycle_pct=30),
+    dict(n=5, instances=16, cmds=100, window=0, cycle_pct=0),
+    dict(n=5, instances=16, cmds=300, window=24, cycle_pct=60),  # deep pending: tier reruns
+    dict(n=2, instances=33, cmds=77, window=5, cycle_pct=40),   # ragged tile (S % 64 != 0)
+]
+
+
+@pytest.mark.parametrize("case", SYNTH_CASES)
+def test_synthetic_parity(gpu, case):
+    p = fs.synth_params(seed=11, **case)
+    planes = fs.synth_host(p)
+    res = fd.run_batch(planes, nbins_chain=64, nbins_delay=2048)
+    o_order, o_rel, o_nexec = assert_parity(planes, res)
+    assert res.status == _lib.FX_OK
+    assert np.all(res.nexec == planes.steps)  # complete streams execute everything
+    chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 64, 2048)
+    assert np.array_equal(res.chain, chain)
+    assert np.array_equal(res.delay, delay)
+
+
+def test_tier_reruns_happen_and_match(gpu):
+    p = fs.synth_params(seed=5, n=5, instances=10, cmds=300, window=40, cycle_pct=70,
+                        conflicts=(100,))
+    planes = fs.synth_host(p)
+    res = fd.run_batch(planes)
+    assert res.tier_counts[1] > 0, res.tier_counts  # tier 0 overflowed and was rerun
+    assert_parity(planes, res)
+
+
+@pytest.mark.parametrize("tier", [0, 1, 2])
+def test_each_tier_standalone(gpu, tier):
+    p = fs.synth_params(seed=9, n=5, instances=20, cmds=150, window=6, cycle_pct=30)
+    planes = fs.synth_host(p)
+    res = fd.run_batch(planes, tiered=False, tier=tier)
+    assert_parity(planes, res)
+
+
+def test_device_generator_matches_host(gpu):
+    import ctypes
+    p = fs.synth_params(seed=123, n=5, instances=70, cmds=64, window=8, cycle_pct=30)
+    host = fs.synth_host(p)
+    lib = _lib.load()
+    bufs = [fd.DeviceBuffer(a.nbytes) for a in (host.dot, host.hdr, host.deps)]
+    _lib.check(lib.fx_synth_generate(ctypes.byref(p), bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, None))
+    for b, a in zip(bufs, (host.dot, host.hdr, host.deps)):
+        assert np.array_equal(b.download(np.uint32, a.size), a)
+
+
+def test_execute_at_commit(gpu):
+    p = fs.synth_params(seed=3, n=3, instances=8, cmds=50, window=8)
+    planes = fs.synth_host(p)
+    res = fd.run_batch(planes, execute_at_commit=True)
+    assert_parity(planes, res, execute_at_commit=True)
+
+
+def test_ragged_lengths_and_truncated_streams(gpu):
+    p = fs.synth_params(seed=21, n=5, instances=30, cmds=100, window=8, cycle_pct=30)
+    planes = fs.synth_host(p)
+    rng = np.random.default_rng(0)
+    planes.lengths = rng.integers(0, planes.steps + 1, planes.S).astype(np.uint32)
+    planes.lengths[0] = 0  # empty stream
+    res = fd.run_batch(planes)
+    assert_parity(planes, res)
+
+
+def test_chunked_resume_equals_one_shot(gpu):
+    import ctypes
+    p = fs.synth_params(seed=8, n=5, instances=30, cmds=100, window=10, cycle_pct=30)
+    planes = fs.synth_host(p)
+    one = fd.run_batch(planes, tiered=False, tier=0, metrics=False)
+    lib = _lib.load()
+    S, steps, pw = planes.S, planes.steps, planes.plane
+    d = [fd.DeviceBuffer(a.nbytes) for a in (planes.dot, planes.hdr, planes.deps)]
+    for b, a in zip(d, (planes.dot, planes.hdr, planes.deps)):
+        b.upload(a)
+    order, release = fd.DeviceBuffer(pw * 4), fd.DeviceBuffer(pw * 4)
+    nexec, err = fd.DeviceBuffer(S * 4), fd.DeviceBuffer(S * 4)
+    state = fd.DeviceBuffer(lib.fx_batch_state_bytes(0, 5, S))
+    inb = _lib.StreamBatch(d[0].ptr, d[1].ptr, d[2].ptr, None, S, steps, planes.dmax, 5)
+    outb = _lib.OrderBatch(order.ptr, release.ptr, nexec.ptr, err.ptr)
+    cuts = [0, 1, 7, 64, 65, 200, 333, steps]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        flags = _lib.FX_FLAG_SAVE_STATE | (_lib.FX_FLAG_INIT if a == 0 else 0)
+        _lib.check(lib.fx_batch_execute(ctypes.byref(inb), ctypes.byref(outb), 0, None, S, state.ptr,
+                                        a, b, flags, None, None))
+    ne = nexec.download(np.uint32, S)
+    assert np.array_equal(ne, one.nexec)
+    assert np.array_equal(err.download(np.uint32, S), one.err)
+    rows = valid_rows(None, ne, S, steps)
+    assert np.array_equal(order.download(np.uint32, pw)[rows], one.order[rows])
+    rrows = release_rows(None, S, steps)
+    assert np.array_equal(release.download(np.uint32, pw)[rrows], one.release[rrows])
+
+
+# ------------------------------------------- the reference's KATs as streams
+def kat_stream(args, t0=0):
+    return [(dot, sorted(deps), t0 + t) for t, (dot, _keys, deps) in enumerate(args)]
+
+
+def test_kat_permutations_as_one_batch(gpu):
+    import itertools
+    streams, n_of = [], []
+    for args in K.random_cases():
+        for perm in itertools.permutations(args):
+            streams.append(kat_stream(list(perm)))
+    for perm in itertools.permutations(K.CYCLE["args"]):
+        streams.append(kat_stream(list(perm)))
+    planes = fs.pack_streams(streams, 3)
+    res = fd.run_batch(planes)
+    assert_parity(planes, res)
+    assert np.all(res.nexec == planes.lengths)
+
+
+def test_sccs_found_and_missing_dep_batch(gpu):
+    f = K.SCCS_MISSING
+    stream = [(dot, deps, 0, _lib.FX_KIND_INDEX_ONLY) for dot, deps in f["indexed"]]
+    stream.append((f["root"][0], f["root"][1], 0))
+    planes = fs.pack_streams([stream], f["n"])
+    front = np.zeros((1, 8), np.uint32)
+    front[0, :5] = f["executed"]
+    res = fd.run_batch(planes, tiered=False, tier=0, init_frontier=front)
+    assert_parity(planes, res, init_frontier=front)
+    order = fs.decode_orders(res.order, res.nexec, 1, planes.steps)[0]
+    assert [rec for rec, _ in order] == list(range(10))  # (4,31)..(4,40)
+    assert all(start for _, start in order)
+
+
+# ------------------------------------- single executor (Executor trait)
+class GpuExec:
+    def __init__(self, n):
+        self.ex = GraphExecutor(1, 0, n, monitor=True)
+
+    def handle_add(self, dot, deps, t):
+        self.ex.handle_add(dot, dot, [0], deps, t)
+
+    def drain(self):
+        return [d for d, _ in self.ex.drain_dots()]
+
+
+def make_gpu(n):
+    return GpuExec(n)
+
+
+def test_executor_simple(gpu):
+    ex = GraphExecutor(1, 0, 2)
+    ex.handle_add((1, 1), (1, 1), [0], [(2, 1)], 0)
+    assert ex.drain_dots() == []
+    ex.handle_add((2, 1), (2, 1), [0], [(1, 1)], 0)
+    assert ex.drain_dots() == [((1, 1), True), ((2, 1), False)]
+
+
+def test_executor_cycle(gpu):
+    K.shuffle_it(make_gpu, K.CYCLE["n"], K.CYCLE["args"])
+
+
+def test_executor_regressions(gpu):
+    for case in (K.REGRESSION_1, K.REGRESSION_2):
+        # keys matter for regression 2: use the monitor path (per-key order)
+        def run(args):
+            ex = GraphExecutor(1, 0, case["n"], monitor=True)
+            ids = {"A": 1, "B": 2, K.CONF: 0}
+            for t, (dot, keys, deps) in enumerate(args):
+                ex.handle_add(dot, dot, [ids[k] for k in (keys or [K.CONF])], sorted(deps), t)
+            ex.to_clients_iter()
+            return {k: ex.monitor(k) for k in (0, 1, 2)}
+        assert run(case["order_a"]) != run(case["order_b"])
+
+
+def test_executor_sccs_found_and_missing_dep(gpu):
+    f = K.SCCS_MISSING
+    ex = GraphExecutor(f["process_id"], 0, f["n"])
+    ex.set_executed_frontier(f["executed"])
+    for dot, deps in f["indexed"]:
+        ex.index_only(dot, (1, 1), [0], deps)
+    ex.handle_add(f["root"][0], (1, 1), [0], f["root"][1], 0)
+    assert ex.drain_dots() == [((4, s), True) for s in range(31, 41)]
+    assert ex.pending() == [(f["root"][0], f["missing"][0])]
+
+
+def test_executor_metrics_and_results_match_oracle(gpu):
+    p = fs.synth_params(seed=4, n=3, instances=1, cmds=200, window=8, cycle_pct=40)
+    planes = fs.synth_host(p)
+    stream = planes.stream(1)
+    ex = GraphExecutor(2, 0, 3, monitor=True)
+    g = oracle_lib.Graph(2, 3)
+    for i, (dot, deps, t, _kind) in enumerate(stream):
+        ex.handle_add(dot, dot, [0 if i % 3 else 1], deps, 1_700_000_000_000 + t)
+        g.handle_add(dot, deps, t)
+        if i % 17 == 0:  # pull results mid-stream too (resume path)
+            ex.to_clients_iter()
+    got = [d for d, _ in ex.drain_dots()]
+    exp = [d for d, _, _ in g.drain()]
+    assert got == exp
+    assert ex.metrics(CHAIN_SIZE) == g.metrics(1)
+    assert ex.metrics(EXECUTION_DELAY) == g.metrics(0)
+
+
+def test_cpp_executor_tests(gpu):
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "test_graph_executor")
+    assert os.path.exists(exe), "build with `make`"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
