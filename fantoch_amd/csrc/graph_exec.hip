@@ -40,30 +40,35 @@ namespace fx {
 constexpr uint32_t WAVE = 64;
 constexpr uint32_t DCAP = 8;  // deps of the incoming Add held in registers
 
-template <uint32_t NSRC_, uint32_t P_, uint32_t XW_, bool GLOBAL_>
+template <uint32_t NSRC_, uint32_t P_, uint32_t XW_, uint32_t C_, bool GLOBAL_>
 struct Tier {
   static constexpr uint32_t NSRC = NSRC_;  // sources (processes) supported
   static constexpr uint32_t P = P_;        // pending-vertex slots (<= 64: u64 masks)
   static constexpr uint32_t XW = XW_;      // clock window words per source
+  static constexpr uint32_t C = C_;        // cached not-yet-executed deps per vertex
   static constexpr bool GLOBAL = GLOBAL_;  // state in HBM instead of LDS
+  static constexpr bool HINT = P <= 15;    // cached deps carry the dep's slot + 1
   static constexpr uint32_t CLKS = 1 + XW;
   static constexpr uint32_t CLK = 0;
-  static constexpr uint32_t DOT = CLK + NSRC * CLKS;  // packed dot, slot
-  static constexpr uint32_t REC = DOT + P;            // arrival index | nd << 26
+  static constexpr uint32_t DOT = CLK + NSRC * CLKS;  // packed dot, per slot
+  static constexpr uint32_t REC = DOT + P;            // arrival index | ncached << 26
   static constexpr uint32_t WAIT = REC + P;           // registered-on dot (0 = none)
   static constexpr uint32_t TL = WAIT + P;            // id:12 | low:12 | visited epoch:8
-  static constexpr uint32_t TS = TL + P;              // Tarjan stack, u8 slots
+  static constexpr uint32_t DEP = TL + P;             // [C][P] cached deps: dot | hint << 28
+  static constexpr uint32_t TS = DEP + C * P;         // Tarjan stack, u8 slots
   static constexpr uint32_t FR = TS + (P + 3) / 4;    // DFS frames, u16 slot | dep idx << 8
   static constexpr uint32_t WL = FR + (P + 1) / 2;    // worklist, P + 1 packed dots
   static constexpr uint32_t REG = WL + P + 1;         // words mirrored in LDS
   static constexpr uint32_t WORDS = REG + 6;          // + saved registers (global only)
   static_assert(P <= 64, "slot masks are u64");
   static_assert(P < 256, "slots are u8");
+  static_assert(C < 32, "ncached is 5 bits");
 };
 
-using Tier0 = Tier<8, 12, 1, false>;  // 22,016 B LDS / wave -> 7 waves / CU
-using Tier1 = Tier<8, 64, 4, false>;  // 104,704 B LDS / wave -> 1 wave / CU
-using Tier2 = Tier<8, 64, 32, true>;  // HBM-resident, 1024-bit clock windows
+// LDS bytes / wave: Tier0 37,376 -> 4 waves / CU; Tier1 123,136 -> 1 wave / CU.
+using Tier0 = Tier<8, 12, 1, 5, false>;
+using Tier1 = Tier<8, 32, 4, 8, false>;
+using Tier2 = Tier<8, 64, 32, 16, true>;  // HBM-resident, 1024-bit clock windows
 
 struct KArgs {
   const uint32_t* dot;
@@ -170,17 +175,30 @@ struct Exec {
     }
     return -1;
   }
-  __device__ __forceinline__ int pt_insert(uint32_t d, uint32_t rec, uint32_t nd) {
+  __device__ __forceinline__ int pt_insert(uint32_t d, uint32_t rec) {
     constexpr uint64_t full = T::P == 64 ? ~0ull : ((1ull << T::P) - 1ull);
     const uint64_t fre = ~occ & full;
     if (!fre) { err = FX_ERR_CAPACITY; return -1; }
     const int sl = __builtin_ctzll(fre);
     occ |= 1ull << sl;
     w(T::DOT + sl) = d;
-    w(T::REC + sl) = rec | (nd << 26);
+    w(T::REC + sl) = rec;
     w(T::WAIT + sl) = 0;
     w(T::TL + sl) = 0;
     return sl;
+  }
+  // Vertex::deps restricted to the deps not executed at insertion (executed
+  // deps are ignored by every later search, tarjan.rs:128-145, and the
+  // executed clock only grows), ascending; a dep pending at insertion carries
+  // its slot (it can only leave that slot by being executed).
+  __device__ __forceinline__ void pt_cache_dep(int sl, uint32_t d, uint32_t dep, uint32_t& nc) {
+    if (dep == d || clk_contains(dep)) return;
+    if ((dep >> FX_SEQ_BITS) > 15u) { err = FX_ERR_DOT_RANGE; return; }
+    if (nc >= T::C) { err = FX_ERR_CAPACITY; return; }
+    uint32_t hint = 0;
+    if constexpr (T::HINT) hint = (uint32_t)(pt_find(dep) + 1);
+    w(T::DEP + nc * T::P + sl) = dep | (hint << 28);
+    ++nc;
   }
   __device__ __forceinline__ void pt_free(int sl) {
     const uint64_t keep = ~(1ull << sl);
@@ -219,14 +237,19 @@ struct Exec {
     while (nfr > 0) {
       const uint32_t f = fr(nfr - 1);
       const uint32_t v = f & 0xFFu, di = f >> 8;
-      const uint32_t rw = w(T::REC + v);
-      const uint32_t nd = rw >> 26, rec = rw & 0x03FFFFFFu;
+      const uint32_t nd = w(T::REC + v) >> 26;
       if (di < nd) {
         fr(nfr - 1) = (uint16_t)(v | ((di + 1) << 8));
-        const uint32_t dep = deps[(size_t)di * plane + at(rec)];
-        // ignore self or already executed (tarjan.rs:128-145)
-        if (dep == w(T::DOT + v) || clk_contains(dep)) continue;
-        const int x = pt_find(dep);
+        const uint32_t cw = w(T::DEP + di * T::P + v);
+        const uint32_t dep = cw & 0x0FFFFFFFu;
+        // ignore self or already executed (tarjan.rs:128-145); self was dropped at insertion
+        if (clk_contains(dep)) continue;
+        int x = -1;
+        if constexpr (T::HINT) {
+          const uint32_t h = cw >> 28;
+          if (h && w(T::DOT + h - 1) == dep) x = (int)h - 1;
+        }
+        if (x < 0) x = pt_find(dep);
         if (x < 0) {  // missing: give up (tarjan.rs:148-157, shard_count == 1)
           missing = dep;
           break;
@@ -264,6 +287,7 @@ struct Exec {
             const uint32_t sl = ts(a);
             const uint32_t d = w(T::DOT + sl);
             emit(w(T::REC + sl) & 0x03FFFFFFu, d, a == pos);
+            if (err) return 0;
             wl(nwl++) = d;
             pt_free((int)sl);
           }
@@ -333,6 +357,21 @@ struct Exec {
     }
   }
 
+  // VertexIndex::index(Vertex::new(dot, cmd, deps, time)) (index.rs:33-37):
+  // deps j < DCAP come from the prefetched registers, the rest from HBM.
+  __device__ __forceinline__ int insert_vertex(uint32_t i, uint32_t d, uint32_t nd, const uint4* rdeps) {
+    const int sl = pt_insert(d, i);
+    if (sl < 0) return -1;
+    uint32_t nc = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < DCAP; ++j)
+      if (j < nd) pt_cache_dep(sl, d, rdeps[j].x, nc);
+    for (uint32_t j = DCAP; j < nd; ++j) pt_cache_dep(sl, d, deps[(size_t)j * plane + at(i)], nc);
+    if (err) return -1;
+    w(T::REC + sl) = i | (nc << 26);
+    return sl;
+  }
+
   // GraphExecutor::handle(Add) (executor.rs:69-80) -> handle_add (mod.rs:213-275)
   __device__ __forceinline__ void handle(uint32_t i, uint32_t d, uint32_t h, const uint4* rdeps,
                                          bool at_commit) {
@@ -348,7 +387,7 @@ struct Exec {
     }
     if (occ && pt_find(d) >= 0) { err = FX_ERR_DOUBLE_INDEX; return; }  // mod.rs:233-237
     if (kind == FX_KIND_INDEX_ONLY) {
-      pt_insert(d, i, nd);
+      insert_vertex(i, d, nd, rdeps);
       return;
     }
     // Fast path: every dep is self or executed -> strong_connect visits only
@@ -371,7 +410,7 @@ struct Exec {
       if (!wmask || err) return;
       wl(nwl++) = d;
     } else {
-      const int sl = pt_insert(d, i, nd);
+      const int sl = insert_vertex(i, d, nd, rdeps);
       if (sl < 0) return;
       bool em;
       const uint32_t miss = find_scc(sl, false, em);
@@ -423,7 +462,7 @@ __global__ __launch_bounds__(64) void k_graph_exec(KArgs a) {
     e.err = r[5 * WAVE] & 0xFFFFu;
     e.epoch = r[5 * WAVE] >> 16;
   }
-  if (!active) e.err = FX_ERR_INVALID_ARG;
+  if (!active) e.err = FX_ERR_INVALID_ARG;  // idle lane (its loads read stream 0)
 
   const bool at_commit = (a.flags & FX_FLAG_EXECUTE_AT_COMMIT) != 0;
   const uint32_t steps4 = (a.steps + 3) >> 2;
@@ -432,47 +471,31 @@ __global__ __launch_bounds__(64) void k_graph_exec(KArgs a) {
   const uint32_t b_end = (a.step_end + 3) >> 2;
   const uint32_t dmax = a.dmax;
 
+  // Prefetch: every block issues the same 2 + DCAP 16-byte loads per lane
+  // (addresses clamped instead of branched around), so the compiler's
+  // s_waitcnt for a block's data is a precise vmcnt(N) and never waits for
+  // the next block's loads or for this block's scattered stores.
   const uint32_t* dotp = a.dot + lane_off;
   const uint32_t* hdrp = a.hdr + lane_off;
-  const uint32_t* depp = a.deps + lane_off;
-  const size_t plane = a.plane;
-  const uint4 zero4 = make_uint4(0, 0, 0, 0);
-#define FX_LOAD_A(B, D, H)                                                        \
-  do {                                                                            \
-    const uint32_t bb_ = (B);                                                     \
-    if (active && bb_ < b_end) {                                                  \
-      D = *reinterpret_cast<const uint4*>(dotp + (size_t)bb_ * 256);              \
-      H = *reinterpret_cast<const uint4*>(hdrp + (size_t)bb_ * 256);              \
-    } else {                                                                      \
-      D = zero4;                                                                  \
-      H = zero4;                                                                  \
-    }                                                                             \
-  } while (0)
-#define FX_LOAD_D(B, H, DP)                                                                  \
+  const uint32_t* depp = (dmax ? a.deps : a.dot) + lane_off;
+  const size_t plane = dmax ? a.plane : 0;
+  const uint32_t jlast = dmax ? dmax - 1 : 0;
+  const uint32_t b_last = b_end ? b_end - 1 : 0;
+#define FX_LOAD(B, D, H, DP)                                                                 \
   do {                                                                                       \
-    const uint32_t bb_ = (B);                                                                \
-    uint32_t mx_ = max(max(hdr_nd((H).x), hdr_nd((H).y)), max(hdr_nd((H).z), hdr_nd((H).w))); \
-    if (!(active && bb_ < b_end)) mx_ = 0;                                                   \
-    _Pragma("unroll") for (uint32_t j = 0; j < DCAP; ++j) {                                   \
-      if (j < dmax && j < mx_)                                                               \
-        DP[j] = *reinterpret_cast<const uint4*>(depp + (size_t)j * plane + (size_t)bb_ * 256); \
-    }                                                                                        \
+    const size_t off_ = (size_t)min((B), b_last) * 256;                                      \
+    D = *reinterpret_cast<const uint4*>(dotp + off_);                                        \
+    H = *reinterpret_cast<const uint4*>(hdrp + off_);                                        \
+    _Pragma("unroll") for (uint32_t j = 0; j < DCAP; ++j)                                    \
+      DP[j] = *reinterpret_cast<const uint4*>(depp + (size_t)min(j, jlast) * plane + off_); \
   } while (0)
 
-  uint4 a0d, a0h, a1d, a1h, a2d, a2h;
+  uint4 cd, ch, nd_, nh;
   uint4 d0[DCAP], d1[DCAP];
-#pragma unroll
-  for (uint32_t j = 0; j < DCAP; ++j) {
-    d0[j] = zero4;
-    d1[j] = zero4;
-  }
-  FX_LOAD_A(b_begin, a0d, a0h);
-  FX_LOAD_A(b_begin + 1, a1d, a1h);
-  FX_LOAD_D(b_begin, a0h, d0);
+  if (b_begin < b_end) FX_LOAD(b_begin, cd, ch, d0);
 
   for (uint32_t b = b_begin; b < b_end; ++b) {
-    FX_LOAD_A(b + 2, a2d, a2h);
-    FX_LOAD_D(b + 1, a1h, d1);
+    FX_LOAD(b + 1, nd_, nh, d1);
     const uint32_t base = b * 4;
     const uint32_t q0 = base < a.step_begin ? a.step_begin - base : 0u;
     const uint32_t q1 = a.step_end - base < 4u ? a.step_end - base : 4u;
@@ -480,22 +503,18 @@ __global__ __launch_bounds__(64) void k_graph_exec(KArgs a) {
     // iteration so every register index stays static (no scratch).
     for (uint32_t q = 0; q < q1; ++q) {
       const uint32_t i = base + q;
-      if (q >= q0 && !e.err && i < len) e.handle(i, a0d.x, a0h.x, d0, at_commit);
-      a0d = make_uint4(a0d.y, a0d.z, a0d.w, 0u);
-      a0h = make_uint4(a0h.y, a0h.z, a0h.w, 0u);
+      if (q >= q0 && !e.err && i < len) e.handle(i, cd.x, ch.x, d0, at_commit);
+      cd = make_uint4(cd.y, cd.z, cd.w, 0u);
+      ch = make_uint4(ch.y, ch.z, ch.w, 0u);
 #pragma unroll
-      for (uint32_t j = 0; j < DCAP; ++j)
-        if (j < dmax) d0[j] = make_uint4(d0[j].y, d0[j].z, d0[j].w, 0u);
+      for (uint32_t j = 0; j < DCAP; ++j) d0[j] = make_uint4(d0[j].y, d0[j].z, d0[j].w, 0u);
     }
-    a0d = a1d;
-    a0h = a1h;
-    a1d = a2d;
-    a1h = a2h;
+    cd = nd_;
+    ch = nh;
 #pragma unroll
     for (uint32_t j = 0; j < DCAP; ++j) d0[j] = d1[j];
   }
-#undef FX_LOAD_A
-#undef FX_LOAD_D
+#undef FX_LOAD
 
   if (!active) return;
   // Vertices still pending have no release step (yet).

@@ -112,7 +112,9 @@ typedef struct fx_stream_batch {
 
 typedef struct fx_order_batch {
   uint32_t* order;    /* plane, row k: k-th executed command: arrival index | SCC_START */
-  uint32_t* release;  /* plane, row a: step at which arrival a was executed, or NONE   */
+  uint32_t* release;  /* plane, row a: step at which arrival a was executed, or NONE;
+                         rows of arrivals a stream did not process (err != 0, or
+                         beyond its length) are left untouched                 */
   uint32_t* nexec;    /* [S] number of executed commands                            */
   uint32_t* err;      /* [S] FX_* status of the stream                              */
 } fx_order_batch;

@@ -157,11 +157,16 @@ def test_chunked_resume_equals_one_shot(gpu):
         _lib.check(lib.fx_batch_execute(ctypes.byref(inb), ctypes.byref(outb), 0, None, S, state.ptr,
                                         a, b, flags, None, None))
     ne = nexec.download(np.uint32, S)
+    er = err.download(np.uint32, S)
     assert np.array_equal(ne, one.nexec)
-    assert np.array_equal(err.download(np.uint32, S), one.err)
+    assert np.array_equal(er, one.err)
     rows = valid_rows(None, ne, S, steps)
     assert np.array_equal(order.download(np.uint32, pw)[rows], one.order[rows])
-    rrows = release_rows(None, S, steps)
+    # release rows are defined for the arrivals a stream processed; a stream
+    # that stopped at the tier-0 capacity leaves the rest undefined
+    ok = np.flatnonzero(er == 0)
+    assert len(ok) > S // 2
+    rrows = np.concatenate([_lib.index(np.arange(steps), s, steps) for s in ok])
     assert np.array_equal(release.download(np.uint32, pw)[rrows], one.release[rrows])
 
 
