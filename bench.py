@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--window", type=int, default=8)
     ap.add_argument("--cycle-pct", type=int, default=30)
     ap.add_argument("--seed", type=int, default=20250213)
+    ap.add_argument("--conflict-block", type=int, default=-1,
+                    help="instances per conflict rate block (-1 = --seeds: conflict-major "
+                         "enumeration, so a wavefront's streams share a rate; 0 = seed-major)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", type=str, default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -70,9 +73,10 @@ def main():
 
     conflicts = [int(c) for c in args.conflicts.split(",")]
     instances = args.seeds * len(conflicts)
+    cblock = args.seeds if args.conflict_block < 0 else args.conflict_block
     p = fs.synth_params(seed=args.seed, instances=instances, n=args.n, cmds=args.cmds,
                         window=args.window, cycle_pct=args.cycle_pct, conflicts=conflicts,
-                        instance_base=rank * instances)
+                        instance_base=rank * instances, conflict_block=cblock)
     S, steps, dmax = fs.synth_shape(p)
     pw = _lib.plane_words(S, steps)
     stream = torch.cuda.current_stream(dev)
@@ -210,6 +214,8 @@ def main():
                             "(BASELINE configs[1])" % (args.n, args.seeds, args.conflicts, args.cmds),
                 "instances_per_gpu": instances, "streams_per_gpu": S, "adds_per_stream": steps,
                 "window": args.window, "cycle_pct": args.cycle_pct, "seed": args.seed,
+                "instance_order": "conflict-major (%d instances per rate)" % cblock if cblock
+                                  else "seed-major",
                 "parallelism": "instances sharded over %d GPU(s), one wavefront lane per stream" % world,
             },
             "edges_per_s": round(edges, 1),
@@ -227,8 +233,9 @@ def main():
 
 
 def workload_key(args):
-    return "n%d_s%d_c%s_m%d_w%d_y%d_seed%d" % (args.n, args.seeds, args.conflicts.replace(",", "-"),
-                                              args.cmds, args.window, args.cycle_pct, args.seed)
+    return "n%d_s%d_c%s_m%d_w%d_y%d_seed%d_b%d" % (
+        args.n, args.seeds, args.conflicts.replace(",", "-"), args.cmds, args.window,
+        args.cycle_pct, args.seed, args.conflict_block)
 
 
 def cpu_baseline(args, lib, dot, hdr, deps, order, release, nexec, S, steps, dmax, pw):

@@ -191,7 +191,7 @@ int flush(fx_graph_executor* ex) {
         hipMemcpyAsync(&err, ex->d_err.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipStreamSynchronize(ex->stream))
       return ex->sticky = FX_ERR_HIP;
-    if (err == FX_ERR_CAPACITY && ex->tier + 1 < FX_NUM_TIERS) {
+    if (err == FX_ERR_CAPACITY && ex->tier < FX_TIER_GLOBAL) {
       // rerun the whole log one tier up; the already-consumed prefix of the
       // (deterministic) order is skipped below
       ex->tier += 1;
@@ -412,9 +412,7 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
   if (st) return st;
   *n_out = 0;
   if (ex->processed == 0) return FX_OK;
-  fx_tier_info ti;
-  fx_tier_query(ex->tier, ex->cfg.n, &ti);
-  std::vector<uint32_t> block((size_t)ti.state_words * 64);
+  std::vector<uint32_t> block(fx_batch_state_bytes(ex->tier, ex->cfg.n, 1) / 4);
   if (hipMemcpyAsync(block.data(), ex->d_state.p, block.size() * 4, hipMemcpyDeviceToHost, ex->stream) ||
       hipStreamSynchronize(ex->stream))
     return FX_ERR_HIP;

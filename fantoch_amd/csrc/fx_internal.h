@@ -1,8 +1,42 @@
-// fx_internal.h — declarations shared between the kernel TU and the host TU.
+// fx_internal.h — declarations shared by the kernel and host translation units.
 #pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 namespace fx {
+
+// Arguments of one executor launch (fx_batch_execute).
+struct KArgs {
+  const uint32_t* dot;
+  const uint32_t* hdr;
+  const uint32_t* deps;
+  const uint32_t* lengths;
+  uint32_t S, steps, dmax, n;
+  size_t plane;
+  uint32_t* order;
+  uint32_t* release;
+  uint32_t* nexec;
+  uint32_t* err;
+  const uint32_t* stream_map;
+  uint32_t num_lanes;
+  uint32_t* state;
+  uint32_t step_begin, step_end, flags;
+  const uint32_t* init_frontier;
+};
+
+// Lane-per-stream executor tiers (graph_exec.hip) and the 16-lanes-per-stream
+// group tier (graph_group.hip).
+int launch_group(const KArgs& a, hipStream_t stream);
+size_t group_state_bytes(uint32_t streams);
+uint32_t group_state_words_per_stream();
+uint32_t group_decode_pending(const uint32_t* block, uint32_t stream_in_block, uint32_t* dots,
+                              uint32_t* waits, uint32_t cap);
+constexpr uint32_t GROUP_LANES = 16;        // lanes per stream in the group tier
+constexpr uint32_t GROUP_SLOTS = 16;        // pending vertices per stream
+constexpr uint32_t GROUP_CACHE = 8;         // cached deps per pending vertex
+constexpr uint32_t GROUP_WINDOW_BITS = 32;  // executed-clock window per source
+
 // Decodes the pending vertices of lane `lane` from a saved state block
 // (tier layout of graph_exec.hip).  Writes up to cap (dot, waiting_on) pairs;
 // returns the count.

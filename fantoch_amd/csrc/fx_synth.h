@@ -63,8 +63,9 @@ FX_HD SynthInstance synth_instance(const fx_synth_params& p, uint32_t local) {
   si.window = p.window;
   si.cycle_pct = p.cycle_pct;
   si.horizon = p.horizon;
-  uint32_t nc = p.num_conflicts ? p.num_conflicts : 1;
-  si.conflict = p.conflict_pct[si.inst % nc];
+  const uint32_t nc = p.num_conflicts ? p.num_conflicts : 1;
+  const uint32_t ci = p.conflict_block ? (si.inst / p.conflict_block) % nc : si.inst % nc;
+  si.conflict = p.conflict_pct[ci];
   return si;
 }
 

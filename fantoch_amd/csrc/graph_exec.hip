@@ -6,29 +6,38 @@
 // independent executors; there is no inter-lane communication, so nothing
 // here depends on dispatch order or XCD placement.
 //
-// Per-lane executor state lives in LDS in a lane-interleaved layout: state
-// word w of lane l is at LDS dword (w * 64 + l), so whatever slot index each
-// lane touches, the bank is (l mod 32) and every ds_read/ds_write_b32 is
-// conflict-free.  The state restates the reference's containers as fixed
-// tables:
+// State restates the reference's containers as fixed tables (SURVEY §8(a)
+// rows a4-a10):
 //   executed clock AEClock (threshold 0.9.1; tarjan.rs:131-132,293):
-//     per source a u32 frontier + a XW-word bitmap of executed seqs above it
-//   VertexIndex (index.rs:18-51):  P pending-vertex slots {dot, rec|nd, wait, tarjan}
+//     per source a u32 frontier + an XW-word bitmap of executed seqs above it
+//   VertexIndex (index.rs:18-51): P pending-vertex slots {dot, rec, wait,
+//     tarjan id/low/visited-epoch, cached deps}
 //   PendingIndex (index.rs:145-208): slot.wait = the missing dot the vertex is
 //     registered on (a vertex is registered on at most one dot at a time)
 //   TarjanSCCFinder (tarjan.rs:25-33): explicit DFS frame stack + Tarjan stack
 //   check_pending's `dots` (mod.rs:556-587): LIFO worklist
-// plus per-lane bitmasks in VGPRs: occupied slots, registered waiters, and the
-// try_pending snapshot.  A stream whose pending set or clock window outgrows
-// its tier stops with FX_ERR_CAPACITY and is rerun at the next tier.
+// Tier 0 keeps the small hot fields (clock, slot dots/waits/recs) in VGPRs
+// (unrolled selects, so a lookup is P parallel compares) and the rest in LDS
+// in a lane-interleaved layout: word w of lane l at LDS dword (w * 64 + l),
+// so whatever slot a lane touches the bank is (l mod 32) — conflict-free.
+// Larger tiers keep everything in LDS (tier 1) or HBM (tier 2).
 //
-// Records stream through a 3-block register pipeline (a block = 4 steps = one
-// 16-byte load per lane per plane, see fx_index in fantoch_amd.h).
+// Divergence: the slow path (Tarjan search, check_pending, try_pending) is a
+// flat state machine — every iteration each lane performs ONE micro-op (one
+// DFS edge or frame pop, one waiter pick, one worklist pop) — so a wavefront's
+// cost per Add is the max over its lanes of their micro-op counts instead of
+// the product of nested divergent loop trip counts.
+//
+// Records stream through a double-buffered register pipeline (a block = 4
+// steps = one 16-byte load per lane per plane, see fx_index in fantoch_amd.h)
+// whose loads have a static count, so waits are precise vmcnt(N).  Within a
+// block lanes advance through their 4 steps independently.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "fantoch_amd.h"
@@ -38,68 +47,90 @@
 namespace fx {
 
 constexpr uint32_t WAVE = 64;
-constexpr uint32_t DCAP = 8;  // deps of the incoming Add held in registers
 
-template <uint32_t NSRC_, uint32_t P_, uint32_t XW_, uint32_t C_, bool GLOBAL_>
+template <uint32_t NSRC_, uint32_t P_, uint32_t XW_, uint32_t C_, bool GLOBAL_, bool REGS_>
 struct Tier {
   static constexpr uint32_t NSRC = NSRC_;  // sources (processes) supported
-  static constexpr uint32_t P = P_;        // pending-vertex slots (<= 64: u64 masks)
+  static constexpr uint32_t P = P_;        // pending-vertex slots
   static constexpr uint32_t XW = XW_;      // clock window words per source
   static constexpr uint32_t C = C_;        // cached not-yet-executed deps per vertex
   static constexpr bool GLOBAL = GLOBAL_;  // state in HBM instead of LDS
-  static constexpr bool HINT = P <= 15;    // cached deps carry the dep's slot + 1
+  static constexpr bool REGS = REGS_;      // clock + slot dot/wait/rec in VGPRs
+  static constexpr bool SMALL = P <= 15;   // u16 tarjan words, slot hints in cached deps
+  using Mask = typename std::conditional<(P <= 32), uint32_t, uint64_t>::type;
+  // memory-resident words per lane (register-resident fields are absent)
   static constexpr uint32_t CLKS = 1 + XW;
   static constexpr uint32_t CLK = 0;
-  static constexpr uint32_t DOT = CLK + NSRC * CLKS;  // packed dot, per slot
-  static constexpr uint32_t REC = DOT + P;            // arrival index | ncached << 26
-  static constexpr uint32_t WAIT = REC + P;           // registered-on dot (0 = none)
-  static constexpr uint32_t TL = WAIT + P;            // id:12 | low:12 | visited epoch:8
-  static constexpr uint32_t DEP = TL + P;             // [C][P] cached deps: dot | hint << 28
-  static constexpr uint32_t TS = DEP + C * P;         // Tarjan stack, u8 slots
-  static constexpr uint32_t FR = TS + (P + 3) / 4;    // DFS frames, u16 slot | dep idx << 8
-  static constexpr uint32_t WL = FR + (P + 1) / 2;    // worklist, P + 1 packed dots
-  static constexpr uint32_t REG = WL + P + 1;         // words mirrored in LDS
-  static constexpr uint32_t WORDS = REG + 6;          // + saved registers (global only)
-  static_assert(P <= 64, "slot masks are u64");
+  static constexpr uint32_t DOT = CLK + (REGS ? 0 : NSRC * CLKS);
+  static constexpr uint32_t WAIT = DOT + (REGS ? 0 : P);
+  static constexpr uint32_t REC = WAIT + (REGS ? 0 : P);  // arrival index | ncached << 26
+  static constexpr uint32_t TL = REC + (REGS ? 0 : P);    // tarjan id | low | visited epoch
+  static constexpr uint32_t DEP = TL + (SMALL ? (P + 1) / 2 : P);  // [C][P] dot | hint << 28
+  static constexpr uint32_t TS = DEP + C * P;        // Tarjan stack, u8 slots
+  static constexpr uint32_t FR = TS + (P + 3) / 4;   // DFS parent frames, u16 slot | dep idx << 8
+  static constexpr uint32_t WL = FR + (P + 1) / 2;   // worklist, P + 1 packed dots
+  static constexpr uint32_t MEM = WL + P + 1;        // words in LDS (or HBM)
+  static constexpr uint32_t RSAVE = REGS ? 2 * NSRC + 3 * P : 0;  // saved VGPR arrays
+  static constexpr uint32_t WORDS = MEM + RSAVE + 6;  // + occ(2) wmask(2) k err|epoch
+  static_assert(P <= 64, "slot masks are at most u64");
   static_assert(P < 256, "slots are u8");
   static_assert(C < 32, "ncached is 5 bits");
+  static_assert(!REGS || (XW == 1 && SMALL), "register tier: 32-bit windows, <= 15 slots");
 };
 
-// LDS bytes / wave: Tier0 37,376 -> 4 waves / CU; Tier1 123,136 -> 1 wave / CU.
-using Tier0 = Tier<8, 12, 1, 5, false>;
-using Tier1 = Tier<8, 32, 4, 8, false>;
-using Tier2 = Tier<8, 64, 32, 16, true>;  // HBM-resident, 1024-bit clock windows
+// Lane-per-stream tiers (tier 0 is the 16-lanes-per-stream group tier,
+// graph_group.hip).  LDS bytes / wave: TierLane 35,840 -> 4 waves / CU;
+// Tier1 123,136 -> 1 wave / CU.
+using TierLane = Tier<8, 12, 1, 5, false, false>;
+using Tier1 = Tier<8, 32, 4, 8, false, false>;
+using Tier2 = Tier<8, 64, 32, 16, true, false>;  // HBM-resident, 1024-bit clock windows
 
-struct KArgs {
-  const uint32_t* dot;
-  const uint32_t* hdr;
-  const uint32_t* deps;
-  const uint32_t* lengths;
-  uint32_t S, steps, dmax, n;
-  size_t plane;
-  uint32_t* order;
-  uint32_t* release;
-  uint32_t* nexec;
-  uint32_t* err;
-  const uint32_t* stream_map;
-  uint32_t num_lanes;
-  uint32_t* state;
-  uint32_t step_begin, step_end, flags;
-  const uint32_t* init_frontier;
-};
 
 __device__ __forceinline__ uint32_t hdr_nd(uint32_t h) { return (h >> 24) & 31u; }
 
-template <class T>
+// Register arrays indexed by a per-lane value.  Arithmetic masks instead of
+// selects: LLVM folds `i == k ? a[k] : r` chains back into a dynamically
+// indexed load, which demotes the whole array (and the executor) to scratch.
+__device__ __forceinline__ uint32_t lmask(bool c) { return 0u - (uint32_t)c; }
+template <uint32_t N>
+__device__ __forceinline__ uint32_t rsel(const uint32_t (&a)[N], uint32_t i) {
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < N; ++k) r |= a[k] & lmask(i == k);
+  return r;
+}
+template <uint32_t N>
+__device__ __forceinline__ void rput(uint32_t (&a)[N], uint32_t i, uint32_t v) {
+#pragma unroll
+  for (uint32_t k = 0; k < N; ++k) {
+    const uint32_t m = lmask(i == k);
+    a[k] = (v & m) | (a[k] & ~m);
+  }
+}
+
+enum : uint32_t { PH_IDLE = 0, PH_DFS = 1, PH_TRY = 2, PH_CHECK = 3 };
+
+template <class T, uint32_t DCAP>
 struct Exec {
-  uint32_t* st;  // this lane's state: word w at st[w * WAVE]
-  uint64_t occ = 0, wmask = 0, tmask = 0;
+  using Mask = typename T::Mask;
+  static constexpr uint32_t RN = T::REGS ? T::NSRC : 1;
+  static constexpr uint32_t RP = T::REGS ? T::P : 1;
+  static constexpr Mask ONE = 1;
+
+  uint32_t* st;  // this lane's memory state: word w at st[w * WAVE]
+  uint32_t cf[RN], cw[RN];           // clock frontier / window (REGS)
+  uint32_t sd[RP], sw[RP], sr[RP];   // slot dot / wait / rec (REGS)
+  Mask occ = 0, wmask = 0, tmask = 0;
   uint32_t k = 0, err = 0, epoch = 1, nwl = 0, cur = 0;
   uint32_t stream = 0, n = 0, steps = 0, dmax = 0;
   size_t plane = 0;
   const uint32_t* deps = nullptr;
   uint32_t* order = nullptr;
   uint32_t* release = nullptr;
+  // find_scc context
+  uint32_t phase = PH_IDLE, root = 0, idc = 0, nts = 0, nfr = 0, missing = 0;
+  uint32_t fv = 0, fdi = 0, fnc = 0;
+  bool in_try = false, emitted = false;
 
   __device__ __forceinline__ uint32_t& w(uint32_t i) { return st[i * WAVE]; }
   __device__ __forceinline__ uint8_t& ts(uint32_t i) {
@@ -111,41 +142,109 @@ struct Exec {
   __device__ __forceinline__ uint32_t& wl(uint32_t i) { return w(T::WL + i); }
   __device__ __forceinline__ size_t at(uint32_t step) const { return fx_index(step, stream, steps); }
 
+  // ------------------------------------------------------- slot fields
+  __device__ __forceinline__ uint32_t dot_of(uint32_t sl) {
+    if constexpr (T::REGS) return rsel(sd, sl); else return w(T::DOT + sl);
+  }
+  __device__ __forceinline__ void set_dot(uint32_t sl, uint32_t v) {
+    if constexpr (T::REGS) rput(sd, sl, v); else w(T::DOT + sl) = v;
+  }
+  __device__ __forceinline__ uint32_t wait_of(uint32_t sl) {
+    if constexpr (T::REGS) return rsel(sw, sl); else return w(T::WAIT + sl);
+  }
+  __device__ __forceinline__ void set_wait(uint32_t sl, uint32_t v) {
+    if constexpr (T::REGS) rput(sw, sl, v); else w(T::WAIT + sl) = v;
+  }
+  __device__ __forceinline__ uint32_t rec_of(uint32_t sl) {
+    if constexpr (T::REGS) return rsel(sr, sl); else return w(T::REC + sl);
+  }
+  __device__ __forceinline__ void set_rec(uint32_t sl, uint32_t v) {
+    if constexpr (T::REGS) rput(sr, sl, v); else w(T::REC + sl) = v;
+  }
+  // Tarjan word: id | low | visited epoch (u16 4|4|8 on small tiers, u32 12|12|8)
+  static constexpr uint32_t IDB = T::SMALL ? 4 : 12;
+  static constexpr uint32_t IDM = (1u << IDB) - 1;
+  __device__ __forceinline__ uint32_t tl_of(uint32_t sl) {
+    if constexpr (T::SMALL) return reinterpret_cast<uint16_t*>(&w(T::TL + (sl >> 1)))[sl & 1];
+    else return w(T::TL + sl);
+  }
+  __device__ __forceinline__ void set_tl(uint32_t sl, uint32_t v) {
+    if constexpr (T::SMALL) reinterpret_cast<uint16_t*>(&w(T::TL + (sl >> 1)))[sl & 1] = (uint16_t)v;
+    else w(T::TL + sl) = v;
+  }
+  static __device__ __forceinline__ uint32_t tid(uint32_t t) { return t & IDM; }
+  static __device__ __forceinline__ uint32_t tlow(uint32_t t) { return (t >> IDB) & IDM; }
+  static __device__ __forceinline__ uint32_t tep(uint32_t t) { return t >> (2 * IDB); }
+  static __device__ __forceinline__ uint32_t tmk(uint32_t id, uint32_t low, uint32_t ep) {
+    return id | (low << IDB) | (ep << (2 * IDB));
+  }
+
   // ---------------------------------------------- executed clock (AEClock)
   // AEClock::contains (tarjan.rs:131-132)
   __device__ __forceinline__ bool clk_contains(uint32_t d) {
     const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
     if (si >= n) return false;
     const uint32_t seq = d & FX_SEQ_MASK;
-    const uint32_t b = T::CLK + si * T::CLKS;
-    const uint32_t f = w(b);
-    if (seq <= f) return true;
-    const uint32_t off = seq - f - 1u;
-    if (off >= 32u * T::XW) return false;
-    return (w(b + 1 + (off >> 5)) >> (off & 31u)) & 1u;
+    if constexpr (T::REGS) {
+      uint32_t f = 0, wv = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < T::NSRC; ++q) {
+        const uint32_t m = lmask(si == q);
+        f |= cf[q] & m;
+        wv |= cw[q] & m;
+      }
+      const uint32_t off = seq - f - 1u;
+      return seq <= f || (off < 32u && ((wv >> off) & 1u));
+    } else {
+      const uint32_t b = T::CLK + si * T::CLKS;
+      const uint32_t f = w(b);
+      if (seq <= f) return true;
+      const uint32_t off = seq - f - 1u;
+      if (off >= 32u * T::XW) return false;
+      return (w(b + 1 + (off >> 5)) >> (off & 31u)) & 1u;
+    }
   }
   // AEClock::add (tarjan.rs:293): frontier + exception window
   __device__ __forceinline__ void clk_add(uint32_t d) {
     const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
     if (si >= n) { err = FX_ERR_DOT_RANGE; return; }
     const uint32_t seq = d & FX_SEQ_MASK;
-    const uint32_t b = T::CLK + si * T::CLKS;
-    const uint32_t f = w(b);
-    if (seq <= f) return;
-    const uint32_t off = seq - f - 1u;
-    if (off >= 32u * T::XW) { err = FX_ERR_CAPACITY; return; }
-    if (off != 0) {
-      w(b + 1 + (off >> 5)) |= 1u << (off & 31u);
-      return;
-    }
-    if constexpr (T::XW == 1) {
-      const uint32_t win = w(b + 1) >> 1;          // bit j <-> seq f + 2 + j
-      const uint32_t ones = __builtin_ctz(~win);   // top bit of win is 0 -> <= 31
-      w(b) = f + 1 + ones;
-      w(b + 1) = win >> ones;
+    if constexpr (T::REGS) {
+      uint32_t f = 0, wv = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < T::NSRC; ++q) {
+        const uint32_t m = lmask(si == q);
+        f |= cf[q] & m;
+        wv |= cw[q] & m;
+      }
+      if (seq <= f) return;
+      const uint32_t off = seq - f - 1u;
+      if (off >= 32u) { err = FX_ERR_CAPACITY; return; }
+      if (off != 0) {
+        wv |= 1u << off;
+      } else {
+        const uint32_t win = wv >> 1;               // bit j <-> seq f + 2 + j
+        const uint32_t ones = __builtin_ctz(~win);  // top bit of win is 0 -> <= 31
+        f = f + 1 + ones;
+        wv = win >> ones;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < T::NSRC; ++q) {
+        const uint32_t m = lmask(si == q);
+        cf[q] = (f & m) | (cf[q] & ~m);
+        cw[q] = (wv & m) | (cw[q] & ~m);
+      }
     } else {
-      // t = 1 + trailing ones of the window from bit 1
-      uint32_t t = 1;
+      const uint32_t b = T::CLK + si * T::CLKS;
+      const uint32_t f = w(b);
+      if (seq <= f) return;
+      const uint32_t off = seq - f - 1u;
+      if (off >= 32u * T::XW) { err = FX_ERR_CAPACITY; return; }
+      if (off != 0) {
+        w(b + 1 + (off >> 5)) |= 1u << (off & 31u);
+        return;
+      }
+      uint32_t t = 1;  // 1 + trailing ones of the window from bit 1
       while (t < 32u * T::XW) {
         const uint32_t word = w(b + 1 + (t >> 5)) >> (t & 31u);
         const uint32_t avail = 32u - (t & 31u);
@@ -169,49 +268,110 @@ struct Exec {
 
   // ----------------------------------------------- VertexIndex slot table
   __device__ __forceinline__ int pt_find(uint32_t d) {
-    for (uint64_t m = occ; m; m &= m - 1) {
-      const int sl = __builtin_ctzll(m);
-      if (w(T::DOT + sl) == d) return sl;
+    if constexpr (T::REGS) {
+      Mask m = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < T::P; ++q) m |= (Mask)(sd[q] == d) << q;
+      m &= occ;
+      return m ? (int)__builtin_ctzll((uint64_t)m) : -1;
+    } else {
+      for (Mask m = occ; m; m &= m - 1) {
+        const int sl = __builtin_ctzll((uint64_t)m);
+        if (w(T::DOT + sl) == d) return sl;
+      }
+      return -1;
     }
-    return -1;
+  }
+  // registered waiters of x: PendingIndex::remove(x) (index.rs:205-207)
+  __device__ __forceinline__ Mask waiters(uint32_t x) {
+    Mask t = 0;
+    if constexpr (T::REGS) {
+#pragma unroll
+      for (uint32_t q = 0; q < T::P; ++q) t |= (Mask)(sw[q] == x) << q;
+      return t & wmask;
+    } else {
+      for (Mask m = wmask; m; m &= m - 1) {
+        const int sl = __builtin_ctzll((uint64_t)m);
+        if (w(T::WAIT + sl) == x) t |= ONE << sl;
+      }
+      return t;
+    }
+  }
+  // slot with the smallest dot among `m` (canonical C2 order)
+  __device__ __forceinline__ int argmin_dot(Mask m) {
+    int best = -1;
+    uint32_t bd = 0xFFFFFFFFu;
+    if constexpr (T::REGS) {
+#pragma unroll
+      for (uint32_t q = 0; q < T::P; ++q) {
+        const uint32_t tk = lmask(((m >> q) & 1) && sd[q] < bd);
+        bd = (sd[q] & tk) | (bd & ~tk);
+        best = (int)((q & tk) | ((uint32_t)best & ~tk));
+      }
+    } else {
+      for (; m; m &= m - 1) {
+        const int sl = __builtin_ctzll((uint64_t)m);
+        const uint32_t dd = w(T::DOT + sl);
+        if (dd < bd) { bd = dd; best = sl; }
+      }
+    }
+    return best;
   }
   __device__ __forceinline__ int pt_insert(uint32_t d, uint32_t rec) {
-    constexpr uint64_t full = T::P == 64 ? ~0ull : ((1ull << T::P) - 1ull);
-    const uint64_t fre = ~occ & full;
+    constexpr Mask full = T::P == 8 * sizeof(Mask) ? ~(Mask)0 : ((ONE << T::P) - 1);
+    const Mask fre = ~occ & full;
     if (!fre) { err = FX_ERR_CAPACITY; return -1; }
-    const int sl = __builtin_ctzll(fre);
-    occ |= 1ull << sl;
-    w(T::DOT + sl) = d;
-    w(T::REC + sl) = rec;
-    w(T::WAIT + sl) = 0;
-    w(T::TL + sl) = 0;
-    return sl;
+    const uint32_t sl = __builtin_ctzll((uint64_t)fre);
+    occ |= ONE << sl;
+    set_dot(sl, d);
+    set_rec(sl, rec);
+    set_wait(sl, 0);
+    set_tl(sl, 0);
+    return (int)sl;
+  }
+  __device__ __forceinline__ void pt_free(uint32_t sl) {
+    const Mask keep = ~(ONE << sl);
+    occ &= keep;
+    wmask &= keep;
+    tmask &= keep;
   }
   // Vertex::deps restricted to the deps not executed at insertion (executed
   // deps are ignored by every later search, tarjan.rs:128-145, and the
   // executed clock only grows), ascending; a dep pending at insertion carries
-  // its slot (it can only leave that slot by being executed).
-  __device__ __forceinline__ void pt_cache_dep(int sl, uint32_t d, uint32_t dep, uint32_t& nc) {
+  // its slot + 1 (it can only leave that slot by being executed).
+  __device__ __forceinline__ void pt_cache_dep(uint32_t sl, uint32_t d, uint32_t dep, uint32_t& nc) {
     if (dep == d || clk_contains(dep)) return;
     if ((dep >> FX_SEQ_BITS) > 15u) { err = FX_ERR_DOT_RANGE; return; }
     if (nc >= T::C) { err = FX_ERR_CAPACITY; return; }
     uint32_t hint = 0;
-    if constexpr (T::HINT) hint = (uint32_t)(pt_find(dep) + 1);
+    if constexpr (T::SMALL) hint = (uint32_t)(pt_find(dep) + 1);
     w(T::DEP + nc * T::P + sl) = dep | (hint << 28);
     ++nc;
   }
-  __device__ __forceinline__ void pt_free(int sl) {
-    const uint64_t keep = ~(1ull << sl);
-    occ &= keep;
-    wmask &= keep;
-    tmask &= keep;
+  // VertexIndex::index(Vertex::new(dot, cmd, deps, time)) (index.rs:33-37):
+  // deps j < DCAP come from the prefetched registers, the rest from HBM.
+  __device__ __forceinline__ int insert_vertex(uint32_t i, uint32_t d, uint32_t nd, const uint32_t* rdeps) {
+    const int sl = pt_insert(d, i);
+    if (sl < 0) return -1;
+    uint32_t nc = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < DCAP; ++j)
+      if (j < nd) pt_cache_dep((uint32_t)sl, d, rdeps[j], nc);
+    for (uint32_t j = DCAP; j < nd; ++j) pt_cache_dep((uint32_t)sl, d, deps[(size_t)j * plane + at(i)], nc);
+    if (err) return -1;
+    set_rec((uint32_t)sl, i | (nc << 26));
+    return sl;
   }
 
   // try_pending's `visited` set (mod.rs:598): an epoch stamp per slot
   __device__ __forceinline__ void new_epoch() {
     epoch = (epoch + 1) & 0xFFu;
     if (epoch == 0) {
-      for (uint64_t m = occ; m; m &= m - 1) w(T::TL + __builtin_ctzll(m)) &= 0x00FFFFFFu;
+      for (Mask m = occ; m; m &= m - 1) {
+        const uint32_t sl = __builtin_ctzll((uint64_t)m);
+        const uint32_t t = tl_of(sl);
+        set_tl(sl, tmk(tid(t), tlow(t), 0));
+      }
       epoch = 1;
     }
   }
@@ -225,157 +385,161 @@ struct Exec {
     clk_add(d);
   }
 
-  // find_scc (mod.rs:409-486) + TarjanSCCFinder::strong_connect
-  // (tarjan.rs:96-316) + finalize (tarjan.rs:60-93), iterative.  Returns the
-  // missing dep (0 = Found).  `emitted` = an SCC was saved by this search.
-  __device__ __forceinline__ uint32_t find_scc(int root, bool in_try, bool& emitted) {
-    uint32_t idc = 1, nts = 0, nfr = 0, missing = 0;
+  // ------------------------------ find_scc as a micro-op state machine
+  // find_scc (mod.rs:409-486) = TarjanSCCFinder::strong_connect
+  // (tarjan.rs:96-316) run iteratively + save_scc + finalize (tarjan.rs:60-93)
+  __device__ __forceinline__ void dfs_start(uint32_t r, bool intry) {
+    root = r;
+    in_try = intry;
     emitted = false;
-    w(T::TL + root) = (w(T::TL + root) & 0xFF000000u) | 1u | (1u << 12);
-    ts(nts++) = (uint8_t)root;
-    fr(nfr++) = (uint16_t)root;
-    while (nfr > 0) {
-      const uint32_t f = fr(nfr - 1);
-      const uint32_t v = f & 0xFFu, di = f >> 8;
-      const uint32_t nd = w(T::REC + v) >> 26;
-      if (di < nd) {
-        fr(nfr - 1) = (uint16_t)(v | ((di + 1) << 8));
-        const uint32_t cw = w(T::DEP + di * T::P + v);
-        const uint32_t dep = cw & 0x0FFFFFFFu;
-        // ignore self or already executed (tarjan.rs:128-145); self was dropped at insertion
-        if (clk_contains(dep)) continue;
-        int x = -1;
-        if constexpr (T::HINT) {
-          const uint32_t h = cw >> 28;
-          if (h && w(T::DOT + h - 1) == dep) x = (int)h - 1;
-        }
-        if (x < 0) x = pt_find(dep);
-        if (x < 0) {  // missing: give up (tarjan.rs:148-157, shard_count == 1)
-          missing = dep;
-          break;
-        }
-        const uint32_t tx = w(T::TL + x);
-        if ((tx & 0xFFFu) == 0) {  // not visited: recurse (tarjan.rs:172-214)
-          ++idc;
-          w(T::TL + x) = (tx & 0xFF000000u) | idc | (idc << 12);
-          ts(nts++) = (uint8_t)x;
-          fr(nfr++) = (uint16_t)x;
-        } else {  // visited and on the stack (tarjan.rs:215-225)
-          const uint32_t tv = w(T::TL + v);
-          const uint32_t idx = tx & 0xFFFu;
-          if (idx < ((tv >> 12) & 0xFFFu)) w(T::TL + v) = (tv & 0xFF000FFFu) | (idx << 12);
-        }
-      } else {
-        --nfr;
-        const uint32_t tv = w(T::TL + v);
-        const uint32_t lowv = (tv >> 12) & 0xFFFu;
-        if ((tv & 0xFFFu) == lowv) {  // SCC root (tarjan.rs:233-312)
-          uint32_t pos = nts - 1;
-          while (ts(pos) != v) --pos;
-          // members ascending by dot (SCC = BTreeSet<Dot>, tarjan.rs:15)
-          for (uint32_t a = pos + 1; a < nts; ++a) {
-            const uint8_t key = ts(a);
-            const uint32_t kd = w(T::DOT + key);
-            uint32_t b = a;
-            while (b > pos && w(T::DOT + ts(b - 1)) > kd) {
-              ts(b) = ts(b - 1);
-              --b;
-            }
-            ts(b) = key;
-          }
-          for (uint32_t a = pos; a < nts; ++a) {
-            const uint32_t sl = ts(a);
-            const uint32_t d = w(T::DOT + sl);
-            emit(w(T::REC + sl) & 0x03FFFFFFu, d, a == pos);
-            if (err) return 0;
-            wl(nwl++) = d;
-            pt_free((int)sl);
-          }
-          nts = pos;
-          emitted = true;
-          if (err) return 0;
-        }
-        if (nfr > 0) {  // low = min(low, dep.low) after the recursion (tarjan.rs:211)
-          const uint32_t p = fr(nfr - 1) & 0xFFu;
-          const uint32_t tp = w(T::TL + p);
-          if (lowv < ((tp >> 12) & 0xFFFu)) w(T::TL + p) = (tp & 0xFF000FFFu) | (lowv << 12);
-        }
+    missing = 0;
+    idc = 1;
+    set_tl(r, tmk(1, 1, tep(tl_of(r))));
+    ts(0) = (uint8_t)r;
+    nts = 1;
+    nfr = 0;
+    fv = r;
+    fdi = 0;
+    fnc = rec_of(r) >> 26;
+    phase = PH_DFS;
+  }
+
+  // SCC rooted at fv: members are TS[pos..nts), saved in ascending dot order
+  // (SCC = BTreeSet<Dot>, tarjan.rs:15); executed clock updated per member.
+  __device__ __forceinline__ void save_scc() {
+    uint32_t pos = nts - 1;
+    while (ts(pos) != fv) --pos;
+    for (uint32_t a = pos + 1; a < nts; ++a) {
+      const uint8_t key = ts(a);
+      const uint32_t kd = dot_of(key);
+      uint32_t b = a;
+      while (b > pos && dot_of(ts(b - 1)) > kd) {
+        ts(b) = ts(b - 1);
+        --b;
       }
+      ts(b) = key;
     }
-    // finalize: reset the ids of the vertices left on the stack; in try_pending
-    // a failed search that found no SCC adds them to `visited` (mod.rs:621-629)
+    for (uint32_t a = pos; a < nts; ++a) {
+      const uint32_t sl = ts(a);
+      const uint32_t d = dot_of(sl);
+      emit(rec_of(sl) & 0x03FFFFFFu, d, a == pos);
+      wl(nwl++) = d;
+      pt_free(sl);
+    }
+    nts = pos;
+    emitted = true;
+  }
+
+  __device__ __forceinline__ void dfs_finish() {
+    // finalize: reset ids of the vertices left on the stack; in try_pending a
+    // failed search that saved no SCC adds them to `visited` (mod.rs:621-629)
     const bool mark = in_try && missing != 0 && !emitted;
     for (uint32_t a = 0; a < nts; ++a) {
       const uint32_t sl = ts(a);
-      const uint32_t tv = w(T::TL + sl);
-      w(T::TL + sl) = mark ? (epoch << 24) : (tv & 0xFF000000u);
+      set_tl(sl, tmk(0, 0, mark ? epoch : tep(tl_of(sl))));
     }
-    return missing;
-  }
-
-  // try_pending (mod.rs:589-642): the snapshot in tmask, tried ascending (C2)
-  __device__ __forceinline__ void try_pending() {
-    new_epoch();  // visited = {}
-    while (tmask && !err) {
-      int best = -1;
-      uint32_t bd = 0xFFFFFFFFu;
-      for (uint64_t m = tmask; m; m &= m - 1) {
-        const int sl = __builtin_ctzll(m);
-        const uint32_t dd = w(T::DOT + sl);
-        if (dd < bd) { bd = dd; best = sl; }
-      }
-      tmask &= ~(1ull << best);
-      if ((w(T::TL + best) >> 24) == epoch) continue;  // visited: skipped, not re-registered
-      bool em;
-      const uint32_t miss = find_scc(best, true, em);
-      if (err) return;
-      if (miss == 0) {
-        new_epoch();  // Found: visited.clear()
-      } else {
-        w(T::WAIT + best) = miss;  // index_pending (mod.rs:525-554)
-        wmask |= 1ull << best;
-        if (em) new_epoch();
-      }
+    nts = 0;
+    if (missing) {  // index_pending(dot, missing) (mod.rs:525-554)
+      set_wait(root, missing);
+      wmask |= ONE << root;
+    }
+    if (in_try) {
+      if (!missing || emitted) new_epoch();  // visited.clear() (mod.rs:607, 621-623)
+      phase = PH_TRY;
+    } else {
+      phase = PH_CHECK;
     }
   }
 
-  // check_pending (mod.rs:556-587): LIFO over released dots
-  __device__ __forceinline__ void check_pending() {
-    while (nwl > 0 && !err) {
-      if (!wmask) { nwl = 0; return; }
-      const uint32_t x = wl(--nwl);
-      uint64_t t = 0;
-      for (uint64_t m = wmask; m; m &= m - 1) {
-        const int sl = __builtin_ctzll(m);
-        if (w(T::WAIT + sl) == x) t |= 1ull << sl;
+  // one DFS edge or one frame pop
+  __device__ __forceinline__ void dfs_iter() {
+    if (fdi < fnc) {
+      const uint32_t cwd = w(T::DEP + fdi * T::P + fv);
+      ++fdi;
+      const uint32_t dep = cwd & 0x0FFFFFFFu;
+      if (clk_contains(dep)) return;  // executed (tarjan.rs:128-145)
+      int x = -1;
+      if constexpr (T::SMALL) {
+        const uint32_t h = cwd >> 28;
+        if (h) x = (int)h - 1;
       }
-      if (!t) continue;
-      wmask &= ~t;  // PendingIndex::remove(x) (index.rs:205-207)
-      for (uint64_t m = t; m; m &= m - 1) w(T::WAIT + __builtin_ctzll(m)) = 0;
-      tmask = t;
-      try_pending();
+      if (x < 0) x = pt_find(dep);
+      if (x < 0) {  // missing: give up (tarjan.rs:148-157, shard_count == 1)
+        missing = dep;
+        dfs_finish();
+        return;
+      }
+      const uint32_t tx = tl_of((uint32_t)x);
+      if (tid(tx) == 0) {  // not visited: recurse (tarjan.rs:172-214)
+        ++idc;
+        set_tl((uint32_t)x, tmk(idc, idc, tep(tx)));
+        ts(nts++) = (uint8_t)x;
+        fr(nfr++) = (uint16_t)(fv | (fdi << 8));
+        fv = (uint32_t)x;
+        fdi = 0;
+        fnc = rec_of(fv) >> 26;
+      } else {  // visited and on the stack (tarjan.rs:215-225)
+        const uint32_t tv = tl_of(fv);
+        if (tid(tx) < tlow(tv)) set_tl(fv, tmk(tid(tv), tid(tx), tep(tv)));
+      }
+    } else {
+      const uint32_t tv = tl_of(fv);
+      const uint32_t lowv = tlow(tv);
+      if (tid(tv) == lowv) {  // SCC root (tarjan.rs:233-312)
+        save_scc();
+        if (err) { phase = PH_IDLE; return; }
+      }
+      if (nfr == 0) {  // root done: Found
+        dfs_finish();
+        return;
+      }
+      const uint32_t f = fr(--nfr);  // back in the parent: low = min(low, dep.low) (tarjan.rs:211)
+      fv = f & 0xFFu;
+      fdi = f >> 8;
+      fnc = rec_of(fv) >> 26;
+      const uint32_t tp = tl_of(fv);
+      if (lowv < tlow(tp)) set_tl(fv, tmk(tid(tp), lowv, tep(tp)));
     }
   }
 
-  // VertexIndex::index(Vertex::new(dot, cmd, deps, time)) (index.rs:33-37):
-  // deps j < DCAP come from the prefetched registers, the rest from HBM.
-  __device__ __forceinline__ int insert_vertex(uint32_t i, uint32_t d, uint32_t nd, const uint4* rdeps) {
-    const int sl = pt_insert(d, i);
-    if (sl < 0) return -1;
-    uint32_t nc = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < DCAP; ++j)
-      if (j < nd) pt_cache_dep(sl, d, rdeps[j].x, nc);
-    for (uint32_t j = DCAP; j < nd; ++j) pt_cache_dep(sl, d, deps[(size_t)j * plane + at(i)], nc);
-    if (err) return -1;
-    w(T::REC + sl) = i | (nc << 26);
-    return sl;
+  // try_pending (mod.rs:589-642): next waiter of the snapshot, ascending (C2)
+  __device__ __forceinline__ void try_iter() {
+    if (!tmask) { phase = PH_CHECK; return; }
+    const int best = argmin_dot(tmask);
+    tmask &= ~(ONE << best);
+    if (tep(tl_of((uint32_t)best)) == epoch) return;  // visited: skipped, not re-registered
+    dfs_start((uint32_t)best, true);
   }
 
-  // GraphExecutor::handle(Add) (executor.rs:69-80) -> handle_add (mod.rs:213-275)
-  __device__ __forceinline__ void handle(uint32_t i, uint32_t d, uint32_t h, const uint4* rdeps,
-                                         bool at_commit) {
+  // check_pending (mod.rs:556-587): pop one released dot (LIFO)
+  __device__ __forceinline__ void check_iter() {
+    if (nwl == 0 || !wmask) {
+      nwl = 0;
+      phase = PH_IDLE;
+      return;
+    }
+    const uint32_t x = wl(--nwl);
+    const Mask t = waiters(x);
+    if (!t) return;
+    wmask &= ~t;  // PendingIndex::remove(x): the waiters are no longer registered
+    tmask = t;
+    new_epoch();  // try_pending's fresh `visited`
+    phase = PH_TRY;
+  }
+
+  __device__ __forceinline__ void slow_iter() {
+    if (phase == PH_DFS) dfs_iter();
+    if (phase == PH_TRY) try_iter();
+    if (phase == PH_CHECK) check_iter();
+    if (err) phase = PH_IDLE;
+  }
+
+  // GraphExecutor::handle(Add) (executor.rs:69-80) -> handle_add (mod.rs:213-275):
+  // the fast path completes here; otherwise the lane enters the state machine.
+  __device__ __forceinline__ void step_start(uint32_t i, uint32_t d, uint32_t h, const uint32_t* rdeps,
+                                             bool at_commit) {
     cur = i;
+    nwl = 0;
     const uint32_t nd = hdr_nd(h), kind = h >> 29;
     if (nd > dmax) { err = FX_ERR_INVALID_ARG; return; }  // deps beyond the dep planes
     if ((d >> FX_SEQ_BITS) - 1u >= n || (d & FX_SEQ_MASK) == 0) { err = FX_ERR_DOT_RANGE; return; }
@@ -397,34 +561,28 @@ struct Exec {
 #pragma unroll
     for (uint32_t j = 0; j < DCAP; ++j) {
       if (j < nd) {
-        const uint32_t dep = rdeps[j].x;
+        const uint32_t dep = rdeps[j];
         if (dep <= prev) err = FX_ERR_DEPS_UNSORTED;
         prev = dep;
         if (dep != d && !clk_contains(dep)) fast = false;
       }
     }
     if (err) return;
-    nwl = 0;
     if (fast) {
       emit(i, d, true);
-      if (!wmask || err) return;
-      wl(nwl++) = d;
+      if (wmask && !err) {  // check_pending([dot])
+        wl(0) = d;
+        nwl = 1;
+        phase = PH_CHECK;
+      }
     } else {
       const int sl = insert_vertex(i, d, nd, rdeps);
-      if (sl < 0) return;
-      bool em;
-      const uint32_t miss = find_scc(sl, false, em);
-      if (err) return;
-      if (miss) {  // index_pending(dot, missing) (mod.rs:251-256)
-        w(T::WAIT + sl) = miss;
-        wmask |= 1ull << sl;
-      }
+      if (sl >= 0) dfs_start((uint32_t)sl, false);
     }
-    check_pending();
   }
 };
 
-template <class T>
+template <class T, uint32_t DCAP>
 __global__ __launch_bounds__(64) void k_graph_exec(KArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t lane = threadIdx.x;
@@ -434,7 +592,7 @@ __global__ __launch_bounds__(64) void k_graph_exec(KArgs a) {
   const uint32_t len = active ? (a.lengths ? min(a.lengths[s], a.steps) : a.steps) : 0u;
   uint32_t* gblock = a.state ? a.state + (size_t)blockIdx.x * T::WORDS * WAVE : nullptr;
 
-  Exec<T> e;
+  Exec<T, DCAP> e;
   if constexpr (T::GLOBAL) e.st = gblock + lane;
   else e.st = smem + lane;
   e.stream = s;
@@ -445,19 +603,44 @@ __global__ __launch_bounds__(64) void k_graph_exec(KArgs a) {
   e.deps = a.deps;
   e.order = a.order;
   e.release = a.release;
+#pragma unroll
+  for (uint32_t q = 0; q < Exec<T, DCAP>::RN; ++q) e.cf[q] = e.cw[q] = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < Exec<T, DCAP>::RP; ++q) e.sd[q] = e.sw[q] = e.sr[q] = 0;
 
   if (a.flags & FX_FLAG_INIT) {
-    for (uint32_t q = 0; q < T::NSRC * T::CLKS; ++q) e.w(T::CLK + q) = 0;
+    if constexpr (!T::REGS) {
+      for (uint32_t q = 0; q < T::NSRC * T::CLKS; ++q) e.w(T::CLK + q) = 0;
+    }
     if (a.init_frontier && active) {
-      for (uint32_t p = 0; p < T::NSRC && p < 8; ++p) e.w(T::CLK + p * T::CLKS) = a.init_frontier[(size_t)s * 8 + p];
+#pragma unroll
+      for (uint32_t p = 0; p < T::NSRC && p < 8; ++p) {
+        const uint32_t f = a.init_frontier[(size_t)s * 8 + p];
+        if constexpr (T::REGS) e.cf[p] = f;
+        else e.w(T::CLK + p * T::CLKS) = f;
+      }
     }
   } else {
     if constexpr (!T::GLOBAL) {
-      for (uint32_t q = 0; q < T::REG; ++q) smem[q * WAVE + lane] = gblock[q * WAVE + lane];
+      for (uint32_t q = 0; q < T::MEM; ++q) smem[q * WAVE + lane] = gblock[q * WAVE + lane];
     }
-    const uint32_t* r = gblock + (size_t)T::REG * WAVE + lane;
-    e.occ = (uint64_t)r[0] | ((uint64_t)r[WAVE] << 32);
-    e.wmask = (uint64_t)r[2 * WAVE] | ((uint64_t)r[3 * WAVE] << 32);
+    const uint32_t* r = gblock + (size_t)T::MEM * WAVE + lane;
+    if constexpr (T::REGS) {
+#pragma unroll
+      for (uint32_t q = 0; q < T::NSRC; ++q) {
+        e.cf[q] = r[q * WAVE];
+        e.cw[q] = r[(T::NSRC + q) * WAVE];
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < T::P; ++q) {
+        e.sd[q] = r[(2 * T::NSRC + q) * WAVE];
+        e.sw[q] = r[(2 * T::NSRC + T::P + q) * WAVE];
+        e.sr[q] = r[(2 * T::NSRC + 2 * T::P + q) * WAVE];
+      }
+    }
+    r += (size_t)T::RSAVE * WAVE;
+    e.occ = (typename T::Mask)((uint64_t)r[0] | ((uint64_t)r[WAVE] << 32));
+    e.wmask = (typename T::Mask)((uint64_t)r[2 * WAVE] | ((uint64_t)r[3 * WAVE] << 32));
     e.k = r[4 * WAVE];
     e.err = r[5 * WAVE] & 0xFFFFu;
     e.epoch = r[5 * WAVE] >> 16;
@@ -499,15 +682,25 @@ __global__ __launch_bounds__(64) void k_graph_exec(KArgs a) {
     const uint32_t base = b * 4;
     const uint32_t q0 = base < a.step_begin ? a.step_begin - base : 0u;
     const uint32_t q1 = a.step_end - base < 4u ? a.step_end - base : 4u;
-    // Steps are consumed from component x; the block is rotated one step per
-    // iteration so every register index stays static (no scratch).
-    for (uint32_t q = 0; q < q1; ++q) {
-      const uint32_t i = base + q;
-      if (q >= q0 && !e.err && i < len) e.handle(i, cd.x, ch.x, d0, at_commit);
-      cd = make_uint4(cd.y, cd.z, cd.w, 0u);
-      ch = make_uint4(ch.y, ch.z, ch.w, 0u);
+    // Lanes progress through the block's steps independently: a lane starts
+    // its next step as soon as its previous one (fast path or micro-op state
+    // machine) is done, so the wavefront waits once per block for its slowest
+    // lane instead of once per step.
+    uint32_t q = q0;
+    while (true) {
+      const bool want = e.phase == PH_IDLE && q < q1 && !e.err && base + q < len;
+      if (!__any(want || e.phase != PH_IDLE)) break;
+      if (want) {
+        const uint32_t m0 = lmask(q == 0), m1 = lmask(q == 1), m2 = lmask(q == 2), m3 = lmask(q == 3);
+#define FX_PICK(V) (((V).x & m0) | ((V).y & m1) | ((V).z & m2) | ((V).w & m3))
+        uint32_t rd[DCAP];
 #pragma unroll
-      for (uint32_t j = 0; j < DCAP; ++j) d0[j] = make_uint4(d0[j].y, d0[j].z, d0[j].w, 0u);
+        for (uint32_t j = 0; j < DCAP; ++j) rd[j] = FX_PICK(d0[j]);
+        e.step_start(base + q, FX_PICK(cd), FX_PICK(ch), rd, at_commit);
+#undef FX_PICK
+        ++q;
+      }
+      if (e.phase != PH_IDLE) e.slow_iter();
     }
     cd = nd_;
     ch = nh;
@@ -518,21 +711,35 @@ __global__ __launch_bounds__(64) void k_graph_exec(KArgs a) {
 
   if (!active) return;
   // Vertices still pending have no release step (yet).
-  for (uint64_t m = e.occ; m; m &= m - 1) {
-    const int sl = __builtin_ctzll(m);
-    a.release[e.at(e.w(T::REC + sl) & 0x03FFFFFFu)] = FX_RELEASE_NONE;
+  for (typename T::Mask m = e.occ; m; m &= m - 1) {
+    const uint32_t sl = __builtin_ctzll((uint64_t)m);
+    a.release[e.at(e.rec_of(sl) & 0x03FFFFFFu)] = FX_RELEASE_NONE;
   }
   a.nexec[s] = e.k;
   a.err[s] = e.err;
   if (a.flags & FX_FLAG_SAVE_STATE) {
     if constexpr (!T::GLOBAL) {
-      for (uint32_t q = 0; q < T::REG; ++q) gblock[q * WAVE + lane] = smem[q * WAVE + lane];
+      for (uint32_t q = 0; q < T::MEM; ++q) gblock[q * WAVE + lane] = smem[q * WAVE + lane];
     }
-    uint32_t* r = gblock + (size_t)T::REG * WAVE + lane;
-    r[0] = (uint32_t)e.occ;
-    r[WAVE] = (uint32_t)(e.occ >> 32);
-    r[2 * WAVE] = (uint32_t)e.wmask;
-    r[3 * WAVE] = (uint32_t)(e.wmask >> 32);
+    uint32_t* r = gblock + (size_t)T::MEM * WAVE + lane;
+    if constexpr (T::REGS) {
+#pragma unroll
+      for (uint32_t q = 0; q < T::NSRC; ++q) {
+        r[q * WAVE] = e.cf[q];
+        r[(T::NSRC + q) * WAVE] = e.cw[q];
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < T::P; ++q) {
+        r[(2 * T::NSRC + q) * WAVE] = e.sd[q];
+        r[(2 * T::NSRC + T::P + q) * WAVE] = e.sw[q];
+        r[(2 * T::NSRC + 2 * T::P + q) * WAVE] = e.sr[q];
+      }
+    }
+    r += (size_t)T::RSAVE * WAVE;
+    r[0] = (uint32_t)(uint64_t)e.occ;
+    r[WAVE] = (uint32_t)((uint64_t)e.occ >> 32);
+    r[2 * WAVE] = (uint32_t)(uint64_t)e.wmask;
+    r[3 * WAVE] = (uint32_t)((uint64_t)e.wmask >> 32);
     r[4 * WAVE] = e.k;
     r[5 * WAVE] = (e.err & 0xFFFFu) | (e.epoch << 16);
   }
@@ -622,34 +829,45 @@ static size_t state_bytes(uint32_t lanes) {
   return (size_t)((lanes + WAVE - 1) / WAVE) * T::WORDS * WAVE * 4;
 }
 
-template <class T>
-static int launch_exec(const KArgs& a, hipStream_t stream) {
+template <class T, uint32_t DCAP>
+static int launch_exec_d(const KArgs& a, hipStream_t stream) {
   if (T::GLOBAL && !a.state) return FX_ERR_INVALID_ARG;
   const uint32_t blocks = (a.num_lanes + WAVE - 1) / WAVE;
   if (blocks == 0) return FX_OK;
-  const size_t lds = T::GLOBAL ? 0 : (size_t)T::REG * WAVE * 4;
+  const size_t lds = T::GLOBAL ? 0 : (size_t)T::MEM * WAVE * 4;
   static bool configured = false;
   if (!configured && lds > 64 * 1024) {
-    (void)hipFuncSetAttribute((const void*)k_graph_exec<T>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_graph_exec<T, DCAP>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     configured = true;
   }
-  hipLaunchKernelGGL(k_graph_exec<T>, dim3(blocks), dim3(WAVE), lds, stream, a);
+  hipLaunchKernelGGL((k_graph_exec<T, DCAP>), dim3(blocks), dim3(WAVE), lds, stream, a);
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
+}
+
+// deps of the incoming Add prefetched into registers: the smallest of 3/5/8
+// that covers the batch's dep planes (more than 8 are read on demand)
+template <class T>
+static int launch_exec(const KArgs& a, hipStream_t stream) {
+  if (a.dmax <= 3) return launch_exec_d<T, 3>(a, stream);
+  if (a.dmax <= 5) return launch_exec_d<T, 5>(a, stream);
+  return launch_exec_d<T, 8>(a, stream);
 }
 
 template <class T>
 static uint32_t decode_pending_t(const uint32_t* block, uint32_t lane, uint32_t* dots,
                                  uint32_t* waits, uint32_t cap) {
-  const uint32_t* r = block + (size_t)T::REG * WAVE + lane;
+  const uint32_t* r = block + (size_t)(T::MEM + T::RSAVE) * WAVE + lane;
   const uint64_t occ = (uint64_t)r[0] | ((uint64_t)r[WAVE] << 32);
   const uint64_t wm = (uint64_t)r[2 * WAVE] | ((uint64_t)r[3 * WAVE] << 32);
+  const uint32_t dot_w = T::REGS ? T::MEM + 2 * T::NSRC : T::DOT;
+  const uint32_t wait_w = T::REGS ? T::MEM + 2 * T::NSRC + T::P : T::WAIT;
   uint32_t c = 0;
   for (uint64_t m = occ; m; m &= m - 1) {
     const int sl = __builtin_ctzll(m);
     if (c < cap) {
-      dots[c] = block[(T::DOT + sl) * WAVE + lane];
-      waits[c] = ((wm >> sl) & 1) ? block[(T::WAIT + sl) * WAVE + lane] : 0u;
+      dots[c] = block[(dot_w + sl) * WAVE + lane];
+      waits[c] = ((wm >> sl) & 1) ? block[(wait_w + sl) * WAVE + lane] : 0u;
     }
     ++c;
   }
@@ -659,9 +877,10 @@ static uint32_t decode_pending_t(const uint32_t* block, uint32_t lane, uint32_t*
 uint32_t decode_pending(uint32_t tier, const uint32_t* block, uint32_t lane, uint32_t* dots,
                         uint32_t* waits, uint32_t cap) {
   switch (tier) {
-    case 0: return decode_pending_t<Tier0>(block, lane, dots, waits, cap);
+    case 0: return group_decode_pending(block, lane, dots, waits, cap);
     case 1: return decode_pending_t<Tier1>(block, lane, dots, waits, cap);
     case 2: return decode_pending_t<Tier2>(block, lane, dots, waits, cap);
+    case 3: return decode_pending_t<TierLane>(block, lane, dots, waits, cap);
     default: return 0;
   }
 }
@@ -700,9 +919,10 @@ const char* fx_status_string(int s) {
 int fx_tier_query(uint32_t tier, uint32_t n, fx_tier_info* out) {
   if (!out) return FX_ERR_INVALID_ARG;
   switch (tier) {
-    case 0: *out = {Tier0::NSRC, Tier0::P, 32 * Tier0::XW, Tier0::WORDS}; break;
+    case 0: *out = {GROUP_LANES, GROUP_SLOTS, GROUP_WINDOW_BITS, group_state_words_per_stream()}; break;
     case 1: *out = {Tier1::NSRC, Tier1::P, 32 * Tier1::XW, Tier1::WORDS}; break;
     case 2: *out = {Tier2::NSRC, Tier2::P, 32 * Tier2::XW, Tier2::WORDS}; break;
+    case 3: *out = {TierLane::NSRC, TierLane::P, 32 * TierLane::XW, TierLane::WORDS}; break;
     default: return FX_ERR_INVALID_ARG;
   }
   return n >= 1 && n <= out->max_sources ? FX_OK : FX_ERR_INVALID_ARG;
@@ -711,9 +931,10 @@ int fx_tier_query(uint32_t tier, uint32_t n, fx_tier_info* out) {
 size_t fx_batch_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes) {
   (void)n;
   switch (tier) {
-    case 0: return state_bytes<Tier0>(lanes);
+    case 0: return group_state_bytes(lanes);
     case 1: return state_bytes<Tier1>(lanes);
     case 2: return state_bytes<Tier2>(lanes);
+    case 3: return state_bytes<TierLane>(lanes);
     default: return 0;
   }
 }
@@ -766,9 +987,10 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
     (void)hipEventRecord(g_ev0, hs);
   }
   switch (tier) {
-    case 0: st = launch_exec<Tier0>(a, hs); break;
+    case 0: st = launch_group(a, hs); break;
     case 1: st = launch_exec<Tier1>(a, hs); break;
     case 2: st = launch_exec<Tier2>(a, hs); break;
+    case 3: st = launch_exec<TierLane>(a, hs); break;
     default: return FX_ERR_INVALID_ARG;
   }
   if (g_profile) {
@@ -892,14 +1114,21 @@ int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out, ui
   const uint32_t S = in->num_streams;
   flags |= FX_FLAG_INIT;
   flags &= ~FX_FLAG_SAVE_STATE;
-  st = fx_batch_execute(in, out, 0, nullptr, S, nullptr, 0, in->steps, flags, nullptr, hip_stream);
+  const uint32_t first = in->dmax <= GROUP_LANES ? 0u : 1u;  // the group tier holds <= 16 deps
+  void* st1 = nullptr;
+  if (first == 1 && hipMalloc(&st1, fx_batch_state_bytes(1, in->n, S)) != hipSuccess) return FX_ERR_HIP;
+  st = fx_batch_execute(in, out, first, nullptr, S, st1, 0, in->steps, flags, nullptr, hip_stream);
+  if (st1) (void)hipFree(st1);
   if (st) return st;
-  if (tier_counts) tier_counts[0] = S;
+  if (tier_counts) {
+    for (uint32_t t = 0; t < FX_NUM_TIERS; ++t) tier_counts[t] = 0;
+    tier_counts[first] = S;
+  }
   std::vector<uint32_t> err(S);
   if (hipMemcpyAsync(err.data(), out->err, (size_t)S * 4, hipMemcpyDeviceToHost, hs) != hipSuccess)
     return FX_ERR_HIP;
   if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
-  for (uint32_t tier = 1; tier < FX_NUM_TIERS; ++tier) {
+  for (uint32_t tier = first + 1; tier <= FX_TIER_GLOBAL; ++tier) {
     std::vector<uint32_t> redo;
     for (uint32_t s = 0; s < S; ++s)
       if (err[s] == FX_ERR_CAPACITY) redo.push_back(s);

@@ -131,11 +131,13 @@ typedef struct fx_hist_batch {
 
 /* Executor tiers: capacity of the per-stream pending table and of the
  * executed-clock window above each source's frontier.  A stream that exceeds
- * its tier stops with FX_ERR_CAPACITY and is rerun at the next tier. */
-#define FX_TIER_LDS_SMALL 0 /* LDS-resident state, occupancy-sized   */
-#define FX_TIER_LDS_LARGE 1 /* LDS-resident state, one wave per CU    */
-#define FX_TIER_GLOBAL 2    /* HBM-resident state, deep capacities    */
-#define FX_NUM_TIERS 3
+ * its tier stops with FX_ERR_CAPACITY and is rerun at the next tier
+ * (fx_batch_run_tiered escalates 0 -> 1 -> 2). */
+#define FX_TIER_GROUP 0      /* 16 lanes per stream: 16 pending, 8 cached deps, n <= 16 */
+#define FX_TIER_LDS_LARGE 1  /* lane per stream, LDS-resident: 32 pending, one wave per CU */
+#define FX_TIER_GLOBAL 2     /* lane per stream, HBM-resident: 64 pending, 1024-bit windows */
+#define FX_TIER_LANE 3       /* lane per stream, LDS-resident: 12 pending (alternative tier 0) */
+#define FX_NUM_TIERS 4
 
 typedef struct fx_tier_info {
   uint32_t max_sources;    /* n supported                                   */
@@ -202,6 +204,9 @@ typedef struct fx_synth_params {
   uint32_t horizon;          /* rounds searched back for the latest conflict */
   uint32_t num_conflicts;
   uint32_t conflict_pct[8];
+  uint32_t conflict_block;   /* 0: rate = conflict_pct[i % num_conflicts] (seed-major);
+                                B: rate = conflict_pct[(i / B) % num_conflicts]
+                                (conflict-major: B consecutive instances share a rate) */
 } fx_synth_params;
 
 /* Planes of the synthetic batch: S = instances * n, steps = n * cmds, dmax = n. */

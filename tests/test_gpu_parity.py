@@ -100,7 +100,7 @@ def test_tier_reruns_happen_and_match(gpu):
     assert_parity(planes, res)
 
 
-@pytest.mark.parametrize("tier", [0, 1, 2])
+@pytest.mark.parametrize("tier", [0, 1, 2, 3])
 def test_each_tier_standalone(gpu, tier):
     p = fs.synth_params(seed=9, n=5, instances=20, cmds=150, window=6, cycle_pct=30)
     planes = fs.synth_host(p)
@@ -136,11 +136,12 @@ def test_ragged_lengths_and_truncated_streams(gpu):
     assert_parity(planes, res)
 
 
-def test_chunked_resume_equals_one_shot(gpu):
+@pytest.mark.parametrize("tier", [0, 1, 2, 3])
+def test_chunked_resume_equals_one_shot(gpu, tier):
     import ctypes
     p = fs.synth_params(seed=8, n=5, instances=30, cmds=100, window=10, cycle_pct=30)
     planes = fs.synth_host(p)
-    one = fd.run_batch(planes, tiered=False, tier=0, metrics=False)
+    one = fd.run_batch(planes, tiered=False, tier=tier, metrics=False)
     lib = _lib.load()
     S, steps, pw = planes.S, planes.steps, planes.plane
     d = [fd.DeviceBuffer(a.nbytes) for a in (planes.dot, planes.hdr, planes.deps)]
@@ -148,14 +149,14 @@ def test_chunked_resume_equals_one_shot(gpu):
         b.upload(a)
     order, release = fd.DeviceBuffer(pw * 4), fd.DeviceBuffer(pw * 4)
     nexec, err = fd.DeviceBuffer(S * 4), fd.DeviceBuffer(S * 4)
-    state = fd.DeviceBuffer(lib.fx_batch_state_bytes(0, 5, S))
+    state = fd.DeviceBuffer(lib.fx_batch_state_bytes(tier, 5, S))
     inb = _lib.StreamBatch(d[0].ptr, d[1].ptr, d[2].ptr, None, S, steps, planes.dmax, 5)
     outb = _lib.OrderBatch(order.ptr, release.ptr, nexec.ptr, err.ptr)
     cuts = [0, 1, 7, 64, 65, 200, 333, steps]
     for a, b in zip(cuts[:-1], cuts[1:]):
         flags = _lib.FX_FLAG_SAVE_STATE | (_lib.FX_FLAG_INIT if a == 0 else 0)
-        _lib.check(lib.fx_batch_execute(ctypes.byref(inb), ctypes.byref(outb), 0, None, S, state.ptr,
-                                        a, b, flags, None, None))
+        _lib.check(lib.fx_batch_execute(ctypes.byref(inb), ctypes.byref(outb), tier, None, S,
+                                        state.ptr, a, b, flags, None, None))
     ne = nexec.download(np.uint32, S)
     er = err.download(np.uint32, S)
     assert np.array_equal(ne, one.nexec)
