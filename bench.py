@@ -27,6 +27,10 @@ sys.path.insert(0, ROOT)
 
 METRIC = "executed cmds/sec (node) for batched Atlas/EPaxos sims; % of HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+KERNEL_NAMES = {0: "k_graph_group", 1: "k_graph_exec<Tier1>", 2: "k_graph_exec<Tier2>",
+                3: "k_graph_exec<TierLane>", 4: "k_graph_wave"}
+LAYOUT = {0: "16 lanes per stream", 1: "one lane per stream", 2: "one lane per stream",
+          3: "one lane per stream", 4: "one wavefront per stream"}
 
 
 def parse():
@@ -44,6 +48,7 @@ def parse():
     ap.add_argument("--conflict-block", type=int, default=-1,
                     help="instances per conflict rate block (-1 = --seeds: conflict-major "
                          "enumeration, so a wavefront's streams share a rate; 0 = seed-major)")
+    ap.add_argument("--tier", type=int, default=-1, help="executor tier (-1 = FX_TIER_DEFAULT)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", type=str, default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -108,6 +113,7 @@ def main():
     n_adds = S * steps
     alg_bytes = 16 * n_adds + 4 * nd_total
 
+    tier = _lib.FX_TIER_DEFAULT if args.tier < 0 else args.tier
     tiered = [False]
     tier_counts = (ctypes.c_uint32 * _lib.FX_NUM_TIERS)()
 
@@ -115,9 +121,10 @@ def main():
         chain.zero_()
         delay.zero_()
         if tiered[0]:
-            st = lib.fx_batch_run_tiered(ctypes.byref(inb), ctypes.byref(outb), 0, hs, tier_counts)
+            st = lib.fx_batch_run_tiered(ctypes.byref(inb), ctypes.byref(outb),
+                                         _lib.first_tier_flag(tier), hs, tier_counts)
         else:
-            st = lib.fx_batch_execute(ctypes.byref(inb), ctypes.byref(outb), 0, None, S, None, 0,
+            st = lib.fx_batch_execute(ctypes.byref(inb), ctypes.byref(outb), tier, None, S, None, 0,
                                       steps, _lib.FX_FLAG_INIT, None, hs)
         _lib.check(st, "executor")
         _lib.check(lib.fx_batch_metrics(ctypes.byref(inb), ctypes.byref(outb), ctypes.byref(hb), hs),
@@ -190,7 +197,7 @@ def main():
                     traffic = None
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                    "traffic": traffic, "kernel": "k_graph_exec<Tier0>",
+                    "traffic": traffic, "kernel": KERNEL_NAMES.get(tier, "tier%d" % tier),
                     "kernel_ms_avg": round(kavg, 4), "alg_bytes_per_launch": alg_bytes,
                     "alg_bytes_per_cmd": round(alg_bytes / n_adds, 3)}
         cpu = None
@@ -216,7 +223,8 @@ def main():
                 "window": args.window, "cycle_pct": args.cycle_pct, "seed": args.seed,
                 "instance_order": "conflict-major (%d instances per rate)" % cblock if cblock
                                   else "seed-major",
-                "parallelism": "instances sharded over %d GPU(s), one wavefront lane per stream" % world,
+                "parallelism": "instances sharded over %d GPU(s), %s" % (world, LAYOUT.get(tier, "")),
+                "tier": tier,
             },
             "edges_per_s": round(edges, 1),
             "executed_per_step": int(executed_total),
@@ -233,9 +241,9 @@ def main():
 
 
 def workload_key(args):
-    return "n%d_s%d_c%s_m%d_w%d_y%d_seed%d_b%d" % (
+    return "n%d_s%d_c%s_m%d_w%d_y%d_seed%d_b%d_t%d" % (
         args.n, args.seeds, args.conflicts.replace(",", "-"), args.cmds, args.window,
-        args.cycle_pct, args.seed, args.conflict_block)
+        args.cycle_pct, args.seed, args.conflict_block, args.tier)
 
 
 def cpu_baseline(args, lib, dot, hdr, deps, order, release, nexec, S, steps, dmax, pw):

@@ -76,7 +76,7 @@ struct fx_graph_executor {
   uint32_t dmax = 0;     // dep planes in use
   uint32_t uploaded = 0; // rows present on the device
   DevBuf d_dot, d_hdr, d_deps, d_order, d_release, d_nexec, d_err, d_state;
-  uint32_t tier = 0;
+  uint32_t tier = FX_TIER_DEFAULT;
   uint32_t processed = 0;  // steps executed by the device state
   uint32_t consumed = 0;   // order entries already converted
 
@@ -172,6 +172,10 @@ int flush(fx_graph_executor* ex) {
   fx_order_batch out{ex->d_order.u32(), ex->d_release.u32(), ex->d_nexec.u32(), ex->d_err.u32()};
   uint32_t nexec = 0, err = 0;
   while (true) {
+    if (ex->tier == FX_TIER_WAVE && in.dmax > 14) {  // wider Adds than the wave tier reads
+      ex->tier = FX_TIER_LDS_LARGE;
+      ex->processed = 0;
+    }
     if (!ex->d_state.ensure(fx_batch_state_bytes(ex->tier, ex->cfg.n, 1))) return ex->sticky = FX_ERR_HIP;
     uint32_t flags = FX_FLAG_SAVE_STATE;
     if (ex->processed == 0) flags |= FX_FLAG_INIT;
@@ -191,10 +195,11 @@ int flush(fx_graph_executor* ex) {
         hipMemcpyAsync(&err, ex->d_err.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipStreamSynchronize(ex->stream))
       return ex->sticky = FX_ERR_HIP;
-    if (err == FX_ERR_CAPACITY && ex->tier < FX_TIER_GLOBAL) {
+    if (err == FX_ERR_CAPACITY && ex->tier != FX_TIER_GLOBAL) {
       // rerun the whole log one tier up; the already-consumed prefix of the
       // (deterministic) order is skipped below
-      ex->tier += 1;
+      ex->tier = ex->tier == FX_TIER_WAVE || ex->tier == FX_TIER_LDS_LARGE ? FX_TIER_GLOBAL
+                                                                         : FX_TIER_LDS_LARGE;
       ex->processed = 0;
       continue;
     }

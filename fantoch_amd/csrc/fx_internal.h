@@ -37,6 +37,17 @@ constexpr uint32_t GROUP_SLOTS = 16;        // pending vertices per stream
 constexpr uint32_t GROUP_CACHE = 8;         // cached deps per pending vertex
 constexpr uint32_t GROUP_WINDOW_BITS = 32;  // executed-clock window per source
 
+// Wavefront-per-stream tier (graph_wave.hip).
+int launch_wave(const KArgs& a, hipStream_t stream);
+size_t wave_state_bytes(uint32_t streams);
+uint32_t wave_state_words_per_stream();
+uint32_t wave_decode_pending(const uint32_t* block, uint32_t stream_in_launch, uint32_t* dots,
+                             uint32_t* waits, uint32_t cap);
+constexpr uint32_t WAVE_SLOTS = 64;        // pending vertices per stream (one per lane)
+constexpr uint32_t WAVE_CACHE = 8;         // cached deps per pending vertex
+constexpr uint32_t WAVE_WINDOW_BITS = 32;  // executed-clock window per source
+constexpr uint32_t WAVE_MAX_DEPS = 14;     // dep planes read per Add
+
 // Decodes the pending vertices of lane `lane` from a saved state block
 // (tier layout of graph_exec.hip).  Writes up to cap (dot, waiting_on) pairs;
 // returns the count.

@@ -881,6 +881,7 @@ uint32_t decode_pending(uint32_t tier, const uint32_t* block, uint32_t lane, uin
     case 1: return decode_pending_t<Tier1>(block, lane, dots, waits, cap);
     case 2: return decode_pending_t<Tier2>(block, lane, dots, waits, cap);
     case 3: return decode_pending_t<TierLane>(block, lane, dots, waits, cap);
+    case 4: return wave_decode_pending(block, lane, dots, waits, cap);
     default: return 0;
   }
 }
@@ -923,6 +924,7 @@ int fx_tier_query(uint32_t tier, uint32_t n, fx_tier_info* out) {
     case 1: *out = {Tier1::NSRC, Tier1::P, 32 * Tier1::XW, Tier1::WORDS}; break;
     case 2: *out = {Tier2::NSRC, Tier2::P, 32 * Tier2::XW, Tier2::WORDS}; break;
     case 3: *out = {TierLane::NSRC, TierLane::P, 32 * TierLane::XW, TierLane::WORDS}; break;
+    case 4: *out = {8, WAVE_SLOTS, WAVE_WINDOW_BITS, wave_state_words_per_stream()}; break;
     default: return FX_ERR_INVALID_ARG;
   }
   return n >= 1 && n <= out->max_sources ? FX_OK : FX_ERR_INVALID_ARG;
@@ -935,6 +937,7 @@ size_t fx_batch_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes) {
     case 1: return state_bytes<Tier1>(lanes);
     case 2: return state_bytes<Tier2>(lanes);
     case 3: return state_bytes<TierLane>(lanes);
+    case 4: return wave_state_bytes(lanes);
     default: return 0;
   }
 }
@@ -991,6 +994,7 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
     case 1: st = launch_exec<Tier1>(a, hs); break;
     case 2: st = launch_exec<Tier2>(a, hs); break;
     case 3: st = launch_exec<TierLane>(a, hs); break;
+    case 4: st = launch_wave(a, hs); break;
     default: return FX_ERR_INVALID_ARG;
   }
   if (g_profile) {
@@ -1104,8 +1108,19 @@ int fx_synth_generate_host(const fx_synth_params* p, uint32_t* dot, uint32_t* hd
   return FX_OK;
 }
 
-// Synchronous tiered driver: tier 0 for all, then reruns of the streams that
-// ran out of capacity at tiers 1 and 2.
+// Escalation chain of fx_batch_run_tiered (FX_NUM_TIERS = none).
+static uint32_t escalate(uint32_t tier) {
+  switch (tier) {
+    case FX_TIER_GROUP: return FX_TIER_LDS_LARGE;
+    case FX_TIER_LANE: return FX_TIER_LDS_LARGE;
+    case FX_TIER_LDS_LARGE: return FX_TIER_GLOBAL;
+    case FX_TIER_WAVE: return FX_TIER_GLOBAL;
+    default: return FX_NUM_TIERS;
+  }
+}
+
+// Synchronous tiered driver: the first tier for all, then reruns of the
+// streams that ran out of capacity up the escalation chain.
 int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags,
                         void* hip_stream, uint32_t* tier_counts) {
   int st = check_batch(in, out);
@@ -1114,9 +1129,16 @@ int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out, ui
   const uint32_t S = in->num_streams;
   flags |= FX_FLAG_INIT;
   flags &= ~FX_FLAG_SAVE_STATE;
-  const uint32_t first = in->dmax <= GROUP_LANES ? 0u : 1u;  // the group tier holds <= 16 deps
+  const uint32_t ft = (flags >> FX_FLAG_TIER_SHIFT) & 7u;
+  flags &= ~(7u << FX_FLAG_TIER_SHIFT);
+  uint32_t first = ft ? ft - 1u : (uint32_t)FX_TIER_DEFAULT;
+  if (first >= FX_NUM_TIERS) return FX_ERR_INVALID_ARG;
+  // tiers that cannot hold the widest Add start one step up the chain
+  if ((first == FX_TIER_WAVE && in->dmax > WAVE_MAX_DEPS) || (first == FX_TIER_GROUP && in->dmax > GROUP_LANES))
+    first = FX_TIER_LDS_LARGE;
   void* st1 = nullptr;
-  if (first == 1 && hipMalloc(&st1, fx_batch_state_bytes(1, in->n, S)) != hipSuccess) return FX_ERR_HIP;
+  if (first == FX_TIER_GLOBAL && hipMalloc(&st1, fx_batch_state_bytes(first, in->n, S)) != hipSuccess)
+    return FX_ERR_HIP;
   st = fx_batch_execute(in, out, first, nullptr, S, st1, 0, in->steps, flags, nullptr, hip_stream);
   if (st1) (void)hipFree(st1);
   if (st) return st;
@@ -1128,7 +1150,7 @@ int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out, ui
   if (hipMemcpyAsync(err.data(), out->err, (size_t)S * 4, hipMemcpyDeviceToHost, hs) != hipSuccess)
     return FX_ERR_HIP;
   if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
-  for (uint32_t tier = first + 1; tier <= FX_TIER_GLOBAL; ++tier) {
+  for (uint32_t tier = escalate(first); tier < FX_NUM_TIERS; tier = escalate(tier)) {
     std::vector<uint32_t> redo;
     for (uint32_t s = 0; s < S; ++s)
       if (err[s] == FX_ERR_CAPACITY) redo.push_back(s);

@@ -1,0 +1,530 @@
+// graph_wave.hip — the wavefront-per-stream tier of the batched GraphExecutor.
+//
+// Same algorithm as graph_exec.hip / graph_group.hip (DependencyGraph::handle_add,
+// fantoch_ps/src/executor/graph/mod.rs:213-642, canonical orders C1 and C2),
+// laid out so that ONE 64-lane wavefront runs ONE executor and every control
+// decision is wave-uniform (scalar branches, no divergence at all):
+//   * lane l owns pending-vertex slot l (VertexIndex, index.rs:18-51): its dot,
+//     arrival index, registered-on dot (PendingIndex, index.rs:145-208), Tarjan
+//     id/low/visited-epoch word and one DFS frame sit in lane l's VGPRs; a
+//     lookup by dot is one compare + ballot, a field read is one v_readlane;
+//   * lane l < n owns the executed clock of source l + 1 (AEClock, threshold
+//     0.9.1: frontier + 32-bit exception window);
+//   * the deps of an incoming Add are checked in parallel (lane j: dep j);
+//   * the Tarjan stack is implicit: the vertices on it are exactly the pending
+//     slots with a non-zero id, in id order (tarjan.rs:96-316), so an SCC pop
+//     is one ballot (id >= id(root));
+//   * the deps of each pending vertex that were not yet executed when it was
+//     indexed, the check_pending worklist and a 16-step chunk of the input
+//     planes live in LDS.
+// The input chunk for steps [16c, 16c+16) is fetched one chunk ahead by one
+// 16-byte load per lane (lane 4p+b: plane p, 4-step block b of the chunk), so
+// HBM latency is covered by 16 steps of work and the vmcnt wait is static.
+// A stream that outgrows 64 pending vertices, 8 cached deps per vertex or the
+// 32-bit clock window stops with FX_ERR_CAPACITY and is rerun at tier 2.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fantoch_amd.h"
+#include "fx_internal.h"
+
+namespace fx {
+namespace wav {
+
+constexpr uint32_t P = WAVE_SLOTS;      // pending slots (one per lane)
+constexpr uint32_t C = WAVE_CACHE;      // cached deps per slot
+constexpr uint32_t WLC = P + 1;         // check_pending worklist capacity
+constexpr uint32_t CH = 16;             // steps per input chunk
+constexpr uint32_t NPL = 16;            // input planes per chunk: dot, hdr, 14 dep planes
+constexpr uint32_t MAXD = NPL - 2;      // deps per Add this tier reads
+constexpr uint32_t WPB = 4;             // wavefronts (streams) per workgroup
+constexpr uint32_t L_CACHE = 0;         // LDS words per stream: [P][C] cached deps
+constexpr uint32_t L_WL = P * C;        //                        [WLC] worklist
+constexpr uint32_t L_IN = (L_WL + WLC + 3) & ~3u;  //            [NPL][CH] input chunk
+constexpr uint32_t LW = L_IN + NPL * CH;
+constexpr uint32_t RREGS = 7;           // saved per-lane registers
+constexpr uint32_t S_LDS = 64 * RREGS;  // saved state: regs | LDS cache + worklist | scalars
+constexpr uint32_t S_SCAL = S_LDS + L_IN;
+constexpr uint32_t WPS = S_SCAL + 8;
+
+enum : uint32_t { PH_IDLE = 0, PH_DFS = 1, PH_TRY = 2, PH_CHECK = 3 };
+
+// Tarjan word: id (7 bits) | low (7 bits) | visited epoch (16 bits)
+__device__ __forceinline__ uint32_t tid(uint32_t t) { return t & 127u; }
+__device__ __forceinline__ uint32_t tlow(uint32_t t) { return (t >> 7) & 127u; }
+__device__ __forceinline__ uint32_t tep(uint32_t t) { return t >> 14; }
+__device__ __forceinline__ uint32_t tmk(uint32_t id, uint32_t low, uint32_t ep) {
+  return id | (low << 7) | (ep << 14);
+}
+constexpr uint32_t EPOCH_MAX = 0xFFFFu;
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)src);
+}
+__device__ __forceinline__ uint32_t uni(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+__device__ __forceinline__ uint32_t gather(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+__device__ __forceinline__ uint64_t bal(bool p) { return (uint64_t)__ballot(p); }
+__device__ __forceinline__ uint32_t ctz64(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
+__device__ __forceinline__ uint32_t pop64(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
+
+struct Wave {
+  uint32_t lid;
+  uint64_t lbit;  // 1 << lid
+  // lane-owned slot fields (slot = lid), DFS frame (depth = lid), clock (source = lid + 1)
+  uint32_t sdot = 0, srec = 0, swait = 0, stl = 0, sfr = 0;
+  uint32_t cf = 0, cw = 0;
+  // wave-uniform state
+  uint64_t occ = 0, wmask = 0, tmask = 0;
+  uint32_t k = 0, err = 0, epoch = 1, nwl = 0, cur = 0;
+  uint32_t phase = PH_IDLE, root = 0, idc = 0, nfr = 0, missing = 0;
+  uint32_t fv = 0, fdi = 0, fnc = 0, in_try = 0, emitted = 0;
+  // stream context
+  uint32_t stream = 0, n = 0, steps = 0;
+  uint32_t* lds = nullptr;
+  uint32_t* order = nullptr;
+  uint32_t* release = nullptr;
+
+  __device__ __forceinline__ size_t at(uint32_t step) const { return fx_index(step, stream, steps); }
+  __device__ __forceinline__ bool mine(uint64_t m) const { return (m & lbit) != 0; }
+
+  // ------------------------------------------------------------ clock
+  // AEClock::contains for a per-lane dot (tarjan.rs:131-132)
+  __device__ __forceinline__ bool contains_v(uint32_t d) const {
+    const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
+    const uint32_t f = gather(cf, si & 63u), w = gather(cw, si & 63u);
+    const uint32_t seq = d & FX_SEQ_MASK, off = seq - f - 1u;
+    return si < n && (seq <= f || (off < 32u && ((w >> (off & 31u)) & 1u)));
+  }
+  // AEClock::contains for a wave-uniform dot
+  __device__ __forceinline__ bool contains_u(uint32_t d) const {
+    const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
+    if (si >= n) return false;
+    const uint32_t f = rl(cf, si), w = rl(cw, si);
+    const uint32_t seq = d & FX_SEQ_MASK, off = seq - f - 1u;
+    return seq <= f || (off < 32u && ((w >> off) & 1u));
+  }
+  // AEClock::add for a wave-uniform dot (tarjan.rs:293)
+  __device__ __forceinline__ void clk_add(uint32_t d) {
+    const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
+    if (si >= n) { err = FX_ERR_DOT_RANGE; return; }
+    uint32_t f = rl(cf, si), w = rl(cw, si);
+    const uint32_t seq = d & FX_SEQ_MASK;
+    if (seq <= f) return;
+    const uint32_t off = seq - f - 1u;
+    if (off >= 32u) { err = FX_ERR_CAPACITY; return; }
+    if (off != 0) {
+      w |= 1u << off;
+    } else {
+      const uint32_t win = w >> 1;               // bit j <-> seq f + 2 + j
+      const uint32_t ones = __builtin_ctz(~win);  // top bit of win is 0 -> <= 31
+      f = f + 1 + ones;
+      w = win >> ones;
+    }
+    if (lid == si) {
+      cf = f;
+      cw = w;
+    }
+  }
+
+  // ------------------------------------------------------ slot table
+  __device__ __forceinline__ int find(uint32_t d) const {
+    const uint64_t m = bal(mine(occ) && sdot == d);
+    return m ? (int)ctz64(m) : -1;
+  }
+  __device__ __forceinline__ uint32_t& cache(uint32_t sl, uint32_t j) { return lds[L_CACHE + sl * C + j]; }
+  __device__ __forceinline__ uint32_t& wl(uint32_t i) { return lds[L_WL + i]; }
+
+  __device__ __forceinline__ void new_epoch() {
+    epoch = epoch + 1;
+    if (epoch > EPOCH_MAX) {
+      if (mine(occ)) stl = tmk(tid(stl), tlow(stl), 0);
+      epoch = 1;
+    }
+  }
+
+  // VertexIndex::index(Vertex::new(dot, cmd, deps, time)) (index.rs:33-37);
+  // keep = lane j holds dep j of the Add and it is not executed (executed deps
+  // are ignored by every later search, tarjan.rs:128-145, and the executed
+  // clock only grows); they are cached in ascending order.
+  __device__ __forceinline__ int insert_vertex(uint32_t i, uint32_t d, bool keep, uint32_t depj) {
+    const uint64_t fre = ~occ;
+    if (!fre) { err = FX_ERR_CAPACITY; return -1; }
+    const uint32_t sl = ctz64(fre);
+    const uint64_t km = bal(keep);
+    const uint32_t nc = pop64(km);
+    if (nc > C) { err = FX_ERR_CAPACITY; return -1; }
+    if (keep) cache(sl, pop64(km & (lbit - 1u))) = depj;
+    if (lid == sl) {
+      sdot = d;
+      srec = i | (nc << 26);
+      swait = 0;
+      stl = 0;
+    }
+    occ |= 1ull << sl;
+    return (int)sl;
+  }
+
+  // save_scc (mod.rs:488-523) for a singleton: to_execute + executed clock
+  __device__ __forceinline__ void emit_one(uint32_t rec, uint32_t d) {
+    if (k >= steps) { err = FX_ERR_ORDER_OVERFLOW; return; }
+    if (lid == 0) {
+      order[at(k)] = rec | FX_ORDER_SCC_START;
+      release[at(rec)] = cur;
+    }
+    ++k;
+    clk_add(d);
+  }
+
+  __device__ __forceinline__ void dfs_start(uint32_t r, bool intry) {
+    root = r;
+    in_try = intry;
+    emitted = 0;
+    missing = 0;
+    idc = 1;
+    const uint32_t tr = rl(stl, r);
+    if (lid == r) stl = tmk(1, 1, tep(tr));
+    nfr = 0;
+    fv = r;
+    fdi = 0;
+    fnc = rl(srec, r) >> 26;
+    phase = PH_DFS;
+  }
+
+  // The SCC rooted at fv = the stack vertices with id >= id(fv), saved in
+  // ascending dot order (SCC = BTreeSet<Dot>, tarjan.rs:15), clock updated.
+  __device__ __forceinline__ void save_scc() {
+    const uint32_t idv = tid(rl(stl, fv));
+    const bool mem = mine(occ) && tid(stl) >= idv;
+    const uint64_t mm = bal(mem);
+    const uint32_t cnt = pop64(mm);
+    if (k + cnt > steps) { err = FX_ERR_ORDER_OVERFLOW; return; }
+    if (nwl + cnt > WLC) { err = FX_ERR_CAPACITY; return; }
+    uint32_t rank = 0;
+    if (cnt == 1) {
+      const uint32_t d = rl(sdot, fv);
+      if (lid == 0) {
+        const uint32_t rec = rl(srec, fv) & 0x03FFFFFFu;
+        order[at(k)] = rec | FX_ORDER_SCC_START;
+        release[at(rec)] = cur;
+        wl(nwl) = d;
+      }
+      ++k;
+      ++nwl;
+      clk_add(d);
+    } else {
+      for (uint64_t m = mm; m; m &= m - 1) rank += rl(sdot, ctz64(m)) < sdot ? 1u : 0u;
+      if (mem) {
+        const uint32_t rec = srec & 0x03FFFFFFu;
+        order[at(k + rank)] = rec | (rank == 0 ? FX_ORDER_SCC_START : 0u);
+        release[at(rec)] = cur;
+        wl(nwl + rank) = sdot;
+      }
+      k += cnt;
+      nwl += cnt;
+      for (uint32_t r = 0; r < cnt; ++r) {  // clock in ascending dot order
+        const uint32_t lr = ctz64(bal(mem && rank == r));
+        clk_add(rl(sdot, lr));
+      }
+    }
+    occ &= ~mm;
+    wmask &= ~mm;
+    tmask &= ~mm;
+    emitted = 1;
+  }
+
+  __device__ __forceinline__ void dfs_finish() {
+    // finalize (tarjan.rs:60-93): reset ids of the vertices left on the stack;
+    // in try_pending a failed search that saved no SCC marks them visited
+    const bool mark = in_try && missing != 0 && !emitted;
+    if (mine(occ) && tid(stl) != 0) stl = tmk(0, 0, mark ? epoch : tep(stl));
+    if (missing) {  // index_pending(dot, missing) (mod.rs:525-554)
+      if (lid == root) swait = missing;
+      wmask |= 1ull << root;
+    }
+    if (in_try) {
+      if (!missing || emitted) new_epoch();  // visited.clear() (mod.rs:607, 621-623)
+      phase = PH_TRY;
+    } else {
+      phase = PH_CHECK;
+    }
+  }
+
+  // one DFS edge or one frame pop (TarjanSCCFinder::strong_connect, iterative)
+  __device__ __forceinline__ void dfs_iter() {
+    if (fdi < fnc) {
+      const uint32_t dep = uni(cache(fv, fdi));
+      ++fdi;
+      if (contains_u(dep)) return;  // executed (tarjan.rs:128-145)
+      const int x = find(dep);
+      if (x < 0) {  // missing: give up (tarjan.rs:148-157, shard_count == 1)
+        missing = dep;
+        dfs_finish();
+        return;
+      }
+      const uint32_t tx = rl(stl, (uint32_t)x);
+      if (tid(tx) == 0) {  // not visited: recurse (tarjan.rs:172-214)
+        ++idc;
+        if (lid == (uint32_t)x) stl = tmk(idc, idc, tep(tx));
+        if (lid == nfr) sfr = fv | (fdi << 8);
+        ++nfr;
+        fv = (uint32_t)x;
+        fdi = 0;
+        fnc = rl(srec, fv) >> 26;
+      } else {  // visited and on the stack (tarjan.rs:215-225)
+        const uint32_t tv = rl(stl, fv);
+        if (tid(tx) < tlow(tv) && lid == fv) stl = tmk(tid(tv), tid(tx), tep(tv));
+      }
+    } else {
+      const uint32_t tv = rl(stl, fv);
+      const uint32_t lowv = tlow(tv);
+      if (tid(tv) == lowv) {  // SCC root (tarjan.rs:233-312)
+        save_scc();
+        if (err) return;
+      }
+      if (nfr == 0) {  // root done: Found
+        dfs_finish();
+        return;
+      }
+      --nfr;
+      const uint32_t f = rl(sfr, nfr);  // back in the parent (tarjan.rs:211)
+      fv = f & 0xFFu;
+      fdi = f >> 8;
+      fnc = rl(srec, fv) >> 26;
+      const uint32_t tp = rl(stl, fv);
+      if (lowv < tlow(tp) && lid == fv) stl = tmk(tid(tp), lowv, tep(tp));
+    }
+  }
+
+  // try_pending (mod.rs:589-642): next waiter of the snapshot, ascending (C2)
+  __device__ __forceinline__ void try_iter() {
+    if (!tmask) { phase = PH_CHECK; return; }
+    uint32_t best = ctz64(tmask), best_dot = rl(sdot, best);
+    for (uint64_t m = tmask & (tmask - 1); m; m &= m - 1) {
+      const uint32_t b = ctz64(m), v = rl(sdot, b);
+      if (v < best_dot) {
+        best_dot = v;
+        best = b;
+      }
+    }
+    tmask &= ~(1ull << best);
+    if (tep(rl(stl, best)) == epoch) return;  // visited: skipped, not re-registered
+    dfs_start(best, true);
+  }
+
+  // check_pending (mod.rs:556-587): pop one released dot (LIFO)
+  __device__ __forceinline__ void check_iter() {
+    if (nwl == 0 || !wmask) {
+      nwl = 0;
+      phase = PH_IDLE;
+      return;
+    }
+    --nwl;
+    const uint32_t x = uni(wl(nwl));
+    const uint64_t t = bal(mine(wmask) && swait == x);
+    if (!t) return;
+    wmask &= ~t;  // PendingIndex::remove(x)
+    tmask = t;
+    new_epoch();  // try_pending's fresh `visited`
+    phase = PH_TRY;
+  }
+
+  // GraphExecutor::handle(Add) (executor.rs:69-80) -> handle_add (mod.rs:213-275)
+  __device__ __forceinline__ void step_start(uint32_t i, uint32_t d, uint32_t h, uint32_t depj,
+                                             uint32_t dmax, bool at_commit) {
+    cur = i;
+    nwl = 0;
+    const uint32_t nd = (h >> 24) & 31u, kind = h >> 29;
+    if (nd > dmax || nd > MAXD) { err = FX_ERR_INVALID_ARG; return; }
+    if ((d >> FX_SEQ_BITS) - 1u >= n || (d & FX_SEQ_MASK) == 0) { err = FX_ERR_DOT_RANGE; return; }
+    if (at_commit) {  // execute_at_commit bypass (executor.rs:72-73)
+      if (lid == 0) {
+        order[at(k)] = i | FX_ORDER_SCC_START;
+        release[at(i)] = i;
+      }
+      ++k;
+      return;
+    }
+    if (occ && find(d) >= 0) { err = FX_ERR_DOUBLE_INDEX; return; }  // mod.rs:233-237
+    const bool valid = lid < nd;
+    const uint32_t prev = gather(depj, (lid - 1u) & 63u);
+    if (bal(valid && lid > 0 && depj <= prev)) { err = FX_ERR_DEPS_UNSORTED; return; }
+    const bool keep = valid && depj != d && !contains_v(depj);
+    if (kind == FX_KIND_INDEX_ONLY) {
+      insert_vertex(i, d, keep, depj);
+      return;
+    }
+    // fast path: every dep is self or executed -> a singleton SCC
+    if (!bal(keep)) {
+      emit_one(i, d);
+      if (wmask && !err) {  // check_pending([dot])
+        if (lid == 0) wl(0) = d;
+        nwl = 1;
+        phase = PH_CHECK;
+      }
+      return;
+    }
+    const int sl = insert_vertex(i, d, keep, depj);
+    if (sl >= 0) dfs_start((uint32_t)sl, false);
+  }
+
+  __device__ __forceinline__ void run_slow() {
+    while (phase != PH_IDLE) {
+      if (phase == PH_DFS) dfs_iter();
+      else if (phase == PH_TRY) try_iter();
+      else check_iter();
+      if (err) phase = PH_IDLE;
+    }
+  }
+};
+
+// workgroup index -> logical workgroup: two consecutive logical workgroups
+// (8 streams = one 128-byte line of every input tile row) share an XCD
+// (hardware dispatch is round-robin over the 8 XCDs).
+__device__ __forceinline__ uint32_t logical_block(uint32_t b) {
+  const uint32_t x = b & 7u, j = b >> 3;
+  return 16u * (j >> 1) + 2u * x + (j & 1u);
+}
+
+__global__ __launch_bounds__(64 * WPB) void k_graph_wave(KArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t smem[WPB * LW];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = uni(threadIdx.x >> 6);
+  const uint32_t gg = logical_block(blockIdx.x) * WPB + w;  // stream index within the launch
+  if (gg >= a.num_lanes) return;  // whole wavefront
+  const uint32_t s = a.stream_map ? uni(a.stream_map[gg]) : gg;
+  const uint32_t len = a.lengths ? min(uni(a.lengths[s]), a.steps) : a.steps;
+  uint32_t* gst = a.state ? a.state + (size_t)gg * WPS : nullptr;
+
+  Wave e;
+  e.lid = lane;
+  e.lbit = 1ull << lane;
+  e.stream = s;
+  e.n = a.n;
+  e.steps = a.steps;
+  e.lds = smem + w * LW;
+  e.order = a.order;
+  e.release = a.release;
+
+  if (a.flags & FX_FLAG_INIT) {
+    if (a.init_frontier && lane < 8) e.cf = a.init_frontier[(size_t)s * 8 + lane];
+  } else {
+    const uint32_t* r = gst + lane * RREGS;
+    e.sdot = r[0];
+    e.srec = r[1];
+    e.swait = r[2];
+    e.stl = r[3];
+    e.sfr = r[4];
+    e.cf = r[5];
+    e.cw = r[6];
+    for (uint32_t q = lane; q < L_IN; q += 64) e.lds[q] = gst[S_LDS + q];
+    e.occ = (uint64_t)uni(gst[S_SCAL + 0]) | ((uint64_t)uni(gst[S_SCAL + 1]) << 32);
+    e.wmask = (uint64_t)uni(gst[S_SCAL + 2]) | ((uint64_t)uni(gst[S_SCAL + 3]) << 32);
+    e.k = uni(gst[S_SCAL + 4]);
+    e.err = uni(gst[S_SCAL + 5]);
+    e.epoch = uni(gst[S_SCAL + 6]);
+  }
+
+  const bool at_commit = (a.flags & FX_FLAG_EXECUTE_AT_COMMIT) != 0;
+  const uint32_t dmax = a.dmax;
+  const uint32_t steps4 = (a.steps + 3) >> 2;
+  const size_t soff = (size_t)(s >> 6) * steps4 * 256 + ((s & 63u) << 2);
+  // lane 4p+b fetches plane p (0 dot, 1 hdr, 2+j dep j) of block b of a chunk
+  const uint32_t pl = lane >> 2, bq = lane & 3u;
+  const uint32_t* src = pl == 0 ? a.dot
+                      : pl == 1 ? a.hdr
+                      : (dmax ? a.deps + (size_t)min(pl - 2u, dmax - 1u) * a.plane : a.dot);
+  src += soff;
+  const uint32_t b_last = steps4 ? steps4 - 1 : 0;
+  uint32_t* in = e.lds + L_IN;
+  const uint32_t c_begin = a.step_begin / CH;
+  const uint32_t c_end = (min(a.step_end, len) + CH - 1) / CH;
+
+  uint4 nxt = make_uint4(0, 0, 0, 0);
+  if (c_begin < c_end)
+    nxt = *reinterpret_cast<const uint4*>(src + (size_t)min(c_begin * 4 + bq, b_last) * 256);
+  for (uint32_t c = c_begin; c < c_end && !e.err; ++c) {
+    *reinterpret_cast<uint4*>(in + pl * CH + bq * 4) = nxt;
+    nxt = *reinterpret_cast<const uint4*>(src + (size_t)min((c + 1) * 4 + bq, b_last) * 256);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t base = c * CH;
+    const uint32_t q0 = base < a.step_begin ? a.step_begin - base : 0u;
+    const uint32_t q1 = min(min(a.step_end, len) - base, CH);
+    for (uint32_t q = q0; q < q1; ++q) {
+      const uint32_t d = uni(in[q]);
+      const uint32_t h = uni(in[CH + q]);
+      const uint32_t depj = in[(2 + (lane < MAXD ? lane : 0u)) * CH + q];
+      e.step_start(base + q, d, h, depj, dmax, at_commit);
+      if (e.phase != PH_IDLE) e.run_slow();
+      if (e.err) break;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // vertices still pending have no release step (yet)
+  if (e.mine(e.occ)) a.release[e.at(e.srec & 0x03FFFFFFu)] = FX_RELEASE_NONE;
+  if (lane == 0) {
+    a.nexec[s] = e.k;
+    a.err[s] = e.err;
+  }
+  if (a.flags & FX_FLAG_SAVE_STATE) {
+    uint32_t* r = gst + lane * RREGS;
+    r[0] = e.sdot;
+    r[1] = e.srec;
+    r[2] = e.swait;
+    r[3] = e.stl;
+    r[4] = e.sfr;
+    r[5] = e.cf;
+    r[6] = e.cw;
+    for (uint32_t q = lane; q < L_IN; q += 64) gst[S_LDS + q] = e.lds[q];
+    if (lane == 0) {
+      gst[S_SCAL + 0] = (uint32_t)e.occ;
+      gst[S_SCAL + 1] = (uint32_t)(e.occ >> 32);
+      gst[S_SCAL + 2] = (uint32_t)e.wmask;
+      gst[S_SCAL + 3] = (uint32_t)(e.wmask >> 32);
+      gst[S_SCAL + 4] = e.k;
+      gst[S_SCAL + 5] = e.err;
+      gst[S_SCAL + 6] = e.epoch;
+    }
+  }
+}
+
+}  // namespace wav
+
+int launch_wave(const KArgs& a, hipStream_t stream) {
+  if (a.num_lanes == 0) return FX_OK;
+  if (a.dmax > wav::MAXD) return FX_ERR_INVALID_ARG;
+  const uint32_t lb = (a.num_lanes + wav::WPB - 1) / wav::WPB;  // logical workgroups
+  const uint32_t blocks = (lb + 15u) & ~15u;                     // whole XCD pairs
+  hipLaunchKernelGGL(wav::k_graph_wave, dim3(blocks), dim3(64 * wav::WPB), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
+}
+
+uint32_t wave_state_words_per_stream() { return wav::WPS; }
+
+size_t wave_state_bytes(uint32_t streams) {
+  const uint32_t lb = (streams + wav::WPB - 1) / wav::WPB;
+  return (size_t)(((lb + 15u) & ~15u) * wav::WPB) * wav::WPS * 4;
+}
+
+uint32_t wave_decode_pending(const uint32_t* st, uint32_t stream_in_launch, uint32_t* dots,
+                             uint32_t* waits, uint32_t cap) {
+  const uint32_t* b = st + (size_t)stream_in_launch * wav::WPS;
+  const uint64_t occ = (uint64_t)b[wav::S_SCAL + 0] | ((uint64_t)b[wav::S_SCAL + 1] << 32);
+  const uint64_t wm = (uint64_t)b[wav::S_SCAL + 2] | ((uint64_t)b[wav::S_SCAL + 3] << 32);
+  uint32_t c = 0;
+  for (uint32_t sl = 0; sl < wav::P; ++sl) {
+    if (!((occ >> sl) & 1u)) continue;
+    if (c < cap) {
+      dots[c] = b[sl * wav::RREGS + 0];
+      waits[c] = ((wm >> sl) & 1u) ? b[sl * wav::RREGS + 2] : 0u;
+    }
+    ++c;
+  }
+  return c;
+}
+
+}  // namespace fx

@@ -62,8 +62,11 @@ class BatchResult:
 
 
 def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096, tiered=True,
-              tier=0, init_frontier=None, metrics=True):
-    """Runs a host batch on the GPU; returns host outputs (BatchResult)."""
+              tier=None, init_frontier=None, metrics=True):
+    """Runs a host batch on the GPU; returns host outputs (BatchResult).
+
+    tiered: fx_batch_run_tiered starting at `tier` (None = FX_TIER_DEFAULT);
+    otherwise one fx_batch_execute launch at `tier` (None = FX_TIER_DEFAULT)."""
     lib = _lib.load()
     S, steps, pw = planes.S, planes.steps, planes.plane
     bufs = {}
@@ -85,8 +88,10 @@ def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096,
     flags = _lib.FX_FLAG_EXECUTE_AT_COMMIT if execute_at_commit else 0
     tier_counts = (ctypes.c_uint32 * _lib.FX_NUM_TIERS)()
     if tiered and init_frontier is None:
-        status = lib.fx_batch_run_tiered(ctypes.byref(inb), ctypes.byref(outb), flags, None, tier_counts)
+        tflags = flags | (_lib.first_tier_flag(tier) if tier is not None else 0)
+        status = lib.fx_batch_run_tiered(ctypes.byref(inb), ctypes.byref(outb), tflags, None, tier_counts)
     else:
+        tier = _lib.FX_TIER_DEFAULT if tier is None else tier
         front = None
         if init_frontier is not None:
             front = DeviceBuffer(S * 8 * 4)

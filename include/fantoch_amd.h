@@ -73,6 +73,10 @@ extern "C" {
 #define FX_FLAG_INIT 1u              /* start from an empty executor (else resume from state) */
 #define FX_FLAG_EXECUTE_AT_COMMIT 2u /* Config::execute_at_commit (executor.rs:72-73)    */
 #define FX_FLAG_SAVE_STATE 4u        /* write the executor state back for a later resume */
+/* fx_batch_run_tiered only: first tier = (flags >> FX_FLAG_TIER_SHIFT) & 7
+ * (0 = the default tier, FX_TIER_DEFAULT). */
+#define FX_FLAG_TIER_SHIFT 8u
+#define FX_FLAG_FIRST_TIER(t) ((((uint32_t)(t)) + 1u) << FX_FLAG_TIER_SHIFT)
 
 /* Plane layout.  Every per-(step, stream) array ("plane") is tiled in tiles
  * of 64 streams x 4 steps (1 KiB): element (step, stream) lives at
@@ -132,12 +136,14 @@ typedef struct fx_hist_batch {
 /* Executor tiers: capacity of the per-stream pending table and of the
  * executed-clock window above each source's frontier.  A stream that exceeds
  * its tier stops with FX_ERR_CAPACITY and is rerun at the next tier
- * (fx_batch_run_tiered escalates 0 -> 1 -> 2). */
+ * (fx_batch_run_tiered escalates 0 -> 1 -> 2, 3 -> 1 -> 2, 4 -> 2). */
 #define FX_TIER_GROUP 0      /* 16 lanes per stream: 16 pending, 8 cached deps, n <= 16 */
 #define FX_TIER_LDS_LARGE 1  /* lane per stream, LDS-resident: 32 pending, one wave per CU */
 #define FX_TIER_GLOBAL 2     /* lane per stream, HBM-resident: 64 pending, 1024-bit windows */
 #define FX_TIER_LANE 3       /* lane per stream, LDS-resident: 12 pending (alternative tier 0) */
-#define FX_NUM_TIERS 4
+#define FX_TIER_WAVE 4       /* one wavefront per stream: 64 pending, 8 cached deps, <= 14 deps */
+#define FX_NUM_TIERS 5
+#define FX_TIER_DEFAULT FX_TIER_GROUP
 
 typedef struct fx_tier_info {
   uint32_t max_sources;    /* n supported                                   */
@@ -180,8 +186,9 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out,
 int fx_batch_metrics(const fx_stream_batch* in, const fx_order_batch* out,
                      const fx_hist_batch* hists, void* hip_stream);
 
-/* Synchronous convenience driver: runs every stream at tier 0 and reruns the
- * streams that report FX_ERR_CAPACITY at tiers 1 and 2.  Device pointers.
+/* Synchronous convenience driver: runs every stream at the first tier
+ * (FX_TIER_DEFAULT unless FX_FLAG_FIRST_TIER(t) is set) and reruns the streams
+ * that report FX_ERR_CAPACITY up the escalation chain.  Device pointers.
  * Returns FX_OK when every stream finished with FX_OK. */
 int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out,
                         uint32_t flags, void* hip_stream, uint32_t* tier_counts);

@@ -95,12 +95,33 @@ def test_tier_reruns_happen_and_match(gpu):
     p = fs.synth_params(seed=5, n=5, instances=10, cmds=300, window=40, cycle_pct=70,
                         conflicts=(100,))
     planes = fs.synth_host(p)
-    res = fd.run_batch(planes)
-    assert res.tier_counts[1] > 0, res.tier_counts  # tier 0 overflowed and was rerun
+    res = fd.run_batch(planes, tier=0)
+    assert res.tier_counts[0] == planes.S
+    assert res.tier_counts[1] > 0, res.tier_counts  # the group tier overflowed: reruns
     assert_parity(planes, res)
 
 
-@pytest.mark.parametrize("tier", [0, 1, 2, 3])
+def test_capacity_is_reported_exactly(gpu):
+    """Streams that need more than 64 pending vertices (every tier's ceiling)
+    stop with FX_ERR_CAPACITY after the reruns; all others match the oracle."""
+    p = fs.synth_params(seed=5, n=5, instances=10, cmds=300, window=120, cycle_pct=70,
+                        conflicts=(100, 50))
+    planes = fs.synth_host(p)
+    res = fd.run_batch(planes, metrics=False)
+    o_order, o_rel, o_nexec, o_err, mp, _ = oracle_lib.batch_execute(planes, threads=8, stats=True)
+    over, fits = mp > 64, mp < 64
+    assert over.any() and fits.any()
+    assert np.all(res.err[over] == _lib.FX_ERR_CAPACITY)
+    assert np.all(res.err[fits] == 0) and np.all(o_err == 0)
+    for s in np.flatnonzero(fits):
+        idx = _lib.index(np.arange(int(o_nexec[s])), s, planes.steps)
+        assert res.nexec[s] == o_nexec[s]
+        assert np.array_equal(res.order[idx], o_order[idx])
+        ridx = _lib.index(np.arange(planes.steps), s, planes.steps)
+        assert np.array_equal(res.release[ridx], o_rel[ridx])
+
+
+@pytest.mark.parametrize("tier", [0, 1, 2, 3, 4])
 def test_each_tier_standalone(gpu, tier):
     p = fs.synth_params(seed=9, n=5, instances=20, cmds=150, window=6, cycle_pct=30)
     planes = fs.synth_host(p)
@@ -136,7 +157,7 @@ def test_ragged_lengths_and_truncated_streams(gpu):
     assert_parity(planes, res)
 
 
-@pytest.mark.parametrize("tier", [0, 1, 2, 3])
+@pytest.mark.parametrize("tier", [0, 1, 2, 3, 4])
 def test_chunked_resume_equals_one_shot(gpu, tier):
     import ctypes
     p = fs.synth_params(seed=8, n=5, instances=30, cmds=100, window=10, cycle_pct=30)
