@@ -62,6 +62,7 @@ def main():
     import torch.distributed as dist
 
     from fantoch_amd import _lib
+    from fantoch_amd import sharding
     from fantoch_amd import streams as fs
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -79,9 +80,8 @@ def main():
     conflicts = [int(c) for c in args.conflicts.split(",")]
     instances = args.seeds * len(conflicts)
     cblock = args.seeds if args.conflict_block < 0 else args.conflict_block
-    p = fs.synth_params(seed=args.seed, instances=instances, n=args.n, cmds=args.cmds,
-                        window=args.window, cycle_pct=args.cycle_pct, conflicts=conflicts,
-                        instance_base=rank * instances, conflict_block=cblock)
+    p = sharding.rank_params(rank, args.seeds, conflicts, args.n, args.cmds, args.window,
+                             args.cycle_pct, args.seed, args.conflict_block)
     S, steps, dmax = fs.synth_shape(p)
     pw = _lib.plane_words(S, steps)
     stream = torch.cuda.current_stream(dev)
@@ -130,8 +130,7 @@ def main():
         _lib.check(lib.fx_batch_metrics(ctypes.byref(inb), ctypes.byref(outb), ctypes.byref(hb), hs),
                    "metrics")
         if world > 1:
-            dist.all_reduce(chain)
-            dist.all_reduce(delay)
+            sharding.allreduce_histograms(dist, chain, delay)
 
     # warmup (+ decide whether any stream needs a tier rerun)
     for w in range(max(args.warmup, 1)):
@@ -191,7 +190,8 @@ def main():
             if os.path.exists(args.traffic_json):
                 try:
                     tj = json.load(open(args.traffic_json))
-                    if tj.get("workload_key") == workload_key(args):
+                    if tj.get("workload_key") == workload_key(args) and \
+                            tj.get("kernel") == KERNEL_NAMES.get(tier):
                         traffic = tj.get("hbm_bytes_per_launch")
                 except Exception:
                     traffic = None
