@@ -28,9 +28,10 @@ sys.path.insert(0, ROOT)
 METRIC = "executed cmds/sec (node) for batched Atlas/EPaxos sims; % of HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KERNEL_NAMES = {0: "k_graph_group", 1: "k_graph_exec<Tier1>", 2: "k_graph_exec<Tier2>",
-                3: "k_graph_exec<TierLane>", 4: "k_graph_wave"}
+                3: "k_graph_exec<TierLane>", 4: "k_graph_wave", 5: "k_graph_lane"}
 LAYOUT = {0: "16 lanes per stream", 1: "one lane per stream", 2: "one lane per stream",
-          3: "one lane per stream", 4: "one wavefront per stream"}
+          3: "one lane per stream", 4: "one wavefront per stream",
+          5: "one lane per stream (register slot table, independent lane progress)"}
 
 
 def parse():

@@ -34,8 +34,9 @@ FX_RELEASE_NONE = 0xFFFFFFFF
 FX_FLAG_INIT = 1
 FX_FLAG_EXECUTE_AT_COMMIT = 2
 FX_FLAG_SAVE_STATE = 4
-FX_NUM_TIERS = 5
+FX_NUM_TIERS = 6
 FX_TIER_WAVE = 4
+FX_TIER_LANE_REG = 5
 FX_TIER_DEFAULT = 0  # FX_TIER_GROUP
 FX_FLAG_TIER_SHIFT = 8
 

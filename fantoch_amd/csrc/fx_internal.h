@@ -23,6 +23,7 @@ struct KArgs {
   uint32_t* state;
   uint32_t step_begin, step_end, flags;
   const uint32_t* init_frontier;
+  uint32_t* dbg;  // per-lane diagnostic counters (FX_LANE_DEBUG), normally null
 };
 
 // Lane-per-stream executor tiers (graph_exec.hip) and the 16-lanes-per-stream
@@ -47,6 +48,16 @@ constexpr uint32_t WAVE_SLOTS = 64;        // pending vertices per stream (one p
 constexpr uint32_t WAVE_CACHE = 8;         // cached deps per pending vertex
 constexpr uint32_t WAVE_WINDOW_BITS = 32;  // executed-clock window per source
 constexpr uint32_t WAVE_MAX_DEPS = 14;     // dep planes read per Add
+
+// Lane-per-stream tier with a register-resident slot table (graph_lane.hip).
+int launch_lane(const KArgs& a, hipStream_t stream);
+size_t lane_state_bytes(uint32_t streams);
+uint32_t lane_state_words_per_stream();
+uint32_t lane_decode_pending(const uint32_t* block, uint32_t lane, uint32_t* dots, uint32_t* waits,
+                             uint32_t cap);
+constexpr uint32_t LANE_SLOTS = 12;         // pending vertices per stream
+constexpr uint32_t LANE_MAX_DEPS = 8;       // dep planes (and cached deps per vertex)
+constexpr uint32_t LANE_WINDOW_BITS = 32;   // executed-clock window per source
 
 // Decodes the pending vertices of lane `lane` from a saved state block
 // (tier layout of graph_exec.hip).  Writes up to cap (dot, waiting_on) pairs;

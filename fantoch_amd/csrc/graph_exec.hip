@@ -882,6 +882,7 @@ uint32_t decode_pending(uint32_t tier, const uint32_t* block, uint32_t lane, uin
     case 2: return decode_pending_t<Tier2>(block, lane, dots, waits, cap);
     case 3: return decode_pending_t<TierLane>(block, lane, dots, waits, cap);
     case 4: return wave_decode_pending(block, lane, dots, waits, cap);
+    case 5: return lane_decode_pending(block, lane, dots, waits, cap);
     default: return 0;
   }
 }
@@ -925,6 +926,7 @@ int fx_tier_query(uint32_t tier, uint32_t n, fx_tier_info* out) {
     case 2: *out = {Tier2::NSRC, Tier2::P, 32 * Tier2::XW, Tier2::WORDS}; break;
     case 3: *out = {TierLane::NSRC, TierLane::P, 32 * TierLane::XW, TierLane::WORDS}; break;
     case 4: *out = {8, WAVE_SLOTS, WAVE_WINDOW_BITS, wave_state_words_per_stream()}; break;
+    case 5: *out = {8, LANE_SLOTS, LANE_WINDOW_BITS, lane_state_words_per_stream()}; break;
     default: return FX_ERR_INVALID_ARG;
   }
   return n >= 1 && n <= out->max_sources ? FX_OK : FX_ERR_INVALID_ARG;
@@ -938,6 +940,7 @@ size_t fx_batch_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes) {
     case 2: return state_bytes<Tier2>(lanes);
     case 3: return state_bytes<TierLane>(lanes);
     case 4: return wave_state_bytes(lanes);
+    case 5: return lane_state_bytes(lanes);
     default: return 0;
   }
 }
@@ -982,6 +985,7 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
   a.step_end = step_end;
   a.flags = flags;
   a.init_frontier = init_frontier;
+  a.dbg = nullptr;
   hipStream_t hs = (hipStream_t)hip_stream;
   if (g_profile) {
     if (!g_ev0) {
@@ -995,6 +999,7 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
     case 2: st = launch_exec<Tier2>(a, hs); break;
     case 3: st = launch_exec<TierLane>(a, hs); break;
     case 4: st = launch_wave(a, hs); break;
+    case 5: st = launch_lane(a, hs); break;
     default: return FX_ERR_INVALID_ARG;
   }
   if (g_profile) {
@@ -1115,6 +1120,7 @@ static uint32_t escalate(uint32_t tier) {
     case FX_TIER_LANE: return FX_TIER_LDS_LARGE;
     case FX_TIER_LDS_LARGE: return FX_TIER_GLOBAL;
     case FX_TIER_WAVE: return FX_TIER_GLOBAL;
+    case FX_TIER_LANE_REG: return FX_TIER_LDS_LARGE;
     default: return FX_NUM_TIERS;
   }
 }
@@ -1134,7 +1140,8 @@ int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out, ui
   uint32_t first = ft ? ft - 1u : (uint32_t)FX_TIER_DEFAULT;
   if (first >= FX_NUM_TIERS) return FX_ERR_INVALID_ARG;
   // tiers that cannot hold the widest Add start one step up the chain
-  if ((first == FX_TIER_WAVE && in->dmax > WAVE_MAX_DEPS) || (first == FX_TIER_GROUP && in->dmax > GROUP_LANES))
+  if ((first == FX_TIER_WAVE && in->dmax > WAVE_MAX_DEPS) || (first == FX_TIER_GROUP && in->dmax > GROUP_LANES) ||
+      (first == FX_TIER_LANE_REG && in->dmax > LANE_MAX_DEPS))
     first = FX_TIER_LDS_LARGE;
   void* st1 = nullptr;
   if (first == FX_TIER_GLOBAL && hipMalloc(&st1, fx_batch_state_bytes(first, in->n, S)) != hipSuccess)

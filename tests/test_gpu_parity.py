@@ -91,6 +91,19 @@ def test_synthetic_parity(gpu, case):
     assert np.array_equal(res.delay, delay)
 
 
+@pytest.mark.parametrize("case", SYNTH_CASES)
+def test_synthetic_parity_lane_reg_first(gpu, case):
+    """Tier 5 (register slot table) as the first tier, reruns 5 -> 1 -> 2."""
+    p = fs.synth_params(seed=12, **case)
+    planes = fs.synth_host(p)
+    res = fd.run_batch(planes, tier=_lib.FX_TIER_LANE_REG, nbins_chain=64, nbins_delay=2048)
+    o_order, o_rel, o_nexec = assert_parity(planes, res)
+    assert res.status == _lib.FX_OK
+    chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 64, 2048)
+    assert np.array_equal(res.chain, chain)
+    assert np.array_equal(res.delay, delay)
+
+
 def test_tier_reruns_happen_and_match(gpu):
     p = fs.synth_params(seed=5, n=5, instances=10, cmds=300, window=40, cycle_pct=70,
                         conflicts=(100,))
@@ -121,7 +134,7 @@ def test_capacity_is_reported_exactly(gpu):
         assert np.array_equal(res.release[ridx], o_rel[ridx])
 
 
-@pytest.mark.parametrize("tier", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("tier", [0, 1, 2, 3, 4, 5])
 def test_each_tier_standalone(gpu, tier):
     p = fs.synth_params(seed=9, n=5, instances=20, cmds=150, window=6, cycle_pct=30)
     planes = fs.synth_host(p)
@@ -157,7 +170,7 @@ def test_ragged_lengths_and_truncated_streams(gpu):
     assert_parity(planes, res)
 
 
-@pytest.mark.parametrize("tier", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("tier", [0, 1, 2, 3, 4, 5])
 def test_chunked_resume_equals_one_shot(gpu, tier):
     import ctypes
     p = fs.synth_params(seed=8, n=5, instances=30, cmds=100, window=10, cycle_pct=30)
