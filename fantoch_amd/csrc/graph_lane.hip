@@ -108,15 +108,18 @@ __device__ __forceinline__ uint32_t cdep_dot(uint32_t w) {
 
 template <uint32_t NS, uint32_t DC>
 struct Lane {
-  // LDS words of a lane (word w at lds[w * 64], so every lane hits its own bank)
-  static constexpr uint32_t L_DEP = 0;            // [P][DC] cached deps
-  static constexpr uint32_t L_TW = P * DC;        // [P] Tarjan words
+  // LDS words of a lane (word w at lds[w * 64], so every lane hits its own bank);
+  // the clock rows are u64 (frontier | window << 32) at clk[si * 64] so one
+  // ds_read_b64 fetches a source's state
+  static constexpr uint32_t L_CLK = 0;            // [NS] u64 clock rows (2 words each)
+  static constexpr uint32_t L_DEP = 2 * NS;       // [P][DC] cached deps
+  static constexpr uint32_t L_TW = L_DEP + P * DC;  // [P] Tarjan words
   static constexpr uint32_t L_REC = L_TW + P;     // [P] arrival index | ncached << 26
   static constexpr uint32_t L_WL = L_REC + P;     // worklist: u16 masks, two per word
   static constexpr uint32_t LW = L_WL + (WLC + 1) / 2;
 
   uint32_t* lds;
-  uint32_t cf[NS], cw[NS];  // executed clock: frontier / exception window per source
+  uint64_t* clk;            // this lane's clock row 0 (row si at clk[si * 64])
   uint32_t sd[P], sw[P];    // slot dot / dot the slot is registered on (matched in parallel)
   uint32_t occ = 0, wmask = 0, tmask = 0;
   uint64_t stk = 0;         // Tarjan stack: slot nibbles, entry j at bits 4j
@@ -137,20 +140,23 @@ struct Lane {
   __device__ __forceinline__ size_t at(uint32_t step) const { return fx_index(step, stream, steps); }
 
   // ------------------------------------------------------------ clock
-  // AEClock::contains (tarjan.rs:131-132)
-  __device__ __forceinline__ bool contains(uint32_t d) const {
+  // AEClock (threshold 0.9.1) per source: frontier f + exception bits above it
+  __device__ __forceinline__ uint64_t& crow(uint32_t si) { return clk[(si < NS ? si : NS - 1) * WV]; }
+  // AEClock::contains (tarjan.rs:131-132) given the source's row
+  __device__ __forceinline__ bool row_contains(uint64_t row, uint32_t d) const {
     const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
-    const uint32_t oh = 1u << (si & 31u);
-    const uint32_t f = oget(cf, oh), wv = oget(cw, oh);
+    const uint32_t f = (uint32_t)row, wv = (uint32_t)(row >> 32);
     const uint32_t seq = d & FX_SEQ_MASK, off = seq - f - 1u;
     return si < n && (seq <= f || (off < 32u && ((wv >> (off & 31u)) & 1u)));
   }
+  __device__ __forceinline__ bool contains(uint32_t d) { return row_contains(crow((d >> FX_SEQ_BITS) - 1u), d); }
   // AEClock::add (tarjan.rs:293)
   __device__ __forceinline__ void clk_add(uint32_t d) {
     const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
     if (si >= n) { err = FX_ERR_DOT_RANGE; return; }
-    const uint32_t oh = 1u << si;
-    uint32_t f = oget(cf, oh), wv = oget(cw, oh);
+    uint64_t& row = crow(si);
+    const uint64_t r0 = row;
+    uint32_t f = (uint32_t)r0, wv = (uint32_t)(r0 >> 32);
     const uint32_t seq = d & FX_SEQ_MASK;
     if (seq <= f) return;
     const uint32_t off = seq - f - 1u;
@@ -163,8 +169,7 @@ struct Lane {
       f = f + 1 + ones;
       wv = win >> ones;
     }
-    oput(cf, oh, f);
-    oput(cw, oh, wv);
+    row = (uint64_t)f | ((uint64_t)wv << 32);
   }
 
   // ------------------------------------------------------ slot table
@@ -349,10 +354,13 @@ struct Lane {
       hi = fnc;
     }
     // ---- B: executed-clock tests (AEClock::contains, tarjan.rs:131-132)
+    uint64_t rows[DC];
+#pragma unroll
+    for (uint32_t j = 0; j < DC; ++j) rows[j] = crow((vec[j] >> FX_SEQ_BITS) - 1u);
     uint32_t notex = 0;
 #pragma unroll
     for (uint32_t j = 0; j < DC; ++j)
-      if (j >= lo && j < hi && !(start && vec[j] == d) && !contains(vec[j])) notex |= 1u << j;
+      if (j >= lo && j < hi && !(start && vec[j] == d) && !row_contains(rows[j], vec[j])) notex |= 1u << j;
     // ---- C: one slot lookup (VertexIndex, index.rs:18-51)
     const uint32_t jn = notex ? __builtin_ctz(notex) : 0u;
     uint32_t x1 = d;
@@ -497,10 +505,8 @@ struct Lane {
       tw(q) = g[(3 * P + q) * WV];
     }
 #pragma unroll
-    for (uint32_t q = 0; q < NS; ++q) {
-      cf[q] = g[(S_CLK + q) * WV];
-      cw[q] = g[(S_CLK + 8 + q) * WV];
-    }
+    for (uint32_t q = 0; q < NS; ++q)
+      clk[q * WV] = (uint64_t)g[(S_CLK + q) * WV] | ((uint64_t)g[(S_CLK + 8 + q) * WV] << 32);
     for (uint32_t sl = 0; sl < P; ++sl)
       for (uint32_t j = 0; j < DC; ++j) w(L_DEP + sl * DC + j) = g[(S_DEP + sl * 8 + j) * WV];
     for (uint32_t q = 0; q < (WLC + 1) / 2; ++q) w(L_WL + q) = g[(S_WL + q) * WV];
@@ -520,8 +526,8 @@ struct Lane {
     }
 #pragma unroll
     for (uint32_t q = 0; q < NS; ++q) {
-      g[(S_CLK + q) * WV] = cf[q];
-      g[(S_CLK + 8 + q) * WV] = cw[q];
+      g[(S_CLK + q) * WV] = (uint32_t)clk[q * WV];
+      g[(S_CLK + 8 + q) * WV] = (uint32_t)(clk[q * WV] >> 32);
     }
     for (uint32_t sl = 0; sl < P; ++sl)
       for (uint32_t j = 0; j < DC; ++j) g[(S_DEP + sl * 8 + j) * WV] = w(L_DEP + sl * DC + j);
@@ -548,6 +554,7 @@ void k_graph_lane(KArgs a) {
 
   L e;
   e.lds = smem + lane;
+  e.clk = reinterpret_cast<uint64_t*>(smem + L::L_CLK * WV) + lane;
   e.stream = s;
   e.n = a.n;
   e.steps = a.steps;
@@ -555,13 +562,10 @@ void k_graph_lane(KArgs a) {
   e.release = a.release;
 #pragma unroll
   for (uint32_t q = 0; q < P; ++q) e.sd[q] = e.sw[q] = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < NS; ++q) e.cf[q] = e.cw[q] = 0;
   if (a.flags & FX_FLAG_INIT) {
-    if (a.init_frontier && active) {
 #pragma unroll
-      for (uint32_t q = 0; q < NS; ++q) e.cf[q] = a.init_frontier[(size_t)s * 8 + q];
-    }
+    for (uint32_t q = 0; q < NS; ++q)
+      e.clk[q * WV] = (a.init_frontier && active) ? a.init_frontier[(size_t)s * 8 + q] : 0u;
   } else if (active) {
     e.load_state(gst);
   }
