@@ -28,10 +28,13 @@ sys.path.insert(0, ROOT)
 METRIC = "executed cmds/sec (node) for batched Atlas/EPaxos sims; % of HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KERNEL_NAMES = {0: "k_graph_group", 1: "k_graph_exec<Tier1>", 2: "k_graph_exec<Tier2>",
-                3: "k_graph_exec<TierLane>", 4: "k_graph_wave", 5: "k_graph_lane"}
+                3: "k_graph_exec<TierLane>", 4: "k_graph_wave", 5: "k_graph_lane",
+                6: "k_graph_group||k_graph_lane"}
 LAYOUT = {0: "16 lanes per stream", 1: "one lane per stream", 2: "one lane per stream",
           3: "one lane per stream", 4: "one wavefront per stream",
-          5: "one lane per stream (register slot table, independent lane progress)"}
+          5: "one lane per stream (register slot table, independent lane progress)",
+          6: "per 64-stream tile: 16 lanes per stream for dense tiles, one lane per stream "
+             "for sparse ones, both kernels concurrent"}
 
 
 def parse():
@@ -117,6 +120,9 @@ def main():
     tier = _lib.FX_TIER_DEFAULT if args.tier < 0 else args.tier
     tiered = [False]
     tier_counts = (ctypes.c_uint32 * _lib.FX_NUM_TIERS)()
+    scratch = None
+    if tier in (2, _lib.FX_TIER_SPLIT):  # working memory of the HBM tier / split scratch
+        scratch = buf((lib.fx_batch_state_bytes(tier, args.n, S) + 3) // 4)
 
     def step():
         chain.zero_()
@@ -125,7 +131,8 @@ def main():
             st = lib.fx_batch_run_tiered(ctypes.byref(inb), ctypes.byref(outb),
                                          _lib.first_tier_flag(tier), hs, tier_counts)
         else:
-            st = lib.fx_batch_execute(ctypes.byref(inb), ctypes.byref(outb), tier, None, S, None, 0,
+            st = lib.fx_batch_execute(ctypes.byref(inb), ctypes.byref(outb), tier, None, S,
+                                      scratch.data_ptr() if scratch is not None else None, 0,
                                       steps, _lib.FX_FLAG_INIT, None, hs)
         _lib.check(st, "executor")
         _lib.check(lib.fx_batch_metrics(ctypes.byref(inb), ctypes.byref(outb), ctypes.byref(hb), hs),
@@ -249,45 +256,57 @@ def workload_key(args):
 
 def cpu_baseline(args, lib, dot, hdr, deps, order, release, nexec, S, steps, dmax, pw):
     """Times the CPU oracle (C++ restatement of the reference GraphExecutor) on a
-    bounded prefix of the same batch, with std::threads over streams like the
-    reference's rayon par_iter, and checks that prefix against the GPU output."""
+    bounded sample of the same batch, with std::threads over streams like the
+    reference's rayon par_iter, and checks the sample against the GPU output.
+    The sample is whole 64-stream tiles spread evenly over the batch, so every
+    conflict rate is represented in its batch proportion."""
     import numpy as np
+    import torch
     from fantoch_amd import streams as fs
     from oracle import oracle_lib
 
     threads = max(1, min(16, os.cpu_count() or 1))
-    # calibrate: ~2M Adds/s per thread -> pick whole tiles of 64 streams
-    budget_adds = args.cpu_baseline_seconds * 2.0e6 * threads
-    tiles = int(max(1, min((S + 63) // 64, budget_adds // (64 * steps))))
-    Ss = min(S, tiles * 64)
+    full_tiles = S // 64
+    if full_tiles == 0:
+        return None
+    # calibrate: ~1M Adds/s per thread over the mixed batch -> whole tiles
+    budget_adds = args.cpu_baseline_seconds * 1.0e6 * threads
+    tiles = int(max(1, min(full_tiles, budget_adds // (64 * steps))))
+    pick = np.unique(np.linspace(0, full_tiles - 1, tiles).round().astype(np.int64))
+    tiles = len(pick)
+    Ss = tiles * 64
     steps4 = (steps + 3) // 4
-    words = tiles * steps4 * 256
-    to_np = lambda t, off, cnt: t[off:off + cnt].cpu().numpy().view(np.uint32)
+    tw = steps4 * 256  # words per tile and plane
+    idx = torch.from_numpy((pick[:, None] * tw + np.arange(tw)[None, :]).reshape(-1)).to(dot.device)
+    gather = lambda t, base: t[base + idx].cpu().numpy().view(np.uint32)
     planes = fs.Planes(Ss, steps, dmax, args.n)
-    planes.dot[:] = to_np(dot, 0, words)[:planes.plane]
-    planes.hdr[:] = to_np(hdr, 0, words)[:planes.plane]
+    planes.dot[:] = gather(dot, 0)[:planes.plane]
+    planes.hdr[:] = gather(hdr, 0)[:planes.plane]
     for j in range(dmax):
-        planes.deps[j * planes.plane:(j + 1) * planes.plane] = to_np(deps, j * pw, words)[:planes.plane]
+        planes.deps[j * planes.plane:(j + 1) * planes.plane] = gather(deps, j * pw)[:planes.plane]
     t0 = time.perf_counter()
     o_order, o_rel, o_nexec, o_err = oracle_lib.batch_execute(planes, threads=threads)
     dt = time.perf_counter() - t0
     executed = int(o_nexec.sum())
-    g_order = to_np(order, 0, words)
-    g_rel = to_np(release, 0, words)
-    g_nexec = nexec[:Ss].cpu().numpy().view(np.uint32)
+    g_order = gather(order, 0)
+    g_rel = gather(release, 0)
+    sidx = torch.from_numpy((pick[:, None] * 64 + np.arange(64)[None, :]).reshape(-1)).to(dot.device)
+    g_nexec = nexec[sidx].cpu().numpy().view(np.uint32)
     parity = bool(np.array_equal(g_nexec, o_nexec))
     if parity:
         for s in range(Ss):
-            idx = fs.index(np.arange(int(o_nexec[s])), s, steps)
-            if not np.array_equal(g_order[idx], o_order[idx]):
+            ix = fs.index(np.arange(int(o_nexec[s])), s, steps)
+            if not np.array_equal(g_order[ix], o_order[ix]):
                 parity = False
                 break
         ridx = np.concatenate([fs.index(np.arange(steps), s, steps) for s in range(Ss)])
         parity = parity and bool(np.array_equal(g_rel[ridx], o_rel[ridx]))
     return {"value": round(executed / dt, 1), "unit": "cmds/s", "cores": threads, "kind": "port",
-            "sample": "first %d streams (%d Adds) of the same batch, %.2f s wall on %d threads; "
-                      "GPU output on the sample %s the oracle bit-for-bit"
-                      % (Ss, Ss * steps, dt, threads, "matches" if parity else "DIFFERS FROM"),
+            "sample": "%d of %d 64-stream tiles spread evenly over the batch (%d streams, %d Adds, "
+                      "every conflict rate in proportion), %.2f s wall on %d threads; GPU output "
+                      "on the sample %s the oracle bit-for-bit"
+                      % (tiles, full_tiles, Ss, Ss * steps, dt, threads,
+                         "matches" if parity else "DIFFERS FROM"),
             "sample_parity": parity}
 
 

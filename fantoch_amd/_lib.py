@@ -34,10 +34,12 @@ FX_RELEASE_NONE = 0xFFFFFFFF
 FX_FLAG_INIT = 1
 FX_FLAG_EXECUTE_AT_COMMIT = 2
 FX_FLAG_SAVE_STATE = 4
-FX_NUM_TIERS = 6
+FX_NUM_TIERS = 7
+FX_TIER_GROUP = 0
 FX_TIER_WAVE = 4
 FX_TIER_LANE_REG = 5
-FX_TIER_DEFAULT = 0  # FX_TIER_GROUP
+FX_TIER_SPLIT = 6
+FX_TIER_DEFAULT = FX_TIER_SPLIT
 FX_FLAG_TIER_SHIFT = 8
 
 

@@ -76,7 +76,7 @@ struct fx_graph_executor {
   uint32_t dmax = 0;     // dep planes in use
   uint32_t uploaded = 0; // rows present on the device
   DevBuf d_dot, d_hdr, d_deps, d_order, d_release, d_nexec, d_err, d_state;
-  uint32_t tier = FX_TIER_DEFAULT;
+  uint32_t tier = FX_TIER_GROUP;  // one resumable stream: a tier with saved state
   uint32_t processed = 0;  // steps executed by the device state
   uint32_t consumed = 0;   // order entries already converted
 

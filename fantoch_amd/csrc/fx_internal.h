@@ -24,6 +24,7 @@ struct KArgs {
   uint32_t step_begin, step_end, flags;
   const uint32_t* init_frontier;
   uint32_t* dbg;  // per-lane diagnostic counters (FX_LANE_DEBUG), normally null
+  const uint32_t* lanes_dev;  // device lane count (FX_TIER_SPLIT sub-launches), normally null
 };
 
 // Lane-per-stream executor tiers (graph_exec.hip) and the 16-lanes-per-stream
@@ -58,6 +59,13 @@ uint32_t lane_decode_pending(const uint32_t* block, uint32_t lane, uint32_t* dot
 constexpr uint32_t LANE_SLOTS = 12;         // pending vertices per stream
 constexpr uint32_t LANE_MAX_DEPS = 8;       // dep planes (and cached deps per vertex)
 constexpr uint32_t LANE_WINDOW_BITS = 32;   // executed-clock window per source
+
+// FX_TIER_SPLIT (graph_split.hip): per-tile choice between the group and the
+// lane tier, both launched concurrently.
+int launch_split(const KArgs& a, void* scratch, hipStream_t stream);
+size_t split_scratch_bytes(uint32_t streams);
+constexpr uint32_t SPLIT_DEFAULT_THRESHOLD = 16;  // mean deps per Add x 8 at or above which
+                                                  // a tile runs on the group tier
 
 // Decodes the pending vertices of lane `lane` from a saved state block
 // (tier layout of graph_exec.hip).  Writes up to cap (dot, waiting_on) pairs;

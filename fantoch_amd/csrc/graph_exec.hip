@@ -927,6 +927,7 @@ int fx_tier_query(uint32_t tier, uint32_t n, fx_tier_info* out) {
     case 3: *out = {TierLane::NSRC, TierLane::P, 32 * TierLane::XW, TierLane::WORDS}; break;
     case 4: *out = {8, WAVE_SLOTS, WAVE_WINDOW_BITS, wave_state_words_per_stream()}; break;
     case 5: *out = {8, LANE_SLOTS, LANE_WINDOW_BITS, lane_state_words_per_stream()}; break;
+    case 6: *out = {8, std::min(LANE_SLOTS, GROUP_SLOTS), std::min(LANE_WINDOW_BITS, GROUP_WINDOW_BITS), 0}; break;
     default: return FX_ERR_INVALID_ARG;
   }
   return n >= 1 && n <= out->max_sources ? FX_OK : FX_ERR_INVALID_ARG;
@@ -941,6 +942,7 @@ size_t fx_batch_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes) {
     case 3: return state_bytes<TierLane>(lanes);
     case 4: return wave_state_bytes(lanes);
     case 5: return lane_state_bytes(lanes);
+    case 6: return split_scratch_bytes(lanes);  // scheduling scratch, not resumable state
     default: return 0;
   }
 }
@@ -964,6 +966,11 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
   if (!(flags & FX_FLAG_INIT) && !state) return FX_ERR_INVALID_ARG;
   if ((flags & FX_FLAG_SAVE_STATE) && !state) return FX_ERR_INVALID_ARG;
   if (!stream_map && num_lanes > in->num_streams) return FX_ERR_INVALID_ARG;
+  // the split tier schedules whole batches: no map, no resumable state
+  if (tier == FX_TIER_SPLIT &&
+      (stream_map || num_lanes != in->num_streams || !state || !(flags & FX_FLAG_INIT) ||
+       (flags & FX_FLAG_SAVE_STATE)))
+    return FX_ERR_INVALID_ARG;
   KArgs a;
   a.dot = in->dot;
   a.hdr = in->hdr;
@@ -986,6 +993,7 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
   a.flags = flags;
   a.init_frontier = init_frontier;
   a.dbg = nullptr;
+  a.lanes_dev = nullptr;
   hipStream_t hs = (hipStream_t)hip_stream;
   if (g_profile) {
     if (!g_ev0) {
@@ -1000,6 +1008,7 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
     case 3: st = launch_exec<TierLane>(a, hs); break;
     case 4: st = launch_wave(a, hs); break;
     case 5: st = launch_lane(a, hs); break;
+    case 6: st = launch_split(a, state, hs); break;
     default: return FX_ERR_INVALID_ARG;
   }
   if (g_profile) {
@@ -1121,6 +1130,7 @@ static uint32_t escalate(uint32_t tier) {
     case FX_TIER_LDS_LARGE: return FX_TIER_GLOBAL;
     case FX_TIER_WAVE: return FX_TIER_GLOBAL;
     case FX_TIER_LANE_REG: return FX_TIER_LDS_LARGE;
+    case FX_TIER_SPLIT: return FX_TIER_LDS_LARGE;
     default: return FX_NUM_TIERS;
   }
 }
@@ -1140,11 +1150,12 @@ int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out, ui
   uint32_t first = ft ? ft - 1u : (uint32_t)FX_TIER_DEFAULT;
   if (first >= FX_NUM_TIERS) return FX_ERR_INVALID_ARG;
   // tiers that cannot hold the widest Add start one step up the chain
-  if ((first == FX_TIER_WAVE && in->dmax > WAVE_MAX_DEPS) || (first == FX_TIER_GROUP && in->dmax > GROUP_LANES) ||
+  if ((first == FX_TIER_WAVE && in->dmax > WAVE_MAX_DEPS) ||
+      ((first == FX_TIER_GROUP || first == FX_TIER_SPLIT) && in->dmax > GROUP_LANES) ||
       (first == FX_TIER_LANE_REG && in->dmax > LANE_MAX_DEPS))
     first = FX_TIER_LDS_LARGE;
   void* st1 = nullptr;
-  if (first == FX_TIER_GLOBAL && hipMalloc(&st1, fx_batch_state_bytes(first, in->n, S)) != hipSuccess)
+  if ((first == FX_TIER_GLOBAL || first == FX_TIER_SPLIT) && hipMalloc(&st1, fx_batch_state_bytes(first, in->n, S)) != hipSuccess)
     return FX_ERR_HIP;
   st = fx_batch_execute(in, out, first, nullptr, S, st1, 0, in->steps, flags, nullptr, hip_stream);
   if (st1) (void)hipFree(st1);

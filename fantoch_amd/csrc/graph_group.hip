@@ -369,8 +369,12 @@ __global__ __launch_bounds__(64) void k_graph_group(KArgs a) {
   const uint32_t lane = threadIdx.x;
   const uint32_t g = lane / G;
   const uint32_t gg = blockIdx.x * SPW + g;  // stream index within the launch
-  const bool active = gg < a.num_lanes;
-  const uint32_t s = active ? (a.stream_map ? a.stream_map[gg] : gg) : 0u;
+  const uint32_t nl = a.lanes_dev ? min(a.num_lanes, *a.lanes_dev) : a.num_lanes;
+  if (blockIdx.x * SPW >= nl) return;  // wavefront past a device-side lane count
+  // map entries >= S are padding lanes (FX_TIER_SPLIT's ragged last tile)
+  const uint32_t s0 = gg < nl ? (a.stream_map ? a.stream_map[gg] : gg) : 0xFFFFFFFFu;
+  const bool active = s0 < a.S;
+  const uint32_t s = active ? s0 : 0u;
   const uint32_t len = active ? (a.lengths ? min(a.lengths[s], a.steps) : a.steps) : 0u;
   uint32_t* gst = a.state ? a.state + (size_t)gg * WPS : nullptr;
 

@@ -547,8 +547,12 @@ void k_graph_lane(KArgs a) {
   static_assert(L::LW <= 160, "LDS words per lane");
   const uint32_t lane = threadIdx.x;
   const uint32_t gl = blockIdx.x * WV + lane;
-  const bool active = gl < a.num_lanes;
-  const uint32_t s = active ? (a.stream_map ? a.stream_map[gl] : gl) : 0u;
+  const uint32_t nl = a.lanes_dev ? min(a.num_lanes, *a.lanes_dev) : a.num_lanes;
+  if (blockIdx.x * WV >= nl) return;  // wavefront past a device-side lane count
+  // map entries >= S are padding lanes (FX_TIER_SPLIT's ragged last tile)
+  const uint32_t s0 = gl < nl ? (a.stream_map ? a.stream_map[gl] : gl) : 0xFFFFFFFFu;
+  const bool active = s0 < a.S;
+  const uint32_t s = active ? s0 : 0u;
   const uint32_t len = active ? (a.lengths ? min(a.lengths[s], a.steps) : a.steps) : 0u;
   uint32_t* gst = a.state ? a.state + (size_t)blockIdx.x * WORDS * WV + lane : nullptr;
 

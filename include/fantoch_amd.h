@@ -136,16 +136,21 @@ typedef struct fx_hist_batch {
 /* Executor tiers: capacity of the per-stream pending table and of the
  * executed-clock window above each source's frontier.  A stream that exceeds
  * its tier stops with FX_ERR_CAPACITY and is rerun at the next tier
- * (fx_batch_run_tiered escalates 0 -> 1 -> 2, 3 -> 1 -> 2, 4 -> 2, 5 -> 1 -> 2). */
+ * (fx_batch_run_tiered escalates 0 -> 1 -> 2, 3 -> 1 -> 2, 4 -> 2, 5 -> 1 -> 2,
+ * 6 -> 1 -> 2). */
 #define FX_TIER_GROUP 0      /* 16 lanes per stream: 16 pending, 8 cached deps, n <= 16 */
 #define FX_TIER_LDS_LARGE 1  /* lane per stream, LDS-resident: 32 pending, one wave per CU */
 #define FX_TIER_GLOBAL 2     /* lane per stream, HBM-resident: 64 pending, 1024-bit windows */
 #define FX_TIER_LANE 3       /* lane per stream, LDS-resident: 12 pending (alternative tier 0) */
 #define FX_TIER_WAVE 4       /* one wavefront per stream: 64 pending, 8 cached deps, <= 14 deps */
 #define FX_TIER_LANE_REG 5   /* lane per stream, register-resident slot table, lanes progress
-                                independently: 16 pending, n <= 8, <= 8 deps */
-#define FX_NUM_TIERS 6
-#define FX_TIER_DEFAULT FX_TIER_GROUP
+                                independently: 12 pending, n <= 8, <= 8 deps */
+#define FX_TIER_SPLIT 6      /* per 64-stream tile: tier 5 for tiles with few deps per Add,
+                                tier 0 for dense ones, both launched concurrently; whole
+                                batches only (FX_FLAG_INIT, no stream_map, no saved state);
+                                `state` = fx_batch_state_bytes(6, n, S) bytes of scratch */
+#define FX_NUM_TIERS 7
+#define FX_TIER_DEFAULT FX_TIER_SPLIT
 
 typedef struct fx_tier_info {
   uint32_t max_sources;    /* n supported                                   */

@@ -134,12 +134,37 @@ def test_capacity_is_reported_exactly(gpu):
         assert np.array_equal(res.release[ridx], o_rel[ridx])
 
 
-@pytest.mark.parametrize("tier", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("tier", [0, 1, 2, 3, 4, 5, 6])
 def test_each_tier_standalone(gpu, tier):
     p = fs.synth_params(seed=9, n=5, instances=20, cmds=150, window=6, cycle_pct=30)
     planes = fs.synth_host(p)
     res = fd.run_batch(planes, tiered=False, tier=tier)
     assert_parity(planes, res)
+
+
+@pytest.mark.parametrize("block,instances,n", [(16, 80, 5), (13, 57, 3), (1, 40, 7)])
+def test_split_tier_mixed_tiles(gpu, block, instances, n):
+    """FX_TIER_SPLIT over conflict-major batches (tiles of one rate, tiles
+    straddling two rates, a ragged last tile): sparse tiles run on the lane
+    tier, dense ones on the group tier, concurrently; bit-exact either way."""
+    p = fs.synth_params(seed=31, n=n, instances=instances, cmds=120, window=8, cycle_pct=30,
+                        conflicts=(0, 100, 2, 50, 10), conflict_block=block)
+    planes = fs.synth_host(p)
+    res = fd.run_batch(planes, tiered=False, tier=_lib.FX_TIER_SPLIT, nbins_chain=64,
+                       nbins_delay=2048)
+    ok = res.err == 0
+    assert ok.sum() > planes.S // 2  # capacity stops are allowed, results must still match
+    o_order, o_rel, o_nexec, o_err = oracle_lib.batch_execute(planes, threads=8)
+    for s in np.flatnonzero(ok):
+        idx = _lib.index(np.arange(int(o_nexec[s])), s, planes.steps)
+        assert res.nexec[s] == o_nexec[s]
+        assert np.array_equal(res.order[idx], o_order[idx])
+        ridx = _lib.index(np.arange(planes.steps), s, planes.steps)
+        assert np.array_equal(res.release[ridx], o_rel[ridx])
+    assert np.all(res.err[~ok] == _lib.FX_ERR_CAPACITY)
+    tiered = fd.run_batch(planes, tier=_lib.FX_TIER_SPLIT, nbins_chain=64, nbins_delay=2048)
+    assert tiered.status == _lib.FX_OK
+    assert_parity(planes, tiered)
 
 
 def test_device_generator_matches_host(gpu):
