@@ -53,7 +53,7 @@ def parse():
                     help="instances per conflict rate block (-1 = --seeds: conflict-major "
                          "enumeration, so a wavefront's streams share a rate; 0 = seed-major)")
     ap.add_argument("--tier", type=int, default=-1, help="executor tier (-1 = FX_TIER_DEFAULT)")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=5.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", type=str, default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args()
@@ -269,8 +269,8 @@ def cpu_baseline(args, lib, dot, hdr, deps, order, release, nexec, S, steps, dma
     full_tiles = S // 64
     if full_tiles == 0:
         return None
-    # calibrate: ~1M Adds/s per thread over the mixed batch -> whole tiles
-    budget_adds = args.cpu_baseline_seconds * 1.0e6 * threads
+    # calibrate: ~3.5M Adds/s per thread over the mixed batch (measured) -> whole tiles
+    budget_adds = args.cpu_baseline_seconds * 3.5e6 * threads
     tiles = int(max(1, min(full_tiles, budget_adds // (64 * steps))))
     pick = np.unique(np.linspace(0, full_tiles - 1, tiles).round().astype(np.int64))
     tiles = len(pick)

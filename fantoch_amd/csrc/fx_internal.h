@@ -59,6 +59,7 @@ uint32_t lane_decode_pending(const uint32_t* block, uint32_t lane, uint32_t* dot
 constexpr uint32_t LANE_SLOTS = 12;         // pending vertices per stream
 constexpr uint32_t LANE_MAX_DEPS = 8;       // dep planes (and cached deps per vertex)
 constexpr uint32_t LANE_WINDOW_BITS = 32;   // executed-clock window per source
+constexpr size_t LANE_MAX_PLANE_BYTES = 0xFFFFFFF0u;  // input planes are read with 32-bit buffer offsets
 
 // FX_TIER_SPLIT (graph_split.hip): per-tile choice between the group and the
 // lane tier, both launched concurrently.

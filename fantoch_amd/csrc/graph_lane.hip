@@ -132,6 +132,7 @@ struct Lane {
   uint32_t smem = 0, sall = 0, sfirst = 0;  // SCC being saved: members left / all / next opens it
   uint32_t stream = 0, n = 0, steps = 0;
   uint32_t* order = nullptr;
+  uint4 ob = make_uint4(0, 0, 0, 0);  // order words k & ~3 .. k - 1, not yet stored
   uint32_t* release = nullptr;
 
   __device__ __forceinline__ uint32_t& w(uint32_t i) { return lds[i * WV]; }
@@ -218,9 +219,28 @@ struct Lane {
     return (w(L_WL + (nwl >> 1)) >> ((nwl & 1u) << 4)) & 0xFFFFu;
   }
 
+  // order[at(k)] = w, stored 16 bytes at a time: the 4 order words of steps
+  // 4j..4j+3 of one stream are contiguous in the tile layout, so a lane writes
+  // whole 16-byte segments instead of four scattered words
+  __device__ __forceinline__ void put_order(uint32_t w) {
+    const uint32_t q = k & 3u;
+    ob.x = q == 0 ? w : ob.x;
+    ob.y = q == 1 ? w : ob.y;
+    ob.z = q == 2 ? w : ob.z;
+    ob.w = q == 3 ? w : ob.w;
+    if (q == 3) *reinterpret_cast<uint4*>(order + at(k - 3)) = ob;
+  }
+  // stores the buffered words of an incomplete segment (kernel end)
+  __device__ __forceinline__ void flush_order() {
+    const uint32_t q = k & 3u, b = k - q;
+    if (q > 0) order[at(b)] = ob.x;
+    if (q > 1) order[at(b + 1)] = ob.y;
+    if (q > 2) order[at(b + 2)] = ob.z;
+  }
+
   __device__ __forceinline__ void emit(uint32_t r, uint32_t d, bool start) {
     if (k >= steps) { err = FX_ERR_ORDER_OVERFLOW; return; }
-    order[at(k)] = r | (start ? FX_ORDER_SCC_START : 0u);
+    put_order(r | (start ? FX_ORDER_SCC_START : 0u));
     release[at(r)] = cur;
     ++k;
     clk_add(d);
@@ -381,7 +401,7 @@ struct Lane {
       if (k >= steps) {
         err = FX_ERR_ORDER_OVERFLOW;
       } else {
-        order[at(k)] = r | (fast || sfirst ? FX_ORDER_SCC_START : 0u);
+        put_order(r | (fast || sfirst ? FX_ORDER_SCC_START : 0u));
         release[at(r)] = cur;
         ++k;
         clk_add(ed);
@@ -395,7 +415,7 @@ struct Lane {
         if (k >= steps) {
           err = FX_ERR_ORDER_OVERFLOW;
         } else {
-          order[at(k)] = i | FX_ORDER_SCC_START;
+          put_order(i | FX_ORDER_SCC_START);
           release[at(i)] = i;
           ++k;
         }
@@ -572,6 +592,9 @@ void k_graph_lane(KArgs a) {
       e.clk[q * WV] = (a.init_frontier && active) ? a.init_frontier[(size_t)s * 8 + q] : 0u;
   } else if (active) {
     e.load_state(gst);
+    // a resumed stream part-way through a 16-byte order segment: the previous
+    // launch stored its first words (flush_order)
+    if (e.k & 3u) e.ob = *reinterpret_cast<const uint4*>(a.order + e.at(e.k & ~3u));
   }
   if (!active) e.err = FX_ERR_INVALID_ARG;  // idle lane (its loads read stream 0)
 
@@ -583,42 +606,67 @@ void k_graph_lane(KArgs a) {
   const uint32_t b_last = a.step_end ? (a.step_end - 1) >> 2 : 0u;
   const size_t plane = dmax ? a.plane : 0;
   const uint32_t jlast = dmax ? dmax - 1 : 0;
-  const uint32_t* dotp = a.dot + soff;
-  const uint32_t* hdrp = a.hdr + soff;
-  const uint32_t* depp = (dmax ? a.deps : a.dot) + soff;
-  auto ld = [&](uint32_t b, uint32_t p) -> uint4 {
-    const size_t off = (size_t)min(b, b_last) * 256;
-    const uint32_t* src = p == 0 ? dotp : p == 1 ? hdrp : depp + (size_t)min(p - 2, jlast) * plane;
-    return *reinterpret_cast<const uint4*>(src + off);
+  // Refill loads go through range-checked buffer descriptors (one per plane,
+  // built from kernel arguments only, so they stay in SGPRs): a lane that keeps
+  // its block passes an out-of-range offset, and the load returns zeros
+  // without a memory request.  The instruction count stays static (vmcnt(N),
+  // not vmcnt(0)), and only lanes that moved to a new block fetch it.
+  const uint32_t pbytes = (uint32_t)min(a.plane * 4, (size_t)0xFFFFFFF0u);
+  const uint32_t* depb = dmax ? a.deps : a.dot;
+  __amdgpu_buffer_rsrc_t rs[NP];
+  rs[0] = __builtin_amdgcn_make_buffer_rsrc((void*)a.dot, 0, (int)pbytes, 0x00020000);
+  rs[1] = __builtin_amdgcn_make_buffer_rsrc((void*)a.hdr, 0, (int)pbytes, 0x00020000);
+#pragma unroll
+  for (uint32_t j = 0; j < DC; ++j)
+    rs[2 + j] = __builtin_amdgcn_make_buffer_rsrc((void*)(depb + (size_t)min(j, jlast) * plane), 0,
+                                                  (int)pbytes, 0x00020000);
+  constexpr uint32_t OOB = 0xFFFFFFF0u;
+  const uint32_t sbyte = (uint32_t)(soff * 4);
+  auto boff = [&](uint32_t b) -> uint32_t { return sbyte + min(b, b_last) * 1024u; };
+  auto ld = [&](uint32_t off, uint32_t p) -> uint4 {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs[p], off, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
   };
 
-  // 2-block pipeline: c = block blk (readable), x = block blk + 1 (in flight)
+  // 2-block pipeline: c = block blk (readable); block blk + 1 is in x when this
+  // lane loaded it at the last refill (xl), else in xo (kept from before)
   uint32_t i = a.step_begin;
   uint32_t blk = i >> 2;
-  uint4 c[NP], x[NP];
+  uint4 c[NP], x[NP], xo[NP];
 #pragma unroll
-  for (uint32_t p = 0; p < NP; ++p) c[p] = ld(blk, p);
+  for (uint32_t p = 0; p < NP; ++p) c[p] = ld(boff(blk), p);
 #pragma unroll
-  for (uint32_t p = 0; p < NP; ++p) x[p] = ld(blk + 1, p);
+  for (uint32_t p = 0; p < NP; ++p) x[p] = ld(boff(blk + 1), p);
+#pragma unroll
+  for (uint32_t p = 0; p < NP; ++p) xo[p] = make_uint4(0, 0, 0, 0);
+  uint32_t xl = ~0u;  // all-ones: x holds block blk + 1
 
   for (uint32_t it = 0;; ++it) {
     if ((it & 3u) == 0) {
       const bool live = e.phase != PH_IDLE || (i < lim && !e.err);
       if (!__any(live)) break;
-      // lanes that have consumed their c block take x; every lane then issues
-      // the same NP loads (a lane that did not shift re-reads its x block)
+      // lanes that have consumed their c block take block blk + 1; every lane
+      // then issues the same NP loads, in range only for the lanes that moved
       const bool sh = (i >> 2) > blk;
       blk += sh ? 1u : 0u;
       const uint32_t m = 0u - (uint32_t)sh;  // masks, not selects (a select of the two
 #pragma unroll                               // arrays becomes a select of their addresses)
       for (uint32_t p = 0; p < NP; ++p) {
-        c[p].x = (x[p].x & m) | (c[p].x & ~m);
-        c[p].y = (x[p].y & m) | (c[p].y & ~m);
-        c[p].z = (x[p].z & m) | (c[p].z & ~m);
-        c[p].w = (x[p].w & m) | (c[p].w & ~m);
+        uint4 e4;
+        e4.x = (x[p].x & xl) | (xo[p].x & ~xl);
+        e4.y = (x[p].y & xl) | (xo[p].y & ~xl);
+        e4.z = (x[p].z & xl) | (xo[p].z & ~xl);
+        e4.w = (x[p].w & xl) | (xo[p].w & ~xl);
+        c[p].x = (e4.x & m) | (c[p].x & ~m);
+        c[p].y = (e4.y & m) | (c[p].y & ~m);
+        c[p].z = (e4.z & m) | (c[p].z & ~m);
+        c[p].w = (e4.w & m) | (c[p].w & ~m);
+        xo[p] = e4;
       }
+      xl = m;
+      const uint32_t off = sh ? boff(blk + 1) : OOB;
 #pragma unroll
-      for (uint32_t p = 0; p < NP; ++p) x[p] = ld(blk + 1, p);
+      for (uint32_t p = 0; p < NP; ++p) x[p] = ld(off, p);
     }
     // a lane consumes at most one step per iteration, so between two refills
     // it never runs past the end of x; it only waits (at most 3 iterations)
@@ -648,6 +696,7 @@ void k_graph_lane(KArgs a) {
   // vertices still pending have no release step (yet)
   for (uint32_t m = e.occ; m; m &= m - 1)
     a.release[e.at(e.rec(__builtin_ctz(m)) & 0x03FFFFFFu)] = FX_RELEASE_NONE;
+  e.flush_order();
   a.nexec[s] = e.k;
   a.err[s] = e.err;
   if (a.flags & FX_FLAG_SAVE_STATE) e.save_state(gst);
@@ -700,6 +749,7 @@ static int launch_lane_d(const KArgs& a, hipStream_t stream) {
 
 int launch_lane(const KArgs& a0, hipStream_t stream) {
   if (a0.dmax > LANE_MAX_DEPS || a0.n > 8) return FX_ERR_INVALID_ARG;
+  if (a0.plane * 4 > LANE_MAX_PLANE_BYTES) return FX_ERR_INVALID_ARG;  // 32-bit buffer offsets
   if (!getenv("FX_LANE_DEBUG")) return launch_lane_d(a0, stream);
   // diagnostics: per-lane iteration counters, summarised on stderr
   KArgs a = a0;

@@ -137,9 +137,9 @@ int launch_split(const KArgs& a0, void* scratch, hipStream_t hs) {
   uint32_t* heavy = score + tiles;
   uint32_t* light = heavy + (size_t)tiles * 64;
   uint32_t* counts = light + (size_t)tiles * 64;
-  // the lane tier holds n <= 8 sources and <= LANE_MAX_DEPS deps: otherwise
-  // every tile is heavy
-  const bool lane_ok = a0.n <= 8 && a0.dmax <= LANE_MAX_DEPS;
+  // the lane tier holds n <= 8 sources and <= LANE_MAX_DEPS deps and reads
+  // planes of < 4 GiB: otherwise every tile is heavy
+  const bool lane_ok = a0.n <= 8 && a0.dmax <= LANE_MAX_DEPS && a0.plane * 4 <= LANE_MAX_PLANE_BYTES;
   const uint32_t thr = lane_ok ? threshold() : 0u;
   if (!g_aux) {
     if (hipStreamCreateWithFlags(&g_aux, hipStreamNonBlocking) != hipSuccess) return FX_ERR_HIP;
