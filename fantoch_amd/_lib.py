@@ -24,6 +24,7 @@ FX_ERR_UNSUPPORTED = 7
 FX_ERR_ORDER_OVERFLOW = 8
 FX_ERR_TIME_RANGE = 9
 FX_ERR_NO_DEVICE = 10
+FX_ERR_LOG_FORMAT = 11
 
 FX_SEQ_BITS = 24
 FX_SEQ_MASK = (1 << 24) - 1
@@ -105,6 +106,18 @@ class ExecutorResultC(ctypes.Structure):
     _fields_ = [("rifl", CRifl), ("key", ctypes.c_uint32), ("read_only", ctypes.c_uint32)]
 
 
+class LogSummary(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in
+                ("records", "adds", "others", "keys", "deps", "distinct_keys")]
+
+
+class LogAdd(ctypes.Structure):
+    _fields_ = [("dot", CDot), ("rifl", CRifl), ("key_off", ctypes.c_uint64),
+                ("dep_off", ctypes.c_uint64), ("nkeys", ctypes.c_uint32),
+                ("ndeps", ctypes.c_uint32), ("read_only", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
+
+
 class HistStats(ctypes.Structure):
     _fields_ = [("count", ctypes.c_double), ("mean", ctypes.c_double), ("stddev", ctypes.c_double),
                 ("cov", ctypes.c_double), ("mdtm", ctypes.c_double), ("min", ctypes.c_double),
@@ -155,6 +168,11 @@ SIGNATURES = [
     ("fx_graph_executor_pending", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.POINTER(CDot), ctypes.c_uint32, u32p]),
     ("fx_graph_executor_parallel", ctypes.c_int, []),
+    ("fx_exec_log_scan", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(LogSummary)]),
+    ("fx_exec_log_decode", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(LogAdd), ctypes.c_uint64,
+      u32p, ctypes.c_uint64, ctypes.POINTER(CDot), ctypes.c_uint64, ctypes.POINTER(LogSummary)]),
     ("fx_hist_stats_compute", ctypes.c_int,
      [u64p, u64p, ctypes.c_uint32, ctypes.POINTER(HistStats)]),
     ("fx_hist_percentile", ctypes.c_int,

@@ -43,6 +43,7 @@ extern "C" {
 #define FX_ERR_ORDER_OVERFLOW 8/* more executions than order-plane rows        */
 #define FX_ERR_TIME_RANGE 9    /* t_ms >= 2^24 relative to the stream base     */
 #define FX_ERR_NO_DEVICE 10    /* no GPU visible: the product never falls back */
+#define FX_ERR_LOG_FORMAT 11   /* malformed execution log (rw/mod.rs:90 `expect` panics) */
 
 /* ------------------------------------------------- packed stream format */
 /* A dot (fantoch/src/id.rs:21-27, Id<u8>{source, sequence}, derived Ord) is
@@ -288,6 +289,46 @@ int fx_graph_executor_monitor(fx_graph_executor* ex, uint32_t key, fx_rifl* out,
 int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiting_on, uint32_t cap, uint32_t* n_out);
 /* Executor::parallel (executor.rs:103-105). */
 int fx_graph_executor_parallel(void);
+
+/* ------------------------------------------------------- execution log */
+/* Reader for the run mode's execution log: LengthDelimitedCodec frames
+ * (4-byte big-endian length) of bincode-1 GraphExecutionInfo, as written by
+ * execution_logger_task (fantoch/src/run/task/server/execution_logger.rs:11-55,
+ * Rw::write fantoch/src/run/rw/mod.rs:66-77,93-100) and read back by
+ * graph_executor_replay (fantoch_ps/src/bin/graph_executor_replay.rs:29-37,
+ * Rw::recv rw/mod.rs:37-53).  Each Add becomes the arguments of
+ * fx_graph_executor_handle_add: keys of `shard_id` interned to u32 ids in
+ * first-seen order, deps as dots.  Request/RequestReply/Executed (partial
+ * replication only) are parsed and counted in `others`, never executed. */
+typedef struct fx_log_summary {
+  uint64_t records;       /* frames                                          */
+  uint64_t adds;          /* GraphExecutionInfo::Add frames                  */
+  uint64_t others;        /* Request / RequestReply / Executed frames        */
+  uint64_t keys;          /* sum of keys over the Adds (on shard_id)         */
+  uint64_t deps;          /* sum of deps over the Adds                       */
+  uint64_t distinct_keys; /* interned key ids                                */
+} fx_log_summary;
+
+typedef struct fx_log_add {
+  fx_dot dot;
+  fx_rifl rifl;
+  uint64_t key_off;       /* into the keys array                             */
+  uint64_t dep_off;       /* into the deps array                             */
+  uint32_t nkeys;
+  uint32_t ndeps;
+  uint32_t read_only;     /* Command::read_only (command.rs:80-87)           */
+  uint32_t pad;
+} fx_log_add;
+
+/* Validates the whole log and fills the summary (sizes for the decode call).
+ * FX_ERR_LOG_FORMAT on a truncated frame, unknown tag, trailing bytes, or a
+ * sequence above 2^32-1 (reference: Rw::recv's `expect`, rw/mod.rs:90). */
+int fx_exec_log_scan(const uint8_t* buf, uint64_t len, uint64_t shard_id, fx_log_summary* out);
+/* Decodes every Add in file order into caller-allocated arrays
+ * (FX_ERR_CAPACITY if one is too small). */
+int fx_exec_log_decode(const uint8_t* buf, uint64_t len, uint64_t shard_id, fx_log_add* adds,
+                       uint64_t cap_adds, uint32_t* keys, uint64_t cap_keys, fx_dot* deps,
+                       uint64_t cap_deps, fx_log_summary* out);
 
 /* ------------------------------------------------- histogram statistics */
 /* Histogram stats (histogram.rs:61-235) over (value, count) pairs sorted by value. */
