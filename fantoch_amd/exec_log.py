@@ -174,3 +174,31 @@ def replay(data, n, f=1, now_ms=None, monitor=True):
     for i, (dot, rifl, keys, deps, ro) in enumerate(log):
         ex.handle_add(dot, rifl, keys, deps, now_ms(i) if now_ms else 0, read_only=ro)
     return ex
+
+
+def log_stream(log, now_ms=None):
+    """A decoded log as one commit stream for the batched executor: [(dot, deps, t_ms)]."""
+    out = []
+    for i, (dot, _rifl, _keys, deps, _ro) in enumerate(log):
+        if dot[1] > _lib.FX_SEQ_MASK or any(q > _lib.FX_SEQ_MASK for _, q in deps):
+            raise _lib.FxError(_lib.FX_ERR_DOT_RANGE, "log_stream: sequence >= 2^24")
+        out.append((dot, deps, now_ms(i) if now_ms else 0))
+    return out
+
+
+def replay_batch(logs, n, execute_at_commit=False):
+    """Replays many logs at once: one stream per log through fx_batch_execute (the
+    batched GraphExecutor), e.g. the per-process logs of one run.  Returns
+    ([[dot, ...] per log in execution order], BatchResult)."""
+    from . import device as fd
+    from . import streams as fs
+    decoded = [l if isinstance(l, ExecutionLog) else read_log(l) for l in logs]
+    for l in decoded:
+        if l.summary["others"]:
+            raise _lib.FxError(_lib.FX_ERR_UNSUPPORTED, "replay_batch: partial-replication records")
+    planes = fs.pack_streams([log_stream(l) for l in decoded], n)
+    res = fd.run_batch(planes, execute_at_commit=execute_at_commit)
+    check(res.status, "replay_batch")
+    orders = fs.decode_orders(res.order, res.nexec, planes.S, planes.steps)
+    adds = [list(l) for l in decoded]
+    return [[adds[s][rec][0] for rec, _ in orders[s]] for s in range(planes.S)], res

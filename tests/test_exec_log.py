@@ -130,3 +130,19 @@ def test_replay_refuses_partial_replication_records(gpu):
     with pytest.raises(_lib.FxError) as e:
         L.replay(data, 3)
     assert e.value.status == _lib.FX_ERR_UNSUPPORTED
+
+
+@pytest.mark.gpu
+def test_replay_batch_matches_single_replay_and_oracle(gpu):
+    logs, exp = [], []
+    for seed, n in ((5, 3), (6, 3), (7, 3)):
+        stream, data = synth_log(seed=seed, n=n, cmds=150)
+        logs.append(data)
+        g = oracle_lib.Graph(1, n)
+        for dot, deps, _, _ in stream:
+            g.handle_add(dot, deps)
+        exp.append([d for d, _, _ in g.drain()])
+    got, res = L.replay_batch(logs, 3)
+    assert (res.err == 0).all()
+    assert got == exp
+    assert got[0] == [d for d, _ in L.replay(logs[0], 3).drain_dots()]
