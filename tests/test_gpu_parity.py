@@ -162,6 +162,10 @@ def test_split_tier_mixed_tiles(gpu, block, instances, n):
         ridx = _lib.index(np.arange(planes.steps), s, planes.steps)
         assert np.array_equal(res.release[ridx], o_rel[ridx])
     assert np.all(res.err[~ok] == _lib.FX_ERR_CAPACITY)
+    # k_metrics over a batch with errored streams: order-major for those, record-major
+    # for the rest; same histograms as the host fold of the GPU's own order/release
+    chain, delay = oracle_hists(planes, res.order, res.release, res.nexec, 64, 2048)
+    assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
     tiered = fd.run_batch(planes, tier=_lib.FX_TIER_SPLIT, nbins_chain=64, nbins_delay=2048)
     assert tiered.status == _lib.FX_OK
     assert_parity(planes, tiered)
@@ -191,8 +195,10 @@ def test_ragged_lengths_and_truncated_streams(gpu):
     rng = np.random.default_rng(0)
     planes.lengths = rng.integers(0, planes.steps + 1, planes.S).astype(np.uint32)
     planes.lengths[0] = 0  # empty stream
-    res = fd.run_batch(planes)
-    assert_parity(planes, res)
+    res = fd.run_batch(planes, nbins_chain=64, nbins_delay=2048)
+    o_order, o_rel, o_nexec = assert_parity(planes, res)
+    chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 64, 2048)
+    assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
 
 
 @pytest.mark.parametrize("tier", [0, 1, 2, 3, 4, 5])
