@@ -775,9 +775,7 @@ __device__ inline void wave_hist_add(uint32_t* lds, unsigned long long* glob, ui
 __global__ __launch_bounds__(256) void k_metrics(const uint32_t* __restrict__ hdr,
                                                  const uint32_t* __restrict__ order,
                                                  const uint32_t* __restrict__ release,
-                                                 const uint32_t* __restrict__ nexec,
-                                                 const uint32_t* __restrict__ err,
-                                                 const uint32_t* __restrict__ lengths, uint32_t S,
+                                                 const uint32_t* __restrict__ nexec, uint32_t S,
                                                  uint32_t steps, unsigned long long* chain,
                                                  uint32_t nbc, unsigned long long* delay,
                                                  uint32_t nbd, uint32_t use_lds) {
@@ -798,33 +796,20 @@ __global__ __launch_bounds__(256) void k_metrics(const uint32_t* __restrict__ hd
     const uint32_t k = kb * 4 + kq;
     uint32_t db = kNoBin, cb = kNoBin;
     const uint32_t ne = s < S ? nexec[s] : 0;
-    // Position k of this lane is both order row k and record k.  For a stream
-    // that finished with FX_OK, every row below its length holds a release
-    // step or FX_RELEASE_NONE, so the delay of record k is read record-major
-    // (release[k] and t(k) coalesced, one gather for t(release)) instead of
-    // through the order (three gathers); the samples are the same multiset,
-    // one per executed command.  Errored streams (release rows past the error
-    // are left untouched) keep the order-major walk.
-    const size_t at = (size_t)tile * steps4 * 256 + (size_t)kb * 256 + (lane << 2) + kq;
-    const bool ok = s < S && err && err[s] == FX_OK;
-    const uint32_t len = s < S ? (lengths ? min(lengths[s], steps) : steps) : 0u;
-    if (ok ? k < len : k < ne) {
-      uint32_t rec = k;
-      if (!ok) rec = order[at] & 0x7FFFFFFFu;
-      const uint32_t rs = rec < steps ? release[ok ? at : fx_index(rec, s, steps)] : FX_RELEASE_NONE;
-      if (rs < steps) {
-        const uint32_t dl = FX_HDR_T(hdr[fx_index(rs, s, steps)]) -
-                            FX_HDR_T(hdr[ok ? at : fx_index(rec, s, steps)]);
-        db = dl < nbd - 1 ? dl : nbd - 1;
-      }
-    }
     if (k < ne) {
-      const uint32_t o = order[at];
+      const size_t tile_base = (size_t)tile * steps4 * 256 + (lane << 2);
+      const uint32_t o = order[tile_base + (size_t)kb * 256 + kq];
       const uint32_t rec = o & 0x7FFFFFFFu;
-      if ((o & FX_ORDER_SCC_START) && rec < steps && release[fx_index(rec, s, steps)] < steps) {
-        uint32_t size = 1;
-        while (k + size < ne && !(order[fx_index(k + size, s, steps)] & FX_ORDER_SCC_START)) ++size;
-        cb = size < nbc - 1 ? size : nbc - 1;
+      const uint32_t rs = rec < steps ? release[fx_index(rec, s, steps)] : FX_RELEASE_NONE;
+      if (rs < steps) {  // else not executed (errored stream)
+        const uint32_t dl =
+            FX_HDR_T(hdr[fx_index(rs, s, steps)]) - FX_HDR_T(hdr[fx_index(rec, s, steps)]);
+        db = dl < nbd - 1 ? dl : nbd - 1;
+        if (o & FX_ORDER_SCC_START) {
+          uint32_t size = 1;
+          while (k + size < ne && !(order[fx_index(k + size, s, steps)] & FX_ORDER_SCC_START)) ++size;
+          cb = size < nbc - 1 ? size : nbc - 1;
+        }
       }
     }
     wave_hist_add(use_lds ? hist + nbc : nullptr, delay, db, use_lds);
@@ -1104,8 +1089,7 @@ int fx_batch_metrics(const fx_stream_batch* in, const fx_order_batch* out, const
   const size_t lds_bytes = (size_t)(h->nbins_chain + h->nbins_delay) * 4;
   const uint32_t use_lds = lds_bytes <= 48 * 1024 ? 1u : 0u;
   hipLaunchKernelGGL(k_metrics, dim3(grid), dim3(256), use_lds ? lds_bytes : 0, (hipStream_t)hip_stream,
-                     in->hdr, out->order, out->release, out->nexec, out->err, in->lengths,
-                     in->num_streams, in->steps,
+                     in->hdr, out->order, out->release, out->nexec, in->num_streams, in->steps,
                      (unsigned long long*)h->chain_size, h->nbins_chain,
                      (unsigned long long*)h->execution_delay, h->nbins_delay, use_lds);
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
