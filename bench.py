@@ -185,6 +185,13 @@ def main():
     else:
         executed_total, nd_all, adds_all = float(executed_local), float(nd_total), float(n_adds)
 
+    # per-placement results: one all_gather of fixed-size per-instance rows after the
+    # timed region, checked against the executed total
+    rows = sharding.gather_summaries(dist, sharding.instance_summaries(nexec, err, p), world)
+    summary = {"fields": list(sharding.SUMMARY_FIELDS), "instances": int(rows.shape[0]),
+               "all_ok": bool((rows[:, 3] == 0).all().item()),
+               "executed_matches": int(rows[:, 2].sum().item()) == int(executed_total)}
+
     value = executed_total * args.steps / elapsed
     edges = nd_all * args.steps / elapsed
     kavg = sum(kernel_ms) / len(kernel_ms) if kernel_ms else None
@@ -240,6 +247,7 @@ def main():
             "gen_seconds": round(gen_s, 3),
             "roofline": roof,
             "cpu_baseline": cpu,
+            "instance_summary": summary,
         }
         print(json.dumps(result), flush=True)
     if world > 1:
