@@ -344,3 +344,26 @@ def test_cpp_executor_tests(gpu):
     assert os.path.exists(exe), "build with `make`"
     r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+# ------------------------------------------- BASELINE configs at full size
+@pytest.mark.parametrize("name,cmds,conflict", [
+    # configs[4]: one instance, 10^6-command commit streams with cycles (5 executors)
+    ("single_huge_instance", 200_000, 2),
+    # configs[3]: dense-dependency stress, 100 % conflicts, 64 clients/region x 1k
+    # commands at n=5 -> 320k commands per instance, large SCCs
+    ("dense_stress", 64_000, 100),
+])
+def test_full_size_single_instance_matches_oracle(gpu, name, cmds, conflict):
+    p = fs.synth_params(seed=2025, instances=1, n=5, cmds=cmds, window=8, cycle_pct=30,
+                        conflicts=(conflict,))
+    planes = fs.synth_host(p)
+    res = fd.run_batch(planes, nbins_chain=64, nbins_delay=2048)
+    assert res.status == _lib.FX_OK
+    o_order, o_rel, o_nexec = assert_parity(planes, res)
+    assert np.all(res.nexec == planes.steps)
+    chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 64, 2048)
+    assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
+    if conflict == 100:
+        # SCCs larger than one command exist (the worst-case graph of configs[3])
+        assert chain[2:].sum() > 0
