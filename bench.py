@@ -59,6 +59,24 @@ def parse():
     return ap.parse_args()
 
 
+def measured_copy_gbps(torch, dev, nbytes=2 << 30, reps=10):
+    """Achievable HBM bandwidth on this box: a device-to-device copy of nbytes,
+    counted as read + write (SURVEY.md §8(d) asks for it next to the 8 TB/s peak)."""
+    a = torch.empty(nbytes // 4, dtype=torch.int32, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gbps = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    return round(gbps, 1)
+
+
 def main():
     args = parse()
     import numpy as np
@@ -215,6 +233,9 @@ def main():
                     "traffic": traffic, "kernel": KERNEL_NAMES.get(tier, "tier%d" % tier),
                     "kernel_ms_avg": round(kavg, 4), "alg_bytes_per_launch": alg_bytes,
                     "alg_bytes_per_cmd": round(alg_bytes / n_adds, 3)}
+            copy = measured_copy_gbps(torch, dev)
+            roof["measured_copy_gbps"] = copy
+            roof["frac_of_measured_copy"] = round(achieved / copy, 4)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, lib, dot, hdr, deps, order, release, nexec, S, steps, dmax, pw)

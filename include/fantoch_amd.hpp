@@ -9,6 +9,9 @@
 //   ExecutorResult ......... fantoch/src/executor/mod.rs:169-184
 //   GraphExecutor .......... fantoch_ps/src/executor/graph/executor.rs:19-114
 //                            (the `Executor` trait, fantoch/src/executor/mod.rs:27-89)
+//   read_execution_log ..... Rw::recv over an execution log (fantoch/src/run/rw/mod.rs:37-53,
+//                            written by run/task/server/execution_logger.rs:11-55)
+//   replay_execution_log ... fantoch_ps/src/bin/graph_executor_replay.rs:13-38
 #pragma once
 #include <cstdint>
 #include <map>
@@ -183,5 +186,47 @@ class GraphExecutor {
  private:
   fx_graph_executor* h_ = nullptr;
 };
+
+// Decodes every GraphExecutionInfo::Add of an execution log (LengthDelimitedCodec
+// frames of bincode-1) into GraphExecutionInfo values, keys of `shard_id` interned
+// in first-seen order.  A malformed log throws Error(FX_ERR_LOG_FORMAT), as
+// Rw::recv's `expect` panics (rw/mod.rs:90).  `others` counts the
+// Request / RequestReply / Executed frames (partial replication only).
+inline std::vector<GraphExecutionInfo> read_execution_log(const std::vector<uint8_t>& bytes,
+                                                          ShardId shard_id = 0,
+                                                          uint64_t* others = nullptr) {
+  fx_log_summary sum{};
+  check(fx_exec_log_scan(bytes.data(), bytes.size(), shard_id, &sum));
+  std::vector<fx_log_add> adds(sum.adds);
+  std::vector<uint32_t> keys(sum.keys);
+  std::vector<fx_dot> deps(sum.deps);
+  check(fx_exec_log_decode(bytes.data(), bytes.size(), shard_id, adds.data(), sum.adds, keys.data(),
+                           sum.keys, deps.data(), sum.deps, &sum));
+  if (others) *others = sum.others;
+  std::vector<GraphExecutionInfo> out;
+  out.reserve(adds.size());
+  for (const auto& a : adds) {
+    std::vector<Key> ks(keys.begin() + a.key_off, keys.begin() + a.key_off + a.nkeys);
+    std::vector<Dependency> ds;
+    for (uint32_t i = 0; i < a.ndeps; ++i) {
+      const fx_dot& d = deps[a.dep_off + i];
+      ds.push_back(Dependency{Dot((ProcessId)d.source, d.seq)});
+    }
+    out.push_back(GraphExecutionInfo::add(
+        Dot((ProcessId)a.dot.source, a.dot.seq),
+        Command::from(Rifl(a.rifl.source, a.rifl.seq), std::move(ks), a.read_only != 0), std::move(ds)));
+  }
+  return out;
+}
+
+// graph_executor_replay: process 1, shard 0, Config::new(n, f); every Add in file
+// order into `executor` at time `time_ms`.
+inline void replay_execution_log(GraphExecutor& executor, const std::vector<uint8_t>& bytes,
+                                 uint64_t time_ms = 0) {
+  uint64_t others = 0;
+  auto infos = read_execution_log(bytes, 0, &others);
+  if (others) throw Error(FX_ERR_UNSUPPORTED);
+  for (const auto& info : infos) executor.handle(info, time_ms);
+}
 
 }  // namespace fantoch_amd

@@ -183,6 +183,71 @@ static void test_sccs_found_and_missing_dep() {
   EXPECT(np == 1 && pw[0].source == 5 && pw[0].seq == 61, "single missing dependency (5,61)");
 }
 
+// execution log of the `simple` KAT, bincode-1 frames as execution_logger.rs writes
+// them, replayed like graph_executor_replay (graph_executor_replay.rs:13-38)
+static void put_u32be(std::vector<uint8_t>& b, uint32_t v) {
+  for (int i = 3; i >= 0; --i) b.push_back((uint8_t)(v >> (8 * i)));
+}
+static void put_le(std::vector<uint8_t>& b, uint64_t v, int bytes) {
+  for (int i = 0; i < bytes; ++i) b.push_back((uint8_t)(v >> (8 * i)));
+}
+static void put_str(std::vector<uint8_t>& b, const std::string& s) {
+  put_le(b, s.size(), 8);
+  b.insert(b.end(), s.begin(), s.end());
+}
+static std::vector<uint8_t> add_frame(Dot dot, Rifl rifl, const std::string& key, Dot dep) {
+  std::vector<uint8_t> p;
+  put_le(p, 0, 4);  // Add
+  put_le(p, dot.source, 1);
+  put_le(p, dot.sequence, 8);
+  put_le(p, rifl.source, 8);
+  put_le(p, rifl.sequence, 8);
+  put_le(p, 1, 8);  // shard_to_ops: {0: {key: [Put("v")]}}
+  put_le(p, 0, 8);
+  put_le(p, 1, 8);
+  put_str(p, key);
+  put_le(p, 1, 8);
+  put_le(p, 1, 4);
+  put_str(p, "v");
+  put_le(p, 1, 8);  // shard_to_keys: {0: [key]}
+  put_le(p, 0, 8);
+  put_le(p, 1, 8);
+  put_str(p, key);
+  put_le(p, 0, 8);  // _empty_keys
+  put_le(p, 1, 8);  // deps: {Dependency{dep, None}}
+  put_le(p, dep.source, 1);
+  put_le(p, dep.sequence, 8);
+  put_le(p, 0, 1);
+  std::vector<uint8_t> f;
+  put_u32be(f, (uint32_t)p.size());
+  f.insert(f.end(), p.begin(), p.end());
+  return f;
+}
+
+static void test_execution_log_replay() {
+  std::vector<uint8_t> log = add_frame(Dot(1, 1), Rifl(1, 1), "A", Dot(2, 1));
+  auto f2 = add_frame(Dot(2, 1), Rifl(2, 1), "A", Dot(1, 1));
+  log.insert(log.end(), f2.begin(), f2.end());
+  auto infos = read_execution_log(log);
+  EXPECT(infos.size() == 2 && infos[1].dot == Dot(2, 1) && infos[1].deps.size() == 1 &&
+             infos[1].deps[0].dot == Dot(1, 1) && !infos[1].cmd.read_only,
+         "decoded log fields");
+  Config config(2, 1);
+  GraphExecutor queue(1, 0, config);
+  replay_execution_log(queue, log);
+  auto ready = queue.drain_dots();
+  EXPECT(ready.size() == 2 && ready[0].first == Dot(1, 1) && ready[1].first == Dot(2, 1),
+         "replayed log executes [cmd_0, cmd_1]");
+  log.pop_back();
+  bool threw = false;
+  try {
+    read_execution_log(log);
+  } catch (const Error& e) {
+    threw = e.status == FX_ERR_LOG_FORMAT;
+  }
+  EXPECT(threw, "truncated log is rejected");
+}
+
 int main() {
   if (fx_device_count() <= 0) {
     std::fprintf(stderr, "no GPU\n");
@@ -194,6 +259,7 @@ int main() {
   test_regression_1();
   test_regression_2();
   test_sccs_found_and_missing_dep();
+  test_execution_log_replay();
   if (g_failures) {
     std::fprintf(stderr, "%d failure(s)\n", g_failures);
     return 1;
