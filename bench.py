@@ -239,6 +239,11 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args, lib, dot, hdr, deps, order, release, nexec, S, steps, dmax, pw)
+        from fantoch_amd import metrics as fm
+        # statistics of the all-reduced histograms of the last step (Histogram stats,
+        # histogram.rs:61-235, over the exact integer bins)
+        hist_stats = {"chain_size": fm.dense_stats(chain.cpu().numpy()),
+                      "execution_delay_ms": fm.dense_stats(delay.cpu().numpy())}
         result = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -269,6 +274,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "instance_summary": summary,
+            "histograms": hist_stats,
         }
         print(json.dumps(result), flush=True)
     if world > 1:

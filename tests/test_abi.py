@@ -149,3 +149,20 @@ def test_pack_streams_roundtrip():
     p = fs.pack_streams(streams, 2)
     assert p.stream(0) == [((1, 1), [(2, 1)], 5, 0), ((2, 1), [(1, 1)], 7, 0)]
     assert p.stream(1) == [((2, 1), [], 0, 0)]
+
+
+def test_dense_stats_match_the_histogram_oracle():
+    from fantoch_amd import metrics
+    rng = np.random.default_rng(3)
+    counts = np.zeros(64, np.uint64)
+    for v in rng.integers(0, 40, 500):
+        counts[v] += 1
+    h = H.Histogram()
+    for v, c in enumerate(counts):
+        for _ in range(int(c)):
+            h.increment(v)
+    st = metrics.dense_stats(counts)
+    assert st["count"] == 500 and st["clamped"] == 0
+    assert math.isclose(st["mean"], h.mean(), rel_tol=1e-12)
+    assert math.isclose(st["p99"], h.percentile(0.99), rel_tol=1e-12)
+    assert metrics.dense_stats(np.zeros(8)) == {"count": 0, "clamped": 0}
