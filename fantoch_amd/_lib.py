@@ -25,6 +25,8 @@ FX_ERR_ORDER_OVERFLOW = 8
 FX_ERR_TIME_RANGE = 9
 FX_ERR_NO_DEVICE = 10
 FX_ERR_LOG_FORMAT = 11
+FX_PROTOCOL_ATLAS = 0
+FX_PROTOCOL_EPAXOS = 1
 
 FX_SEQ_BITS = 24
 FX_SEQ_MASK = (1 << 24) - 1
@@ -168,6 +170,8 @@ SIGNATURES = [
     ("fx_graph_executor_pending", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.POINTER(CDot), ctypes.c_uint32, u32p]),
     ("fx_graph_executor_parallel", ctypes.c_int, []),
+    ("fx_quorum_sizes", ctypes.c_int,
+     [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p]),
     ("fx_exec_log_scan", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(LogSummary)]),
     ("fx_exec_log_decode", ctypes.c_int,
@@ -244,3 +248,11 @@ def unpack_dot(d):
 
 def make_hdr(t, nd, kind=FX_KIND_ADD):
     return (int(t) & 0xFFFFFF) | ((int(nd) & 31) << 24) | ((int(kind) & 7) << 29)
+
+
+def quorum_sizes(protocol, n, f=0):
+    """(fast, write) quorum sizes (fantoch/src/config.rs:294-312) via fx_quorum_sizes."""
+    fq, wq = ctypes.c_uint32(), ctypes.c_uint32()
+    check(load().fx_quorum_sizes(protocol, n, f, ctypes.byref(fq), ctypes.byref(wq)),
+          "fx_quorum_sizes")
+    return fq.value, wq.value

@@ -290,6 +290,16 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
 /* Executor::parallel (executor.rs:103-105). */
 int fx_graph_executor_parallel(void);
 
+/* ------------------------------------------------------- quorum sizes */
+#define FX_PROTOCOL_ATLAS 0u
+#define FX_PROTOCOL_EPAXOS 1u
+/* Fast and write quorum sizes of the commit-stream producers:
+ * Config::atlas_quorum_sizes (fantoch/src/config.rs:294-301) and
+ * Config::epaxos_quorum_sizes (config.rs:303-312, f ignored).  The deps of a
+ * commit are a union over the fast quorum (atlas.rs:404-475, epaxos.rs:370-428). */
+int fx_quorum_sizes(uint32_t protocol, uint32_t n, uint32_t f, uint32_t* fast_quorum,
+                    uint32_t* write_quorum);
+
 /* ------------------------------------------------------- execution log */
 /* Reader for the run mode's execution log: LengthDelimitedCodec frames
  * (4-byte big-endian length) of bincode-1 GraphExecutionInfo, as written by

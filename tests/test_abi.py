@@ -166,3 +166,14 @@ def test_dense_stats_match_the_histogram_oracle():
     assert math.isclose(st["mean"], h.mean(), rel_tol=1e-12)
     assert math.isclose(st["p99"], h.percentile(0.99), rel_tol=1e-12)
     assert metrics.dense_stats(np.zeros(8)) == {"count": 0, "clamped": 0}
+
+
+def test_quorum_sizes_kats():
+    # config.rs atlas_parameters / epaxos_parameters tests
+    A, E = _lib.FX_PROTOCOL_ATLAS, _lib.FX_PROTOCOL_EPAXOS
+    assert [_lib.quorum_sizes(A, 7, f) for f in (1, 2, 3)] == [(4, 2), (5, 3), (6, 4)]
+    assert [_lib.quorum_sizes(E, n) for n in (3, 5, 7, 9, 11, 13, 15, 17)] == \
+        [(2, 2), (3, 3), (5, 4), (6, 5), (8, 6), (9, 7), (11, 8), (12, 9)]
+    assert _lib.quorum_sizes(A, 3, 1) == (2, 2)  # BASELINE configs[0]: d <= 2
+    with pytest.raises(_lib.FxError):
+        _lib.quorum_sizes(7, 5, 1)
