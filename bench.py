@@ -77,8 +77,27 @@ def measured_copy_gbps(torch, dev, nbytes=2 << 30, reps=10):
     return round(gbps, 1)
 
 
+def launch_ranks(args):
+    """`bench.py --gpus N` (N > 1) without a torch.distributed launcher: start
+    N fresh ranks through torch.distributed.run as a child process BEFORE this
+    process touches the GPU, and exit with its status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -90,9 +109,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     lib = _lib.load()
@@ -129,11 +151,17 @@ def main():
     outb = _lib.OrderBatch(order.data_ptr(), release.data_ptr(), nexec.data_ptr(), err.data_ptr())
     hb = _lib.HistBatch(chain.data_ptr(), NBC, delay.data_ptr(), NBD)
 
-    # algorithmic bytes of one executor launch: read dot + hdr + the used dep
-    # words of every Add, write one order word + one release word per command
+    # algorithmic bytes of one executor launch, SURVEY.md §8(d): a packed input
+    # record of 20 + 4k + 8d bytes (header, seq, rifl, t, k key ids, d deps as
+    # (source, seq) pairs) plus a 12-byte output (dot + release step) per
+    # command = 32 + 4k + 8d, with k = 1 key per command and d read from the
+    # stream.  The packed planes this build actually streams (dot + hdr + 4 B per
+    # dep in, order + release out = 16 + 4d) are reported beside it.
     nd_total = int(((hdr >> 24) & 31).sum(dtype=torch.int64).item())
     n_adds = S * steps
-    alg_bytes = 16 * n_adds + 4 * nd_total
+    KEYS_PER_CMD = 1
+    alg_bytes = (32 + 4 * KEYS_PER_CMD) * n_adds + 8 * nd_total
+    plane_bytes = 16 * n_adds + 4 * nd_total
 
     tier = _lib.FX_TIER_DEFAULT if args.tier < 0 else args.tier
     tiered = [False]
@@ -174,6 +202,7 @@ def main():
 
     lib.fx_profile_enable(1)
     kernel_ms = []
+    kern_ms = {1: [], 2: []}  # split tier: group kernel, lane kernel (own-stream events)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -186,6 +215,9 @@ def main():
             # them after the step keeps the next launch queued behind this one
             if lib.fx_profile_last_exec_ms(ctypes.byref(ms)) == 0:
                 kernel_ms.append(ms.value)
+            for which in (1, 2):
+                if lib.fx_profile_last_kernel_ms(which, ctypes.byref(ms)) == 0:
+                    kern_ms[which].append(ms.value)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -218,21 +250,45 @@ def main():
     if rank == 0:
         roof = None
         if kavg:
-            achieved = alg_bytes / (kavg * 1e-3) / 1e9
-            traffic = None
+            # dominant kernel: the longest-running kernel of the launch, timed by
+            # HIP events on the stream it was launched on (the split tier runs
+            # the group kernel on the caller's stream and the lane kernel on an
+            # auxiliary one, concurrently); other tiers are one kernel
+            kname, dom_ms = KERNEL_NAMES.get(tier, "tier%d" % tier), kavg
+            per_kernel = {}
+            for which, nm in ((1, "k_graph_group"), (2, "k_graph_lane")):
+                if kern_ms[which]:
+                    per_kernel[nm] = round(sum(kern_ms[which]) / len(kern_ms[which]), 4)
+            if per_kernel:
+                kname = max(per_kernel, key=per_kernel.get)
+                dom_ms = per_kernel[kname]
+            achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
+            traffic = traffic_raw = traffic_read = traffic_write = None
             if os.path.exists(args.traffic_json):
                 try:
                     tj = json.load(open(args.traffic_json))
                     if tj.get("workload_key") == workload_key(args) and \
                             tj.get("kernel") == KERNEL_NAMES.get(tier):
                         traffic = tj.get("hbm_bytes_per_launch")
+                        traffic_raw = int(tj["fetch_size_kb"] * 1024 + tj["write_size_kb"] * 1024)
+                        traffic_read = tj.get("read_bytes_per_launch")
+                        traffic_write = tj.get("write_bytes_per_launch")
                 except Exception:
                     traffic = None
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                    "traffic": traffic, "kernel": KERNEL_NAMES.get(tier, "tier%d" % tier),
-                    "kernel_ms_avg": round(kavg, 4), "alg_bytes_per_launch": alg_bytes,
-                    "alg_bytes_per_cmd": round(alg_bytes / n_adds, 3)}
+                    "traffic": traffic, "kernel": kname,
+                    "kernel_ms_avg": round(dom_ms, 4), "per_kernel_ms_avg": per_kernel,
+                    "launch_ms_avg": round(kavg, 4),
+                    "alg_bytes_per_launch": alg_bytes,
+                    "alg_bytes_per_cmd": round(alg_bytes / n_adds, 3),
+                    "alg_bytes_definition": "SURVEY.md 8(d): 32 + 4k + 8d per command, k = 1",
+                    "plane_bytes_per_launch": plane_bytes,
+                    "plane_bytes_per_cmd": round(plane_bytes / n_adds, 3),
+                    "plane_frac_of_launch": round(plane_bytes / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                    "traffic_fetch_plus_write_raw": traffic_raw,
+                    "traffic_read_corrected_x2": traffic_read,
+                    "traffic_write": traffic_write}
             copy = measured_copy_gbps(torch, dev)
             roof["measured_copy_gbps"] = copy
             roof["frac_of_measured_copy"] = round(achieved / copy, 4)
@@ -256,10 +312,13 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (seeded Atlas/EPaxos-like commit streams generated on device)",
+            "data": "synthetic commit streams shaped like EPaxos n=5 (seeded, generated on device; "
+                    "deps = latest same-key command of every process within a horizon, not an "
+                    "EPaxos fast-quorum union)",
             "config": {
-                "workload": "EPaxos n=%d, %d seeds x conflict {%s}%%, %d cmds/process, 1 client/region "
-                            "(BASELINE configs[1])" % (args.n, args.seeds, args.conflicts, args.cmds),
+                "workload": "synthetic EPaxos-shaped commit streams, n=%d, %d seeds x conflict {%s}%%, "
+                            "%d cmds/process, 1 client/region (BASELINE configs[1] shape)"
+                            % (args.n, args.seeds, args.conflicts, args.cmds),
                 "instances_per_gpu": instances, "streams_per_gpu": S, "adds_per_stream": steps,
                 "window": args.window, "cycle_pct": args.cycle_pct, "seed": args.seed,
                 "instance_order": "conflict-major (%d instances per rate)" % cblock if cblock
@@ -283,6 +342,35 @@ def main():
     return result
 
 
+def host_cpus():
+    """Host cores for the CPU baseline: every core this process may run on
+    (nproc = os.cpu_count(); the scheduler affinity and the cgroup CPU quota
+    can be lower on a shared GPU box, and threads beyond them only time-slice)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except Exception:
+        quota = None
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    usable = min(nproc, aff, quota) if quota else min(nproc, aff)
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": usable,
+            "model": model}
+
+
 def workload_key(args):
     return "n%d_s%d_c%s_m%d_w%d_y%d_seed%d_b%d_t%d" % (
         args.n, args.seeds, args.conflicts.replace(",", "-"), args.cmds, args.window,
@@ -300,12 +388,13 @@ def cpu_baseline(args, lib, dot, hdr, deps, order, release, nexec, S, steps, dma
     from fantoch_amd import streams as fs
     from oracle import oracle_lib
 
-    threads = max(1, min(16, os.cpu_count() or 1))
+    host = host_cpus()
+    threads = host["usable"]
     full_tiles = S // 64
     if full_tiles == 0:
         return None
     # calibrate: ~3.5M Adds/s per thread over the mixed batch (measured) -> whole tiles
-    budget_adds = args.cpu_baseline_seconds * 3.5e6 * threads
+    budget_adds = args.cpu_baseline_seconds * 3.5e6 * min(threads, 64)
     tiles = int(max(1, min(full_tiles, budget_adds // (64 * steps))))
     pick = np.unique(np.linspace(0, full_tiles - 1, tiles).round().astype(np.int64))
     tiles = len(pick)
@@ -337,6 +426,7 @@ def cpu_baseline(args, lib, dot, hdr, deps, order, release, nexec, S, steps, dma
         ridx = np.concatenate([fs.index(np.arange(steps), s, steps) for s in range(Ss)])
         parity = parity and bool(np.array_equal(g_rel[ridx], o_rel[ridx]))
     return {"value": round(executed / dt, 1), "unit": "cmds/s", "cores": threads, "kind": "port",
+            "host": host,
             "sample": "%d of %d 64-stream tiles spread evenly over the batch (%d streams, %d Adds, "
                       "every conflict rate in proportion), %.2f s wall on %d threads; GPU output "
                       "on the sample %s the oracle bit-for-bit"

@@ -170,6 +170,7 @@ SIGNATURES = [
     ("fx_graph_executor_pending", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.POINTER(CDot), ctypes.c_uint32, u32p]),
     ("fx_graph_executor_parallel", ctypes.c_int, []),
+    ("fx_graph_executor_transfer_stats", ctypes.c_int, [ctypes.c_void_p, u64p, u64p]),
     ("fx_quorum_sizes", ctypes.c_int,
      [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p]),
     ("fx_exec_log_scan", ctypes.c_int,
@@ -190,6 +191,7 @@ SIGNATURES = [
     ("fx_dev_synchronize", ctypes.c_int, [ctypes.c_void_p]),
     ("fx_profile_enable", ctypes.c_int, [ctypes.c_int]),
     ("fx_profile_last_exec_ms", ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
+    ("fx_profile_last_kernel_ms", ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_float)]),
     ("fx_status_string", ctypes.c_char_p, [ctypes.c_int]),
     ("fx_version", ctypes.c_char_p, []),
 ]

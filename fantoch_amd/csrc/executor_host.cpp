@@ -85,7 +85,8 @@ struct fx_graph_executor {
   std::deque<std::pair<uint32_t, bool>> executed;  // (packed dot, scc start)
   std::map<uint64_t, uint64_t> chain_size, execution_delay;
   std::map<uint32_t, std::vector<fx_rifl>> monitor;
-  std::vector<uint32_t> release_host;
+  DevBuf d_gather;            // release steps of the entries of one flush
+  uint64_t bytes_h2d = 0, bytes_d2h = 0;  // transfer accounting (fx_graph_executor_transfer_stats)
   int sticky = FX_OK;
 };
 
@@ -106,6 +107,7 @@ int upload_all(fx_graph_executor* ex, uint32_t new_cap, uint32_t new_dmax) {
     hh[at] = ex->hdrs[i];
     for (uint32_t j = 0; j < ex->deps[i].size(); ++j) hp[j * plane + at] = ex->deps[i][j];
   }
+  ex->bytes_h2d += (uint64_t)(hd.size() + hh.size() + hp.size()) * 4;
   if (hipMemcpyAsync(ex->d_dot.p, hd.data(), plane * 4, hipMemcpyHostToDevice, ex->stream) ||
       hipMemcpyAsync(ex->d_hdr.p, hh.data(), plane * 4, hipMemcpyHostToDevice, ex->stream) ||
       hipMemcpyAsync(ex->d_deps.p, hp.data(), hp.size() * 4, hipMemcpyHostToDevice, ex->stream) ||
@@ -132,6 +134,7 @@ int upload_tail(fx_graph_executor* ex) {
     hh[at] = ex->hdrs[i];
     for (uint32_t j = 0; j < ex->deps[i].size(); ++j) hp[j * words + at] = ex->deps[i][j];
   }
+  ex->bytes_h2d += (uint64_t)(hd.size() + hh.size() + hp.size()) * 4;
   if (hipMemcpyAsync(ex->d_dot.u32() + w0, hd.data(), words * 4, hipMemcpyHostToDevice, ex->stream) ||
       hipMemcpyAsync(ex->d_hdr.u32() + w0, hh.data(), words * 4, hipMemcpyHostToDevice, ex->stream))
     return FX_ERR_HIP;
@@ -172,7 +175,11 @@ int flush(fx_graph_executor* ex) {
   fx_order_batch out{ex->d_order.u32(), ex->d_release.u32(), ex->d_nexec.u32(), ex->d_err.u32()};
   uint32_t nexec = 0, err = 0;
   while (true) {
-    if (ex->tier == FX_TIER_WAVE && in.dmax > 14) {  // wider Adds than the wave tier reads
+    // wider Adds than the current tier reads start over one tier up, as
+    // fx_batch_run_tiered picks its first tier (group: <= GROUP_LANES deps,
+    // wave: <= WAVE_MAX_DEPS)
+    if ((ex->tier == FX_TIER_WAVE && in.dmax > fx::WAVE_MAX_DEPS) ||
+        (ex->tier == FX_TIER_GROUP && in.dmax > fx::GROUP_LANES)) {
       ex->tier = FX_TIER_LDS_LARGE;
       ex->processed = 0;
     }
@@ -220,14 +227,17 @@ int flush(fx_graph_executor* ex) {
       return ex->sticky = FX_ERR_HIP;
     for (uint32_t k = k0; k < nexec; ++k) order[k - k0] = rows[fx_index(k, 0, ex->cap) - fx_index(r0, 0, ex->cap)];
   }
+  // the release steps of exactly the commands converted below, gathered on
+  // the device (bytes moved per flush are linear in its new order entries)
+  std::vector<uint32_t> rel(nexec - k0);
   {
-    const uint32_t r1 = (N + 3) & ~3u;
-    std::vector<uint32_t> rows((size_t)r1 / 4 * 256);
-    if (hipMemcpyAsync(rows.data(), ex->d_release.p, rows.size() * 4, hipMemcpyDeviceToHost, ex->stream) ||
+    if (!ex->d_gather.ensure((size_t)(nexec - k0) * 4)) return ex->sticky = FX_ERR_HIP;
+    if (fx::gather_release(ex->d_order.u32(), ex->d_release.u32(), ex->cap, k0, nexec,
+                           ex->d_gather.u32(), ex->stream) ||
+        hipMemcpyAsync(rel.data(), ex->d_gather.p, rel.size() * 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipStreamSynchronize(ex->stream))
       return ex->sticky = FX_ERR_HIP;
-    ex->release_host.resize(N);
-    for (uint32_t i = 0; i < N; ++i) ex->release_host[i] = rows[fx_index(i, 0, ex->cap)];
+    ex->bytes_d2h += (uint64_t)(order.size() + rel.size()) * 4;
   }
   // convert (fetch_commands_to_execute -> execute), collecting metrics
   for (size_t x = 0; x < order.size(); ++x) {
@@ -240,7 +250,7 @@ int flush(fx_graph_executor* ex) {
       ex->chain_size[size] += 1;  // ChainSize (mod.rs:492-493)
     }
     if (!ex->cfg.execute_at_commit) {
-      const uint32_t rs = ex->release_host[rec];
+      const uint32_t rs = rel[x];
       const uint64_t delay = (uint64_t)FX_HDR_T(ex->hdrs[rs]) - FX_HDR_T(ex->hdrs[rec]);
       ex->execution_delay[delay] += 1;  // ExecutionDelay (mod.rs:514-518)
     }
@@ -439,6 +449,13 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
 }
 
 int fx_graph_executor_parallel(void) { return 1; }
+
+int fx_graph_executor_transfer_stats(const fx_graph_executor* ex, uint64_t* h2d, uint64_t* d2h) {
+  if (!ex || !h2d || !d2h) return FX_ERR_INVALID_ARG;
+  *h2d = ex->bytes_h2d;
+  *d2h = ex->bytes_d2h;
+  return FX_OK;
+}
 
 // ------------------------------------------------------------ histogram
 // histogram.rs:172-235

@@ -68,6 +68,18 @@ size_t split_scratch_bytes(uint32_t streams);
 constexpr uint32_t SPLIT_DEFAULT_THRESHOLD = 16;  // mean deps per Add x 8 at or above which
                                                   // a tile runs on the group tier
 
+// Per-kernel profiling of the split tier (fx_profile_last_kernel_ms): HIP
+// events recorded on each kernel's own stream around its launch, so the
+// dominant kernel's duration is measured where it runs.
+bool profile_on();
+void split_profile_record(int which, bool end, hipStream_t s);
+
+// Single-stream gather used by the executor handle: out[k - k0] =
+// release[rec(order[k])] for k in [k0, k1), so a flush reads back only the
+// release steps of the commands it converts (bytes linear in the executed count).
+int gather_release(const uint32_t* order, const uint32_t* release, uint32_t steps, uint32_t k0,
+                   uint32_t k1, uint32_t* out, hipStream_t stream);
+
 // Decodes the pending vertices of lane `lane` from a saved state block
 // (tier layout of graph_exec.hip).  Writes up to cap (dot, waiting_on) pairs;
 // returns the count.

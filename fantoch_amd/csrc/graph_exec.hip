@@ -827,6 +827,26 @@ __global__ __launch_bounds__(256) void k_metrics(const uint32_t* __restrict__ hd
   }
 }
 
+// ------------------------------------------------ single-stream gather
+__global__ __launch_bounds__(256) void k_gather_release(const uint32_t* __restrict__ order,
+                                                        const uint32_t* __restrict__ release,
+                                                        uint32_t steps, uint32_t k0, uint32_t k1,
+                                                        uint32_t* __restrict__ out) {
+  const uint32_t k = k0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= k1) return;
+  const uint32_t rec = FX_ORDER_REC(order[fx_index(k, 0, steps)]);
+  out[k - k0] = rec < steps ? release[fx_index(rec, 0, steps)] : FX_RELEASE_NONE;
+}
+
+int gather_release(const uint32_t* order, const uint32_t* release, uint32_t steps, uint32_t k0,
+                   uint32_t k1, uint32_t* out, hipStream_t stream) {
+  if (k1 <= k0) return FX_OK;
+  const uint32_t n = k1 - k0;
+  hipLaunchKernelGGL(k_gather_release, dim3((n + 255) / 256), dim3(256), 0, stream, order, release,
+                     steps, k0, k1, out);
+  return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
+}
+
 // ----------------------------------------------------------- synthesis
 __global__ __launch_bounds__(256) void k_synth(fx_synth_params p, uint32_t S, uint32_t steps,
                                                uint32_t* dot, uint32_t* hdr, uint32_t* deps) {
@@ -916,6 +936,19 @@ uint32_t decode_pending(uint32_t tier, const uint32_t* block, uint32_t lane, uin
 static bool g_profile = false;
 static hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
 static bool g_ev_valid = false;
+// split-tier kernels: [1] group kernel (caller's stream), [2] lane kernel (aux stream)
+static hipEvent_t g_kev[3][2] = {};
+static bool g_kev_valid[3] = {};
+
+bool profile_on() { return g_profile; }
+
+void split_profile_record(int which, bool end, hipStream_t s) {
+  if (!g_profile || which < 1 || which > 2) return;
+  hipEvent_t& e = g_kev[which][end ? 1 : 0];
+  if (!e && hipEventCreate(&e) != hipSuccess) return;
+  (void)hipEventRecord(e, s);
+  g_kev_valid[which] = end;
+}
 
 }  // namespace fx
 
@@ -1027,6 +1060,7 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
       if (hipEventCreate(&g_ev0) != hipSuccess || hipEventCreate(&g_ev1) != hipSuccess) return FX_ERR_HIP;
     }
     (void)hipEventRecord(g_ev0, hs);
+    g_kev_valid[1] = g_kev_valid[2] = false;
   }
   switch (tier) {
     case 0: st = launch_group(a, hs); break;
@@ -1048,7 +1082,16 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
 int fx_profile_enable(int on) {
   g_profile = on != 0;
   g_ev_valid = false;
+  g_kev_valid[1] = g_kev_valid[2] = false;
   return FX_OK;
+}
+
+int fx_profile_last_kernel_ms(uint32_t which, float* ms) {
+  if (!ms) return FX_ERR_INVALID_ARG;
+  if (which == 0) return fx_profile_last_exec_ms(ms);
+  if (which > 2 || !g_kev_valid[which]) return FX_ERR_INVALID_ARG;
+  if (hipEventSynchronize(g_kev[which][1]) != hipSuccess) return FX_ERR_HIP;
+  return hipEventElapsedTime(ms, g_kev[which][0], g_kev[which][1]) == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 
 int fx_profile_last_exec_ms(float* ms) {

@@ -162,8 +162,14 @@ int launch_split(const KArgs& a0, void* scratch, hipStream_t hs) {
   if (thr < NB) {
     if (hipEventRecord(g_fork, hs) != hipSuccess || hipStreamWaitEvent(g_aux, g_fork, 0) != hipSuccess)
       return FX_ERR_HIP;
-    if (thr > 0) st = launch_lane(lt, g_aux);
+    if (thr > 0) {
+      split_profile_record(2, false, g_aux);
+      st = launch_lane(lt, g_aux);
+      split_profile_record(2, true, g_aux);
+    }
+    split_profile_record(1, false, hs);
     const int st2 = launch_group(h, hs);
+    split_profile_record(1, true, hs);
     if (hipEventRecord(g_join, g_aux) != hipSuccess || hipStreamWaitEvent(hs, g_join, 0) != hipSuccess)
       return FX_ERR_HIP;
     if (st2) return st2;

@@ -122,3 +122,10 @@ class GraphExecutor:
         check(_lib.load().fx_graph_executor_pending(self._h, buf, wb, 64, ctypes.byref(got)))
         return [((buf[i].source, buf[i].seq), (wb[i].source, wb[i].seq))
                 for i in range(min(got.value, 64))]
+
+    def transfer_stats(self):
+        """(host-to-device, device-to-host) bytes moved by this handle so far."""
+        h2d, d2h = ctypes.c_uint64(), ctypes.c_uint64()
+        check(_lib.load().fx_graph_executor_transfer_stats(self._h, ctypes.byref(h2d),
+                                                           ctypes.byref(d2h)))
+        return h2d.value, d2h.value

@@ -289,6 +289,9 @@ int fx_graph_executor_monitor(fx_graph_executor* ex, uint32_t key, fx_rifl* out,
 int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiting_on, uint32_t cap, uint32_t* n_out);
 /* Executor::parallel (executor.rs:103-105). */
 int fx_graph_executor_parallel(void);
+/* Host<->device bytes this handle has moved so far (not in the reference; lets
+ * a test check that draining after every Add moves bytes linear in the Adds). */
+int fx_graph_executor_transfer_stats(const fx_graph_executor* ex, uint64_t* h2d, uint64_t* d2h);
 
 /* ------------------------------------------------------- quorum sizes */
 #define FX_PROTOCOL_ATLAS 0u
@@ -366,6 +369,11 @@ int fx_dev_synchronize(void* hip_stream);
  * fx_profile_enable(1) is set (bench roofline; 0 disables the events). */
 int fx_profile_enable(int on);
 int fx_profile_last_exec_ms(float* ms);
+/* Per-kernel duration of the last profiled launch: which = 0 the whole
+ * executor launch (as fx_profile_last_exec_ms), 1 the group kernel and 2 the
+ * lane kernel of FX_TIER_SPLIT (events recorded on each kernel's own stream);
+ * FX_ERR_INVALID_ARG if that kernel did not run. */
+int fx_profile_last_kernel_ms(uint32_t which, float* ms);
 const char* fx_status_string(int status);
 const char* fx_version(void);
 

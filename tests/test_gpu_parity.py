@@ -339,6 +339,63 @@ def test_executor_metrics_and_results_match_oracle(gpu):
     assert ex.metrics(EXECUTION_DELAY) == g.metrics(0)
 
 
+def test_executor_wide_adds_match_oracle(gpu):
+    """Adds with 17-31 deps (beyond the group tier's 16 lanes) must not poison
+    the handle: it starts such a log one tier up (executor_host.cpp)."""
+    n = 8
+    ex = GraphExecutor(1, 0, n, monitor=True)
+    g = oracle_lib.Graph(1, n)
+    rng = np.random.default_rng(17)
+    seqs = {p: 0 for p in range(1, n + 1)}
+    issued = []
+    for i in range(300):
+        src = int(rng.integers(1, n + 1))
+        seqs[src] += 1
+        dot = (src, seqs[src])
+        pool = [d for d in issued[-60:] if d != dot]
+        k = int(rng.integers(0, min(len(pool), 31) + 1)) if i % 5 else min(len(pool), 24)
+        deps = [pool[j] for j in sorted(rng.choice(len(pool), size=k, replace=False))] if k else []
+        # a few deps on not-yet-issued dots of other sources (pending waits)
+        if i % 7 == 3:
+            other = 1 + src % n
+            deps.append((other, seqs[other] + 1))
+        deps = sorted(set(deps))
+        ex.handle_add(dot, dot, [0], deps, i)
+        g.handle_add(dot, deps, i)
+        issued.append(dot)
+        if i % 11 == 0:
+            ex.to_clients_iter()
+    # deliver the dots waited on but never issued, so every Add executes
+    for p in range(1, n + 1):
+        for q in range(seqs[p] + 1, seqs[p] + 3):
+            ex.handle_add((p, q), (p, q), [0], [], 400)
+            g.handle_add((p, q), [], 400)
+    assert [d for d, _ in ex.drain_dots()] == [d for d, _, _ in g.drain()]
+    assert ex.metrics(CHAIN_SIZE) == g.metrics(1)
+    assert ex.metrics(EXECUTION_DELAY) == g.metrics(0)
+
+
+def test_executor_drain_after_every_add_is_linear(gpu):
+    """The simulator drains to_clients after every handle (runner.rs:406-424):
+    bytes moved per drained Add must not grow with the log length."""
+    p = fs.synth_params(seed=9, n=3, instances=1, cmds=10_000, window=8, cycle_pct=30)
+    planes = fs.synth_host(p)
+    stream = planes.stream(0)
+    ex = GraphExecutor(1, 0, 3, monitor=False)
+    marks = {}
+    for i, (dot, deps, t, _kind) in enumerate(stream):
+        ex.handle_add(dot, dot, [0], deps, t)
+        ex.to_clients_iter()
+        if i + 1 in (3_000, 30_000):
+            marks[i + 1] = sum(ex.transfer_stats())
+    assert len(stream) >= 30_000
+    per_add_small = marks[3_000] / 3_000
+    per_add_large = (marks[30_000] - marks[3_000]) / 27_000
+    # linear: the later Adds cost no more per Add than the early ones (capacity
+    # doubling re-uploads are amortised); quadratic would be ~10x here
+    assert per_add_large < 2.0 * per_add_small + 64, (per_add_small, per_add_large)
+
+
 def test_cpp_executor_tests(gpu):
     exe = os.path.join(ROOT, "tests", "cpp", "build", "test_graph_executor")
     assert os.path.exists(exe), "build with `make`"
