@@ -20,9 +20,10 @@ all: $(LIB) $(ORACLE) $(CPPTEST)
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
 
-$(ORACLE): oracle/graph_oracle.cpp include/fantoch_amd.h
+ORACLE_SRCS := oracle/graph_oracle.cpp oracle/sim_oracle.cpp
+$(ORACLE): $(ORACLE_SRCS) oracle/graph_oracle.hpp include/fantoch_amd.h
 	@mkdir -p oracle/build
-	$(CXX) -O2 -std=c++17 -fPIC -shared -Wall -o $@ oracle/graph_oracle.cpp -lpthread
+	$(CXX) -O2 -std=c++17 -fPIC -shared -Wall -o $@ $(ORACLE_SRCS) -lpthread
 
 # C++ port of the reference's graph unit tests against the C++ Executor mirror
 $(CPPTEST): tests/cpp/test_graph_executor.cpp include/fantoch_amd.hpp include/fantoch_amd.h $(LIB)

@@ -296,12 +296,42 @@ int fx_graph_executor_transfer_stats(const fx_graph_executor* ex, uint64_t* h2d,
 /* ------------------------------------------------------- quorum sizes */
 #define FX_PROTOCOL_ATLAS 0u
 #define FX_PROTOCOL_EPAXOS 1u
+#define FX_PROTOCOL_BASIC 2u  /* fantoch/src/protocol/basic.rs (the simulator's own test protocol) */
 /* Fast and write quorum sizes of the commit-stream producers:
  * Config::atlas_quorum_sizes (fantoch/src/config.rs:294-301) and
  * Config::epaxos_quorum_sizes (config.rs:303-312, f ignored).  The deps of a
  * commit are a union over the fast quorum (atlas.rs:404-475, epaxos.rs:370-428). */
 int fx_quorum_sizes(uint32_t protocol, uint32_t n, uint32_t f, uint32_t* fast_quorum,
                     uint32_t* write_quorum);
+
+/* --------------------------------------------------- batched simulator */
+/* One simulated instance: Runner::new(planet, config, workload,
+ * clients_per_process, process_regions, client_regions) + Runner::run
+ * (fantoch/src/sim/runner.rs:64-231) with the GCP planet.  Regions are
+ * indices into the planet's regions in name order (canonical C12); process i
+ * (id i + 1) sits in process_regions[i]. */
+#define FX_SIM_MAX_N 8u
+#define FX_SIM_MAX_CLIENT_REGIONS 20u
+typedef struct fx_sim_spec {
+  uint64_t seed;                       /* canonical C6 RNG seed                       */
+  uint64_t instance;                   /* global instance index (RNG stream)          */
+  uint32_t protocol;                   /* FX_PROTOCOL_{ATLAS,EPAXOS,BASIC}            */
+  uint32_t n, f;                       /* Config::new(n, f)                           */
+  uint32_t gc_interval_ms;             /* Config::gc_interval (0 = None)              */
+  uint32_t executed_notification_ms;   /* Config::executor_executed_notification_interval */
+  uint32_t clients_per_region;         /* Runner::new clients_per_process             */
+  uint32_t commands_per_client;        /* Workload::commands_per_client               */
+  uint32_t keys_per_command;           /* Workload::keys_per_command (1 or 2)         */
+  uint32_t conflict_rate;              /* KeyGen::ConflictPool::conflict_rate (%)     */
+  uint32_t pool_size;                  /* KeyGen::ConflictPool::pool_size             */
+  uint32_t read_only_pct;              /* Workload::read_only_percentage              */
+  int32_t extra_sim_time_ms;           /* Runner::run(extra_sim_time): -1 = None      */
+  uint32_t reorder_messages;           /* Runner::reorder_messages (C6 multiplier)    */
+  uint32_t nfr;                        /* Config::nfr                                 */
+  uint32_t num_client_regions;
+  uint8_t process_regions[FX_SIM_MAX_N];
+  uint8_t client_regions[FX_SIM_MAX_CLIENT_REGIONS];
+} fx_sim_spec;
 
 /* ------------------------------------------------------- execution log */
 /* Reader for the run mode's execution log: LengthDelimitedCodec frames

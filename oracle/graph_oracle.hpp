@@ -1,0 +1,315 @@
+// oracle/graph_oracle.hpp — TEST INFRASTRUCTURE ONLY.
+//
+// The CPU restatement of fantoch_ps's DependencyGraph (see graph_oracle.cpp
+// for the reference map), shared by the plane-layout batch oracle
+// (graph_oracle.cpp) and the simulator oracle (sim_oracle.cpp).
+#pragma once
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <stdexcept>
+#include <thread>
+#include <vector>
+
+
+namespace oracle {
+
+// fantoch/src/id.rs:21-27 — Id<ProcessId>{source, sequence}, derived Ord.
+struct Dot {
+  uint32_t source = 0;
+  uint64_t sequence = 0;
+  bool operator<(const Dot& o) const {
+    return source != o.source ? source < o.source : sequence < o.sequence;
+  }
+  bool operator==(const Dot& o) const { return source == o.source && sequence == o.sequence; }
+  bool operator!=(const Dot& o) const { return !(*this == o); }
+};
+
+// threshold::AboveExSet — events 1..=max are all present, plus the exception
+// set `exs` of events above max.
+struct AboveExSet {
+  uint64_t max = 0;
+  std::set<uint64_t> exs;
+  // AboveExSet::add: returns whether the event is new.
+  bool add(uint64_t event) {
+    if (event == max + 1) {
+      max = event;
+      // compress: absorb exceptions that are now contiguous
+      while (true) {
+        auto it = exs.find(max + 1);
+        if (it == exs.end()) break;
+        exs.erase(it);
+        max += 1;
+      }
+      return true;
+    } else if (event > max + 1) {
+      return exs.insert(event).second;
+    }
+    return false;
+  }
+  bool contains(uint64_t event) const { return event <= max || exs.count(event) > 0; }
+};
+
+// threshold::AEClock<ProcessId> — one AboveExSet per actor
+// (AEClock::with(ids), graph/mod.rs:90-94).
+struct AEClock {
+  std::map<uint32_t, AboveExSet> clock;
+  bool contains(uint32_t actor, uint64_t event) const {
+    auto it = clock.find(actor);
+    return it != clock.end() && it->second.contains(event);
+  }
+  bool add(uint32_t actor, uint64_t event) { return clock[actor].add(event); }
+};
+
+// graph/tarjan.rs:319-356
+struct Vertex {
+  Dot dot;
+  uint32_t rec = 0;              // arrival index in the stream (stands in for `cmd`)
+  std::vector<Dot> deps;         // canonical C1: ascending
+  uint64_t start_time_ms = 0;
+  size_t id = 0;
+  size_t low = 0;
+  bool on_stack = false;
+};
+
+enum class FinderResult { Found, MissingDependencies, NotPending, NotFound };
+
+// One executed command as the executor emits it (save_scc, mod.rs:488-523).
+struct Executed {
+  Dot dot;
+  uint32_t rec;
+  bool scc_start;
+  uint64_t delay_ms;
+};
+
+struct DependencyGraph {
+  uint32_t process_id;
+  uint32_t n;
+  AEClock executed_clock;
+  std::map<Dot, std::unique_ptr<Vertex>> vertex_index;  // VertexIndex (index.rs:18-51)
+  std::map<Dot, std::set<Dot>> pending_index;           // PendingIndex (index.rs:145-208), C2
+  // TarjanSCCFinder (tarjan.rs:25-33)
+  size_t finder_id = 0;
+  std::vector<Dot> stack;
+  std::vector<std::set<Dot>> sccs;  // SCC = BTreeSet<Dot> (tarjan.rs:15)
+  // to_execute (mod.rs:59)
+  std::vector<Executed> to_execute;
+  // metrics (mod.rs:492-518)
+  std::map<uint64_t, uint64_t> chain_size;
+  std::map<uint64_t, uint64_t> execution_delay;
+
+  DependencyGraph(uint32_t pid, uint32_t n_) : process_id(pid), n(n_) {
+    // AEClock::with(all process ids) — mod.rs:90-94
+    for (uint32_t p = 1; p <= n; ++p) executed_clock.clock[p];
+  }
+
+  Vertex* find(const Dot& d) {
+    auto it = vertex_index.find(d);
+    return it == vertex_index.end() ? nullptr : it->second.get();
+  }
+
+  // VertexIndex::index (index.rs:33-37); returns false if already indexed.
+  bool index(std::unique_ptr<Vertex> v) {
+    Dot d = v->dot;
+    auto res = vertex_index.emplace(d, nullptr);
+    if (!res.second) return false;
+    res.first->second = std::move(v);
+    return true;
+  }
+
+  // mod.rs:213-275; returns false on the double-index panic (mod.rs:233-237).
+  bool handle_add(const Dot& dot, uint32_t rec, std::vector<Dot> deps, uint64_t time_ms) {
+    auto v = std::make_unique<Vertex>();
+    v->dot = dot;
+    v->rec = rec;
+    std::sort(deps.begin(), deps.end());  // C1
+    deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
+    v->deps = std::move(deps);
+    v->start_time_ms = time_ms;
+    if (!index(std::move(v))) return false;
+
+    size_t initial_ready = to_execute.size();
+    size_t total_scc_count = 0;
+    std::vector<Dot> dots;
+    std::set<Dot> visited;
+    std::set<Dot> missing;
+    FinderResult r = find_scc(true, dot, total_scc_count, time_ms, dots, visited, missing);
+    if (r == FinderResult::Found) {
+      check_pending(dots, total_scc_count, time_ms);
+    } else if (r == FinderResult::MissingDependencies) {
+      index_pending(dot, missing);
+      check_pending(dots, total_scc_count, time_ms);
+    } else {
+      throw std::logic_error("just added dot must be pending");  // mod.rs:257-259
+    }
+    if (to_execute.size() != initial_ready + total_scc_count)  // mod.rs:263
+      throw std::logic_error("newly ready commands not incorporated");
+    return true;
+  }
+
+  // mod.rs:409-486.  Out-params: dots of the SCCs saved, visited, missing deps.
+  FinderResult find_scc(bool first_find, const Dot& dot, size_t& total_scc_count, uint64_t time_ms,
+                        std::vector<Dot>& dots, std::set<Dot>& visited, std::set<Dot>& missing) {
+    size_t scc_count = 0;
+    size_t missing_deps_count = 0;
+    Dot result_missing;
+    FinderResult fr;
+    Vertex* v = find(dot);
+    if (v == nullptr) {
+      fr = FinderResult::NotPending;  // mod.rs:664-667
+    } else {
+      fr = strong_connect(first_find, dot, v, scc_count, missing_deps_count, result_missing);
+    }
+    total_scc_count += scc_count;
+    // save new SCCs (mod.rs:438-444)
+    std::vector<std::set<Dot>> found;
+    found.swap(sccs);
+    for (auto& scc : found) save_scc(scc, dots, time_ms);
+    // finalize (tarjan.rs:60-93): reset ids of the vertices still on the stack
+    finder_id = 0;
+    visited.clear();
+    while (!stack.empty()) {
+      Dot d = stack.back();
+      stack.pop_back();
+      Vertex* sv = find(d);
+      if (sv == nullptr) throw std::logic_error("stack member should exist");  // tarjan.rs:81-84
+      sv->id = 0;
+      visited.insert(d);
+    }
+    missing.clear();
+    switch (fr) {
+      case FinderResult::Found:
+        return FinderResult::Found;
+      case FinderResult::MissingDependencies:
+        missing.insert(result_missing);
+        return FinderResult::MissingDependencies;
+      case FinderResult::NotPending:
+        return FinderResult::NotPending;
+      case FinderResult::NotFound:
+      default:
+        // only reachable with partial replication (missing deps collected)
+        throw std::logic_error("either there's a missing dependency, or we should find an SCC");
+    }
+  }
+
+  // tarjan.rs:96-316 (shard_count == 1: give up on the first missing dep).
+  FinderResult strong_connect(bool first_find, const Dot& dot, Vertex* vertex, size_t& scc_count,
+                              size_t& missing_deps_count, Dot& missing_out) {
+    (void)first_find;
+    finder_id += 1;
+    vertex->id = finder_id;
+    vertex->low = finder_id;
+    vertex->on_stack = true;
+    stack.push_back(dot);
+
+    for (size_t i = 0; i < vertex->deps.size(); ++i) {
+      Dot dep_dot = vertex->deps[i];
+      // ignore self or already executed (tarjan.rs:128-145)
+      if (dep_dot == dot || executed_clock.contains(dep_dot.source, dep_dot.sequence)) continue;
+      Vertex* dep_vertex = find(dep_dot);
+      if (dep_vertex == nullptr) {
+        missing_out = dep_dot;  // tarjan.rs:148-157
+        return FinderResult::MissingDependencies;
+      }
+      if (dep_vertex->id == 0) {
+        size_t dep_missing_deps_count = 0;
+        FinderResult r = strong_connect(first_find, dep_dot, dep_vertex, scc_count,
+                                        dep_missing_deps_count, missing_out);
+        missing_deps_count += dep_missing_deps_count;
+        if (r == FinderResult::MissingDependencies) return r;  // tarjan.rs:202-204
+        vertex->low = std::min(vertex->low, dep_vertex->low);   // tarjan.rs:211
+      } else if (dep_vertex->on_stack) {
+        vertex->low = std::min(vertex->low, dep_vertex->id);    // tarjan.rs:217-221
+      }
+    }
+
+    if (missing_deps_count == 0 && vertex->id == vertex->low) {  // tarjan.rs:233
+      std::set<Dot> scc;
+      while (true) {
+        if (stack.empty()) throw std::logic_error("there should be an SCC member on the stack");
+        Dot member = stack.back();
+        stack.pop_back();
+        Vertex* mv = find(member);
+        if (mv == nullptr) throw std::logic_error("stack member should exist");
+        scc_count += 1;
+        mv->on_stack = false;
+        if (!scc.insert(member).second) throw std::logic_error("duplicate SCC member");
+        executed_clock.add(member.source, member.sequence);  // tarjan.rs:293
+        if (member == dot) break;
+      }
+      sccs.push_back(std::move(scc));
+      return FinderResult::Found;
+    }
+    return FinderResult::NotFound;
+  }
+
+  // mod.rs:488-523 — members in ascending Dot order (BTreeSet iteration).
+  void save_scc(const std::set<Dot>& scc, std::vector<Dot>& dots, uint64_t time_ms) {
+    chain_size[scc.size()] += 1;
+    bool first = true;
+    for (const Dot& d : scc) {
+      auto it = vertex_index.find(d);
+      if (it == vertex_index.end()) throw std::logic_error("dots from an SCC should exist");
+      std::unique_ptr<Vertex> v = std::move(it->second);
+      vertex_index.erase(it);
+      dots.push_back(d);
+      uint64_t duration = time_ms - v->start_time_ms;  // Vertex::into_command
+      execution_delay[duration] += 1;
+      to_execute.push_back(Executed{d, v->rec, first, duration});
+      first = false;
+    }
+  }
+
+  // mod.rs:525-554 + PendingIndex::index (index.rs:168-202); shard_count == 1
+  // means every dep is "mine", so no out-requests.
+  void index_pending(const Dot& dot, const std::set<Dot>& missing) {
+    for (const Dot& dep : missing) pending_index[dep].insert(dot);
+  }
+
+  // mod.rs:556-587 — LIFO over the released dots.
+  void check_pending(std::vector<Dot>& dots, size_t& total_scc_count, uint64_t time_ms) {
+    while (!dots.empty()) {
+      Dot d = dots.back();
+      dots.pop_back();
+      auto it = pending_index.find(d);  // PendingIndex::remove (index.rs:205-207)
+      if (it != pending_index.end()) {
+        std::set<Dot> pending = std::move(it->second);
+        pending_index.erase(it);
+        try_pending(pending, dots, total_scc_count, time_ms);
+      }
+    }
+  }
+
+  // mod.rs:589-642 — waiters in ascending Dot order (C2).
+  void try_pending(const std::set<Dot>& pending, std::vector<Dot>& dots, size_t& total_scc_count,
+                   uint64_t time_ms) {
+    std::set<Dot> visited;
+    for (const Dot& d : pending) {
+      if (visited.count(d)) continue;
+      std::vector<Dot> new_dots;
+      std::set<Dot> new_visited;
+      std::set<Dot> missing;
+      FinderResult r = find_scc(false, d, total_scc_count, time_ms, new_dots, new_visited, missing);
+      if (r == FinderResult::Found) {
+        visited.clear();
+        dots.insert(dots.end(), new_dots.begin(), new_dots.end());
+      } else if (r == FinderResult::MissingDependencies) {
+        index_pending(d, missing);
+        if (!new_dots.empty()) {
+          visited.clear();
+        } else {
+          visited.insert(new_visited.begin(), new_visited.end());
+        }
+        dots.insert(dots.end(), new_dots.begin(), new_dots.end());
+      }
+      // NotPending: nothing (mod.rs:635-638)
+    }
+  }
+};
+
+}  // namespace oracle
+

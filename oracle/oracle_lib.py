@@ -12,21 +12,23 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liboracle.so")
-SRC = os.path.join(HERE, "graph_oracle.cpp")
+SRCS = [os.path.join(HERE, f) for f in ("graph_oracle.cpp", "sim_oracle.cpp")]
+DEPS = SRCS + [os.path.join(HERE, "graph_oracle.hpp"),
+               os.path.join(os.path.dirname(HERE), "include", "fantoch_amd.h")]
 
 _lib = None
 
 
 def build():
     os.makedirs(os.path.join(HERE, "build"), exist_ok=True)
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB, SRC,
-                           "-lpthread"])
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB] + SRCS +
+                          ["-lpthread"])
 
 
 def load():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+        if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in DEPS):
             build()
         lib = ctypes.CDLL(LIB)
         vp = ctypes.c_void_p
@@ -162,3 +164,250 @@ class Graph:
         c = (ctypes.c_uint64 * 4096)()
         m = self.lib.oracle_graph_metrics(self.h, kind, v, c, 4096)
         return {int(v[i]): int(c[i]) for i in range(min(m, 4096))}
+
+
+# ------------------------------------------------------------ simulator
+ROOT = os.path.dirname(HERE)
+PLANET_DIR = os.path.join(ROOT, "fantoch_amd", "data", "latency_gcp")
+
+
+class SimSpec(ctypes.Structure):
+    """fx_sim_spec (include/fantoch_amd.h)."""
+    _fields_ = [("seed", ctypes.c_uint64), ("instance", ctypes.c_uint64),
+                ("protocol", ctypes.c_uint32), ("n", ctypes.c_uint32), ("f", ctypes.c_uint32),
+                ("gc_interval_ms", ctypes.c_uint32), ("executed_notification_ms", ctypes.c_uint32),
+                ("clients_per_region", ctypes.c_uint32), ("commands_per_client", ctypes.c_uint32),
+                ("keys_per_command", ctypes.c_uint32), ("conflict_rate", ctypes.c_uint32),
+                ("pool_size", ctypes.c_uint32), ("read_only_pct", ctypes.c_uint32),
+                ("extra_sim_time_ms", ctypes.c_int32), ("reorder_messages", ctypes.c_uint32),
+                ("nfr", ctypes.c_uint32), ("num_client_regions", ctypes.c_uint32),
+                ("process_regions", ctypes.c_uint8 * 8), ("client_regions", ctypes.c_uint8 * 20)]
+
+
+class SimOut(ctypes.Structure):
+    _fields_ = [("executed", ctypes.c_void_p), ("executed_len", ctypes.c_void_p),
+                ("exec_cap", ctypes.c_uint32), ("latency", ctypes.c_void_p), ("issued", ctypes.c_void_p),
+                ("R", ctypes.c_uint32), ("lat_bins", ctypes.c_uint32), ("fast", ctypes.c_void_p),
+                ("slow", ctypes.c_void_p), ("stable", ctypes.c_void_p), ("chain", ctypes.c_void_p),
+                ("delay", ctypes.c_void_p), ("chain_bins", ctypes.c_uint32),
+                ("delay_bins", ctypes.c_uint32), ("end_ms", ctypes.c_uint64),
+                ("events", ctypes.c_uint64), ("trace", ctypes.c_uint64), ("status", ctypes.c_int32),
+                ("pad", ctypes.c_int32), ("monitor_hash", ctypes.c_void_p)]
+
+
+def _sim_lib():
+    lib = load()
+    if not getattr(lib, "_sim_bound", False):
+        lib.oracle_planet_regions.restype = ctypes.c_int
+        lib.oracle_planet_regions.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32]
+        lib.oracle_planet_matrix.restype = ctypes.c_int
+        lib.oracle_planet_matrix.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_uint32]
+        lib.oracle_sort_processes.restype = ctypes.c_int
+        lib.oracle_sort_processes.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        lib.oracle_sim_run.restype = ctypes.c_int
+        lib.oracle_sim_run.argtypes = [ctypes.c_char_p, ctypes.POINTER(SimSpec), ctypes.POINTER(SimOut)]
+        lib.oracle_sim_batch.restype = ctypes.c_int
+        lib.oracle_sim_batch.argtypes = [ctypes.c_char_p, ctypes.POINTER(SimSpec), ctypes.c_uint32,
+                                         ctypes.POINTER(SimOut), ctypes.c_int]
+        lib._sim_bound = True
+    return lib
+
+
+def planet_regions(planet_dir=PLANET_DIR):
+    buf = ctypes.create_string_buffer(4096)
+    r = _sim_lib().oracle_planet_regions(planet_dir.encode(), buf, 4096)
+    if r < 0:
+        raise RuntimeError("cannot load planet %s" % planet_dir)
+    return buf.value.decode().split()
+
+
+def planet_matrix(planet_dir=PLANET_DIR):
+    R = len(planet_regions(planet_dir))
+    lat = np.zeros((R, R), np.int64)
+    srt = np.zeros((R, R), np.uint32)
+    if _sim_lib().oracle_planet_matrix(planet_dir.encode(), lat.ctypes.data, srt.ctypes.data, R):
+        raise RuntimeError("planet matrix")
+    return lat, srt
+
+
+def sort_processes(region, procs, planet_dir=PLANET_DIR):
+    """util.rs:153-185 over [(id, region index)] -> sorted ids."""
+    ids = np.array([p[0] for p in procs], np.uint32)
+    regs = np.array([p[1] for p in procs], np.uint32)
+    out = np.zeros(len(procs), np.uint32)
+    _sim_lib().oracle_sort_processes(planet_dir.encode(), region, ids.ctypes.data, regs.ctypes.data,
+                                     len(procs), out.ctypes.data)
+    return [int(x) for x in out]
+
+
+def make_spec(protocol, n, f, process_regions, client_regions, clients_per_region=1,
+              commands_per_client=100, keys_per_command=1, conflict_rate=2, pool_size=1,
+              read_only_pct=0, gc_interval_ms=10, executed_notification_ms=10,
+              extra_sim_time_ms=-1, reorder=False, nfr=False, seed=0, instance=0):
+    s = SimSpec()
+    s.seed, s.instance, s.protocol, s.n, s.f = seed, instance, protocol, n, f
+    s.gc_interval_ms, s.executed_notification_ms = gc_interval_ms, executed_notification_ms
+    s.clients_per_region, s.commands_per_client = clients_per_region, commands_per_client
+    s.keys_per_command, s.conflict_rate, s.pool_size = keys_per_command, conflict_rate, pool_size
+    s.read_only_pct, s.extra_sim_time_ms = read_only_pct, extra_sim_time_ms
+    s.reorder_messages, s.nfr = int(bool(reorder)), int(bool(nfr))
+    s.num_client_regions = len(client_regions)
+    for i, r in enumerate(process_regions):
+        s.process_regions[i] = r
+    for i, r in enumerate(client_regions):
+        s.client_regions[i] = r
+    return s
+
+
+class _OutBufs:
+    def __init__(self, spec, R, exec_cap, lat_bins, chain_bins, delay_bins):
+        n = spec.n
+        self.executed = np.zeros((n, exec_cap), np.uint32)
+        self.executed_len = np.zeros(n, np.uint64)
+        self.latency = np.zeros((R, lat_bins), np.uint64)
+        self.issued = np.zeros(R, np.uint64)
+        self.fast = np.zeros(n, np.uint64)
+        self.slow = np.zeros(n, np.uint64)
+        self.stable = np.zeros(n, np.uint64)
+        self.chain = np.zeros(chain_bins, np.uint64)
+        self.delay = np.zeros(delay_bins, np.uint64)
+        self.monitor_hash = np.zeros(n, np.uint64)
+        o = SimOut()
+        o.executed, o.executed_len, o.exec_cap = self.executed.ctypes.data, self.executed_len.ctypes.data, exec_cap
+        o.latency, o.issued, o.R, o.lat_bins = self.latency.ctypes.data, self.issued.ctypes.data, R, lat_bins
+        o.fast, o.slow, o.stable = self.fast.ctypes.data, self.slow.ctypes.data, self.stable.ctypes.data
+        o.chain, o.delay = self.chain.ctypes.data, self.delay.ctypes.data
+        o.chain_bins, o.delay_bins = chain_bins, delay_bins
+        o.monitor_hash = self.monitor_hash.ctypes.data
+        self.out = o
+
+    def result(self):
+        o = self.out
+        return {"executed": [self.executed[p, :int(self.executed_len[p])].copy()
+                             for p in range(self.executed.shape[0])],
+                "latency": self.latency, "issued": self.issued, "fast": self.fast,
+                "slow": self.slow, "stable": self.stable, "chain": self.chain, "delay": self.delay,
+                "end_ms": int(o.end_ms), "events": int(o.events), "trace": int(o.trace),
+                "status": int(o.status), "monitor_hash": self.monitor_hash}
+
+
+def sim_run(spec, exec_cap=None, lat_bins=8192, chain_bins=256, delay_bins=8192,
+            planet_dir=PLANET_DIR):
+    """Runs one simulated instance (Runner::run) through the C++ oracle."""
+    R = len(planet_regions(planet_dir))
+    if exec_cap is None:
+        exec_cap = spec.clients_per_region * spec.num_client_regions * spec.commands_per_client + 8
+    b = _OutBufs(spec, R, exec_cap, lat_bins, chain_bins, delay_bins)
+    _sim_lib().oracle_sim_run(planet_dir.encode(), ctypes.byref(spec), ctypes.byref(b.out))
+    r = b.result()
+    if r["status"]:
+        raise RuntimeError("oracle sim failed (status %d)" % r["status"])
+    return r
+
+
+def sim_batch(specs, threads=1, exec_cap=None, lat_bins=8192, chain_bins=256, delay_bins=8192,
+              planet_dir=PLANET_DIR):
+    """Runs many instances on `threads` std::threads; returns a list of results."""
+    R = len(planet_regions(planet_dir))
+    arr = (SimSpec * len(specs))(*specs)
+    bufs = []
+    outs = (SimOut * len(specs))()
+    for i, s in enumerate(specs):
+        cap = exec_cap or s.clients_per_region * s.num_client_regions * s.commands_per_client + 8
+        b = _OutBufs(s, R, cap, lat_bins, chain_bins, delay_bins)
+        bufs.append(b)
+        outs[i] = b.out
+    _sim_lib().oracle_sim_batch(planet_dir.encode(), arr, len(specs), outs, int(threads))
+    res = []
+    for i, b in enumerate(bufs):
+        b.out = outs[i]
+        res.append(b.result())
+    return res
+
+
+def pack(d):
+    return (int(d[0]) << 24) | int(d[1])
+
+
+def unpack(x):
+    return (int(x) >> 24, int(x) & 0xFFFFFF)
+
+
+def quorum_deps(fq, reports, threshold):
+    """QuorumDeps (quorum.rs:16-103): reports = [set of dots] from processes 1..;
+    returns (union, all, check_threshold(threshold), check_equal)."""
+    lib = load()
+    lib.oracle_quorum_deps.restype = ctypes.c_int
+    lens = np.array([len(r) for r in reports] + [0], np.uint32)
+    flat = np.array([pack(d) for r in reports for d in sorted(r)] + [0], np.uint32)
+    out = np.zeros(256, np.uint32)
+    nu, al, th, eq = (ctypes.c_uint32() for _ in range(4))
+    lib.oracle_quorum_deps(ctypes.c_uint32(fq), ctypes.c_uint32(len(reports)),
+                           ctypes.c_void_p(lens.ctypes.data), ctypes.c_void_p(flat.ctypes.data),
+                           ctypes.c_uint32(threshold), ctypes.c_void_p(out.ctypes.data),
+                           ctypes.c_uint32(256), ctypes.byref(nu), ctypes.byref(al), ctypes.byref(th),
+                           ctypes.byref(eq))
+    return {unpack(x) for x in out[:nu.value]}, bool(al.value), bool(th.value), bool(eq.value)
+
+
+def key_deps_script(ops, nfr=False):
+    """ops: ("add", dot, keys, read_only) | ("noop", dot) | ("deps", keys, read_only) |
+    ("noop_deps",) -> list of dep sets (one per op)."""
+    lib = load()
+    kind, dot, nk, keys, ro = [], [], [], [], []
+    for op in ops:
+        if op[0] == "add":
+            kind.append(0); dot.append(pack(op[1])); nk.append(len(op[2])); keys += op[2]; ro.append(int(op[3]))
+        elif op[0] == "noop":
+            kind.append(1); dot.append(pack(op[1])); nk.append(0); ro.append(0)
+        elif op[0] == "deps":
+            kind.append(2); dot.append(0); nk.append(len(op[1])); keys += op[1]; ro.append(int(op[2]))
+        else:
+            kind.append(3); dot.append(0); nk.append(0); ro.append(0)
+    cap = 64
+    a = lambda v: np.array(v + [0], np.uint32)
+    kind_a, dot_a, nk_a, keys_a, ro_a = a(kind), a(dot), a(nk), a(keys), a(ro)
+    out = np.zeros(len(ops) * cap, np.uint32)
+    olen = np.zeros(len(ops), np.uint32)
+    lib.oracle_key_deps_script(ctypes.c_uint32(int(nfr)), ctypes.c_uint32(len(ops)),
+                               *[ctypes.c_void_p(x.ctypes.data) for x in (kind_a, dot_a, nk_a, keys_a, ro_a)],
+                               ctypes.c_uint32(cap), ctypes.c_void_p(out.ctypes.data),
+                               ctypes.c_void_p(olen.ctypes.data))
+    return [{unpack(x) for x in out[i * cap:i * cap + olen[i]]} for i in range(len(ops))]
+
+
+def gc_script(n, ops):
+    """ops: ("add", dot) | ("update", from, [clock n]) | ("stable",) ->
+    list of (stable ranges or None, frontier after the op)."""
+    lib = load()
+    kind = np.array([{"add": 0, "update": 1, "stable": 2}[o[0]] for o in ops], np.uint32)
+    arg = np.array([pack(o[1]) if o[0] == "add" else (o[1] if o[0] == "update" else 0) for o in ops], np.uint32)
+    clocks = np.zeros((len(ops), n), np.uint64)
+    for i, o in enumerate(ops):
+        if o[0] == "update":
+            clocks[i] = o[2]
+    cap = 16
+    out = np.zeros((len(ops), cap, 3), np.uint64)
+    olen = np.zeros(len(ops), np.uint32)
+    fr = np.zeros((len(ops), n), np.uint64)
+    lib.oracle_gc_script(ctypes.c_uint32(n), ctypes.c_uint32(len(ops)),
+                         *[ctypes.c_void_p(x.ctypes.data) for x in (kind, arg, clocks)],
+                         ctypes.c_uint32(cap), ctypes.c_void_p(out.ctypes.data),
+                         ctypes.c_void_p(olen.ctypes.data), ctypes.c_void_p(fr.ctypes.data))
+    res = []
+    for i, o in enumerate(ops):
+        st = [tuple(int(v) for v in out[i, j]) for j in range(olen[i])] if o[0] == "stable" else None
+        res.append((st, [int(v) for v in fr[i]]))
+    return res
+
+
+def workload_keys(spec, client, count):
+    """Keys (and read-only flags) of the first `count` commands of `client`."""
+    lib = load()
+    keys = np.zeros(count * spec.keys_per_command, np.uint32)
+    ro = np.zeros(count, np.uint32)
+    lib.oracle_workload_keys(ctypes.byref(spec), ctypes.c_uint64(client), ctypes.c_uint32(count),
+                             ctypes.c_void_p(keys.ctypes.data), ctypes.c_void_p(ro.ctypes.data))
+    return keys.reshape(count, spec.keys_per_command), ro

@@ -352,9 +352,14 @@ def test_executor_wide_adds_match_oracle(gpu):
         src = int(rng.integers(1, n + 1))
         seqs[src] += 1
         dot = (src, seqs[src])
-        pool = [d for d in issued[-60:] if d != dot]
-        k = int(rng.integers(0, min(len(pool), 31) + 1)) if i % 5 else min(len(pool), 24)
-        deps = [pool[j] for j in sorted(rng.choice(len(pool), size=k, replace=False))] if k else []
+        # wide Adds: up to 27 old deps (long executed: ignored by every search,
+        # tarjan.rs:128-145) plus up to 4 recent ones that may still be pending
+        old_pool = issued[:-40]
+        recent = [d for d in issued[-40:] if d != dot]
+        k = int(rng.integers(0, min(len(old_pool), 27) + 1)) if i % 5 else min(len(old_pool), 24)
+        deps = [old_pool[j] for j in rng.choice(len(old_pool), size=k, replace=False)] if k else []
+        r = int(rng.integers(0, min(len(recent), 4) + 1))
+        deps += [recent[j] for j in rng.choice(len(recent), size=r, replace=False)] if r else []
         # a few deps on not-yet-issued dots of other sources (pending waits)
         if i % 7 == 3:
             other = 1 + src % n
