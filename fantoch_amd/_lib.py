@@ -25,8 +25,16 @@ FX_ERR_ORDER_OVERFLOW = 8
 FX_ERR_TIME_RANGE = 9
 FX_ERR_NO_DEVICE = 10
 FX_ERR_LOG_FORMAT = 11
+FX_ERR_SIM_CAPACITY = 12
+FX_ERR_SIM_LATE = 13
+FX_ERR_SIM_EVENTS = 14
 FX_PROTOCOL_ATLAS = 0
 FX_PROTOCOL_EPAXOS = 1
+FX_PROTOCOL_BASIC = 2
+FX_SIM_FLAG_EXEC_NOTIFICATIONS = 1
+FX_SIM_STAT_FAST, FX_SIM_STAT_SLOW, FX_SIM_STAT_STABLE = 0, 8, 16
+FX_SIM_STAT_EVENTS, FX_SIM_STAT_END_MS, FX_SIM_STAT_TRACE, FX_SIM_STAT_SEQ = 24, 25, 26, 27
+FX_SIM_STATS = 32
 
 FX_SEQ_BITS = 24
 FX_SEQ_MASK = (1 << 24) - 1
@@ -126,6 +134,38 @@ class HistStats(ctypes.Structure):
                 ("max", ctypes.c_double)]
 
 
+class SimSpec(ctypes.Structure):
+    """fx_sim_spec: one simulated instance (Runner::new + Runner::run)."""
+    _fields_ = [("seed", ctypes.c_uint64), ("instance", ctypes.c_uint64),
+                ("protocol", ctypes.c_uint32), ("n", ctypes.c_uint32), ("f", ctypes.c_uint32),
+                ("gc_interval_ms", ctypes.c_uint32), ("executed_notification_ms", ctypes.c_uint32),
+                ("clients_per_region", ctypes.c_uint32), ("commands_per_client", ctypes.c_uint32),
+                ("keys_per_command", ctypes.c_uint32), ("conflict_rate", ctypes.c_uint32),
+                ("pool_size", ctypes.c_uint32), ("read_only_pct", ctypes.c_uint32),
+                ("extra_sim_time_ms", ctypes.c_int32), ("reorder_messages", ctypes.c_uint32),
+                ("nfr", ctypes.c_uint32), ("num_client_regions", ctypes.c_uint32),
+                ("process_regions", ctypes.c_uint8 * 8), ("client_regions", ctypes.c_uint8 * 20)]
+
+
+class SimBatch(ctypes.Structure):
+    _fields_ = [("specs", ctypes.c_void_p), ("host_specs", ctypes.c_void_p),
+                ("instances", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("planet_ping", ctypes.c_void_p), ("planet_rank", ctypes.c_void_p),
+                ("planet_regions", ctypes.c_uint32), ("planet_stride", ctypes.c_uint32),
+                ("exec_cap", ctypes.c_uint32), ("lat_cap", ctypes.c_uint32),
+                ("max_events", ctypes.c_uint32), ("ring_entries", ctypes.c_uint32),
+                ("dot_slots", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
+class SimOutput(ctypes.Structure):
+    _fields_ = [("executed", ctypes.c_void_p), ("executed_len", ctypes.c_void_p),
+                ("latency_log", ctypes.c_void_p), ("latency_hist", ctypes.c_void_p),
+                ("chain_hist", ctypes.c_void_p), ("delay_hist", ctypes.c_void_p),
+                ("stats", ctypes.c_void_p), ("err", ctypes.c_void_p),
+                ("lat_bins", ctypes.c_uint32), ("chain_bins", ctypes.c_uint32),
+                ("delay_bins", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+
+
 # (name, restype, argtypes) of every symbol declared in include/fantoch_amd.h
 SIGNATURES = [
     ("fx_tier_query", ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(TierInfo)]),
@@ -171,6 +211,13 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.POINTER(CDot), ctypes.c_uint32, u32p]),
     ("fx_graph_executor_parallel", ctypes.c_int, []),
     ("fx_graph_executor_transfer_stats", ctypes.c_int, [ctypes.c_void_p, u64p, u64p]),
+    ("fx_sim_plan", ctypes.c_int,
+     [ctypes.POINTER(SimSpec), ctypes.c_uint32, ctypes.c_uint32, u32p]),
+    ("fx_sim_run", ctypes.c_int,
+     [ctypes.POINTER(SimBatch), ctypes.POINTER(SimOutput), ctypes.c_void_p]),
+    ("fx_planet_load", ctypes.c_int,
+     [ctypes.c_char_p, ctypes.c_uint32, u32p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
+      ctypes.c_void_p]),
     ("fx_quorum_sizes", ctypes.c_int,
      [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p]),
     ("fx_exec_log_scan", ctypes.c_int,

@@ -1,0 +1,1330 @@
+// sim_wave.hip — the batched simulator: ONE wavefront runs ONE simulated
+// instance of fantoch's discrete-event simulator (fantoch/src/sim/runner.rs)
+// with Atlas or EPaxos processes and their GraphExecutors, all state in LDS and
+// VGPRs, thousands of instances per launch.
+//
+// Event queue.  The reference keeps every pending action in one BinaryHeap
+// ordered by time (schedule.rs:6-61; ties FIFO here, canonical C3).  Every
+// action travels on a "link" whose delay is a constant (runner.rs:507-530,
+// distance = ping / 2, no reordering), so each link delivers in send order
+// and the heap is exactly a k-way merge of per-link FIFO queues:
+//   P(p,q)  process p -> process q messages (a ring of entries in LDS)
+//   S(c)    client c -> its process (SubmitToProc; one in flight: closed loop)
+//   R(c)    process -> client c (SendToClient; one in flight)
+//   G(p)    process p's periodic GarbageCollection event (runner.rs:179-183)
+//   E(p)    process p's periodic executed notification (runner.rs:184-187);
+//           GraphExecutor::executed is None (executor/mod.rs:74-79), so E
+//           events only matter for where a run with extra time stops, and are
+//           simulated only then
+// Lane l holds the head (time, insertion seq) of links l, l + 64, ...; the
+// next action is a wave-wide min-reduction over those heads.
+//
+// Handlers follow the reference's recursion exactly: a handler's actions
+// (Vec, popped LIFO, runner.rs:403) and execution infos are processed by
+// send_to_processes_and_executors (runner.rs:395-441), self-deliveries recurse
+// at their position in the target iteration (ascending ids, C4), and ready
+// command results are scheduled after the actions.  The recursion is an
+// explicit frame stack in LDS.
+//
+// Per-dot protocol state (SequentialCommandsInfo, info/sequential.rs) lives in
+// a per-instance dot table indexed by (source, seq mod W); a slot also holds
+// the payloads of every message about that dot (MCollect deps, each
+// MCollectAck's deps, the committed value), so a queued message is just
+// (time, seq, kind, dot).  A slot is freed once all n processes executed the
+// dot: by then no message about it can be in flight (every process needed
+// MCollect and MCommit to execute it, and the coordinator needed every
+// MCollectAck / MConsensusAck before committing).
+//
+// Executors: the wavefront-per-stream GraphExecutor of graph_wave.hip
+// (DependencyGraph::handle_add, graph/mod.rs:213-642, canonical C1/C2), one
+// state per process: lane l owns pending slot l (dot, start time, waited-on
+// dot, Tarjan word, DFS frame) and lane l < n the executed clock of source
+// l + 1; vertex deps are read from the dot table.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "fantoch_amd.h"
+#include "fx_internal.h"
+
+namespace fx {
+namespace sim {
+
+constexpr uint32_t NMAX = FX_SIM_MAX_N;  // processes
+constexpr uint32_t CMAX = 32;            // clients per instance
+constexpr uint32_t KMAX = 2;             // keys per command
+constexpr uint32_t VMAX = 16;            // deps of a committed value
+constexpr uint32_t AMAX = 4;             // deps of one MCollectAck
+constexpr uint32_t RS = 32;              // GC frontier snapshots kept per process
+constexpr uint32_t FMAX = 12;            // frame stack depth
+constexpr uint32_t RDMAX = 16;           // ready results per frame
+constexpr uint32_t HMAX = 3;             // link heads per lane (links <= 192)
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+// message kinds (numbering of the oracle's trace, sim_oracle.cpp MK)
+enum : uint32_t { M_COLLECT = 0, M_COLLECT_ACK = 1, M_COMMIT = 2, M_CONSENSUS = 3, M_CONSENSUS_ACK = 4,
+                  M_COMMIT_DOT = 5, M_GC = 6, M_STABLE = 7 };
+enum : uint32_t { ST_START = 0, ST_PAYLOAD = 1, ST_COLLECT = 2, ST_COMMIT = 3 };
+enum : uint32_t { PH_IDLE = 0, PH_DFS = 1, PH_TRY = 2, PH_CHECK = 3 };
+
+// dot-table slot (u32 words)
+constexpr uint32_t SL_DOT = 0, SL_CLIENT = 1, SL_IDX = 2, SL_KEYS = 3, SL_PST = 4,  // 4,5: per-process state bytes
+    SL_MASKS = 6, SL_CNT = 7, SL_COLLECT = 8, SL_VALUE = SL_COLLECT + KMAX, SL_ACK = SL_VALUE + VMAX,
+    SLOTW = SL_ACK + NMAX * AMAX;
+// per-process state byte: status(2) | buffered commit(1) | accepted(1) | buffered-from(4)
+// SL_MASKS: participants(8) | proposer accepts(8) | committed count(8) | executed count(8)
+// SL_CNT:   value count(8) | collect count(8) | proposer ballot set(1) << 16 | nkeys << 20
+
+// per-process words
+constexpr uint32_t PR_SEQ = 0, PR_FAST = 1, PR_SLOW = 2, PR_STABLE = 3, PR_EXEC = 4, PR_OCC = 5,  // 5,6
+    PR_WMASK = 7,                                                                                // 7,8
+    PR_EPOCH = 9, PR_TICK = 10, PR_GCF = 11, PR_GCW = PR_GCF + NMAX, PR_OTH = PR_GCW + NMAX,
+    PR_SEEN = PR_OTH + NMAX * NMAX, PR_PREV = PR_SEEN + 1, PR_FQ = PR_PREV + NMAX, PR_WQ = PR_FQ + 1,
+    PR_REGION = PR_WQ + 1, PRW = PR_REGION + 1;
+// per-client words
+constexpr uint32_t CL_PROC = 0, CL_ISSUED = 1, CL_START = 2, CL_PENDING = 3, CL_REGION = 4, CLW = 5;
+// frame words
+constexpr uint32_t FR_ACT = 0, FR_KIND = 1, FR_DOT = 2, FR_TGT = 3, FR_NEXT = 4, FR_NREADY = 5, FR_READY = 6,
+                   FRW = FR_READY + RDMAX;
+
+struct Geo {  // launch-uniform geometry
+  uint32_t n, C, K, W, R, L, NP, ncli_keys;
+  uint32_t off_ring, off_rh, off_snap, off_slot, off_kd, off_proc, off_cli, off_frame, off_wl, off_delay,
+      words;
+};
+
+struct SimArgs {
+  const fx_sim_spec* specs;
+  uint32_t instances;
+  Geo g;
+  const uint16_t* ping;  // [RP][RP]
+  const uint8_t* rank;   // [RP][RP]
+  uint32_t RP;           // planet row stride
+  uint32_t exec_cap, lat_cap, max_events, sim_exec_notif;
+  uint32_t* executed;
+  uint32_t* executed_len;
+  uint32_t* latency_log;
+  unsigned long long* lat_hist;
+  uint32_t lat_bins;
+  unsigned long long* chain_hist;
+  uint32_t chain_bins;
+  unsigned long long* delay_hist;
+  uint32_t delay_bins;
+  unsigned long long* stats;
+  uint32_t* err;
+};
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)src);
+}
+__device__ __forceinline__ uint32_t gather(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+__device__ __forceinline__ uint64_t bal(bool p) { return (uint64_t)__ballot(p); }
+__device__ __forceinline__ uint32_t ctz64(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
+__device__ __forceinline__ uint32_t pop64(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
+__device__ __forceinline__ uint32_t pop32(uint32_t m) { return (uint32_t)__builtin_popcount(m); }
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finalizer (C6)
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ uint64_t sim_rand(uint64_t seed, uint64_t inst, uint64_t client, uint64_t idx,
+                                             uint64_t purpose) {
+  return mix64(mix64(mix64(mix64(seed ^ 0x5851F42D4C957F2Dull) + inst) + client) + ((idx << 8) | purpose));
+}
+
+// register arrays indexed by a wave-uniform value: arithmetic selects keep
+// them in VGPRs (a dynamically indexed private array goes to scratch)
+template <uint32_t N>
+__device__ __forceinline__ uint32_t rsel(const uint32_t (&a)[N], uint32_t i) {
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < N; ++k) r = (i == k) ? a[k] : r;
+  return r;
+}
+template <uint32_t N>
+__device__ __forceinline__ void rput(uint32_t (&a)[N], uint32_t i, uint32_t v) {
+#pragma unroll
+  for (uint32_t k = 0; k < N; ++k) a[k] = (i == k) ? v : a[k];
+}
+
+// Tarjan word: id (7 bits) | low (7 bits) | visited epoch (16 bits)
+__device__ __forceinline__ uint32_t tid(uint32_t t) { return t & 127u; }
+__device__ __forceinline__ uint32_t tlow(uint32_t t) { return (t >> 7) & 127u; }
+__device__ __forceinline__ uint32_t tep(uint32_t t) { return t >> 14; }
+__device__ __forceinline__ uint32_t tmk(uint32_t id, uint32_t low, uint32_t ep) { return id | (low << 7) | (ep << 14); }
+constexpr uint32_t EPOCH_MAX = 0xFFFFu;
+
+struct Sim {
+  // ---------------------------------------------------------------- context
+  uint32_t lid;
+  uint64_t lbit;
+  SimArgs A;
+  Geo g;
+  uint32_t* lds;
+  uint32_t inst;
+  uint64_t seed, rng_inst;
+  uint32_t protocol, n, f, synod_f, fq, wq, gc_ms, en_ms, cmds, conflict, pool, extra;
+  bool has_extra;
+  uint32_t C;
+  uint32_t err = 0;
+  uint32_t now = 0;       // ms
+  uint32_t seq = 0;       // insertion counter (C3)
+  uint64_t events = 0, trace = 0;
+  uint32_t clients_done = 0;
+  bool done = false, in_extra = false;
+  uint32_t final_ms = 0;
+
+  // link heads owned by this lane: time, seq (time NONE = empty)
+  uint32_t ht[HMAX], hs[HMAX];
+
+  // executor state of every process (lane-owned slot l / clock of source l + 1)
+  uint32_t xdot[NMAX], xrec[NMAX], xwait[NMAX], xtl[NMAX], xfr[NMAX], xcf[NMAX], xcw[NMAX];
+  // executor working copy (the process being run)
+  uint32_t sdot, srec, swait, stl, sfr, cf, cw;
+  uint64_t occ, wmask, tmask;
+  uint32_t xk, epoch, nwl, phase, root, idc, nfr, missing, fv, fdi, fnc, in_try, emitted, xp;
+
+  // ------------------------------------------------------------ LDS views
+  __device__ __forceinline__ uint32_t& W(uint32_t i) { return lds[i]; }
+  __device__ __forceinline__ uint32_t& ring(uint32_t link, uint32_t e, uint32_t w) {
+    return lds[g.off_ring + (link * g.R + e) * 3 + w];
+  }
+  __device__ __forceinline__ uint32_t& rh(uint32_t link) { return lds[g.off_rh + link]; }  // head | tail << 16
+  __device__ __forceinline__ uint32_t& snap(uint32_t p, uint32_t k, uint32_t s) {
+    return lds[g.off_snap + (p * RS + (k & (RS - 1))) * g.n + s];
+  }
+  __device__ __forceinline__ uint32_t slot_of(uint32_t d) const {
+    return ((d >> FX_SEQ_BITS) - 1u) * g.W + (d & (g.W - 1u));
+  }
+  __device__ __forceinline__ uint32_t& S(uint32_t sl, uint32_t w) { return lds[g.off_slot + sl * SLOTW + w]; }
+  __device__ __forceinline__ uint32_t& kd(uint32_t p, uint32_t key) { return lds[g.off_kd + p * g.ncli_keys + key]; }
+  __device__ __forceinline__ uint32_t& P(uint32_t p, uint32_t w) { return lds[g.off_proc + p * PRW + w]; }
+  __device__ __forceinline__ uint32_t& CL(uint32_t c, uint32_t w) { return lds[g.off_cli + c * CLW + w]; }
+  __device__ __forceinline__ uint32_t& FR(uint32_t fi, uint32_t w) { return lds[g.off_frame + fi * FRW + w]; }
+  __device__ __forceinline__ uint32_t& wl(uint32_t i) { return lds[g.off_wl + i]; }
+  // link delays: [0, n*n) process->process, then client->process [C], process->client [C]
+  __device__ __forceinline__ uint32_t& dly(uint32_t i) { return lds[g.off_delay + i]; }
+
+  __device__ __forceinline__ uint32_t pst(uint32_t sl, uint32_t p) {
+    return (uni(S(sl, SL_PST + (p >> 2))) >> ((p & 3u) * 8u)) & 0xFFu;
+  }
+  __device__ __forceinline__ void set_pst(uint32_t sl, uint32_t p, uint32_t v) {
+    const uint32_t w = uni(S(sl, SL_PST + (p >> 2)));
+    const uint32_t sh = (p & 3u) * 8u;
+    const uint32_t nw = (w & ~(0xFFu << sh)) | ((v & 0xFFu) << sh);
+    if (lid == 0) S(sl, SL_PST + (p >> 2)) = nw;
+  }
+  // store a uniform value from lane 0 (every lane computed the same)
+  __device__ __forceinline__ void put(uint32_t& dst, uint32_t v) {
+    if (lid == 0) dst = v;
+  }
+
+  // ------------------------------------------------------------- links
+  __device__ __forceinline__ uint32_t link_p(uint32_t p, uint32_t q) const {  // 0-based p != q
+    return p * (g.n - 1) + (q < p ? q : q - 1);
+  }
+  __device__ __forceinline__ uint32_t link_g(uint32_t p) const { return g.NP + p; }
+  __device__ __forceinline__ uint32_t link_e(uint32_t p) const { return g.NP + g.n + p; }
+  __device__ __forceinline__ uint32_t link_s(uint32_t c) const { return g.NP + 2 * g.n + c; }
+  __device__ __forceinline__ uint32_t link_r(uint32_t c) const { return g.NP + 2 * g.n + g.C + c; }
+
+  __device__ __forceinline__ void head_set(uint32_t link, uint32_t t, uint32_t s) {
+    const uint32_t ln = link & 63u, h = link >> 6;
+    if (lid == ln) {
+#pragma unroll
+      for (uint32_t k = 0; k < HMAX; ++k)
+        if (h == k) {
+          ht[k] = t;
+          hs[k] = s;
+        }
+    }
+  }
+
+  // Schedule::schedule on a link (schedule.rs:38-49): insertion seq = C3 tie-break
+  __device__ __forceinline__ void schedule_timer(uint32_t link, uint32_t delay) {
+    head_set(link, now + delay, seq);
+    ++seq;
+  }
+  __device__ __forceinline__ void send_p(uint32_t from, uint32_t to, uint32_t kind, uint32_t w2) {  // 0-based processes
+    const uint32_t link = link_p(from, to);
+    const uint32_t t = now + uni(dly(from * g.n + to));
+    const uint32_t ht_ = uni(rh(link));
+    const uint32_t head = ht_ & 0xFFFFu, tail = ht_ >> 16;
+    if (((tail - head) & 0xFFFFu) >= g.R) {
+      err = FX_ERR_SIM_CAPACITY;
+      return;
+    }
+    const uint32_t e = tail & (g.R - 1u);
+    if (t >= (1u << 28)) {
+      err = FX_ERR_TIME_RANGE;
+      return;
+    }
+    put(ring(link, e, 0), t | (kind << 28));
+    put(ring(link, e, 1), seq);
+    put(ring(link, e, 2), w2);
+    put(rh(link), head | (((tail + 1u) & 0xFFFFu) << 16));
+    if (head == tail) head_set(link, t, seq);
+    ++seq;
+  }
+
+  // -------------------------------------------------------------- trace
+  __device__ __forceinline__ void note(uint64_t kind, uint64_t a, uint64_t b, uint64_t c) {
+    ++events;
+    trace = mix64(trace ^ ((uint64_t)now << 24) ^ (kind << 20) ^ (a << 12) ^ (b << 4)) + c;
+  }
+
+  // ------------------------------------------------------------ workload
+  // Workload::gen_cmd (workload.rs:142-197) keys of command idx of client c
+  // (1-based id), canonical C6/C7/C11: packed key0 | key1 << 16, count
+  __device__ __forceinline__ uint32_t gen_keys(uint32_t cid, uint32_t idx, uint32_t& nk) {
+    uint32_t k0 = 0xFFFFu, k1 = 0xFFFFu;
+    nk = 0;
+    for (uint32_t draw = 0; nk < g.K && draw < 64; ++draw) {
+      bool conflict;
+      if (conflict_ == 0) conflict = false;
+      else if (conflict_ >= 100) conflict = true;
+      else conflict = sim_rand(seed, rng_inst, cid, (uint64_t)idx * 64 + draw, 1) % 100ull < conflict_;
+      uint32_t key;
+      if (conflict) key = pool <= 1 ? 0u : (uint32_t)(sim_rand(seed, rng_inst, cid, (uint64_t)idx * 64 + draw, 2) % pool);
+      else key = pool + cid;
+      if (nk == 0) { k0 = key; nk = 1; }
+      else if (key != k0) { k1 = key; nk = 2; }
+    }
+    if (nk != g.K) err = FX_ERR_SIM_CAPACITY;
+    if (nk == 2 && k1 < k0) { const uint32_t t = k0; k0 = k1; k1 = t; }  // C11
+    return k0 | (k1 << 16);
+  }
+  uint32_t conflict_;
+
+  // ------------------------------------------------------- frame stack
+  uint32_t nfrm = 0;  // frames in use
+  uint32_t cur_p = 0; // process of the current frame chain (0-based)
+  uint32_t xinfo = 0; // execution info pushed by the current handler (dot, 0 = none)
+
+  __device__ __forceinline__ void act_send(uint32_t kind, uint32_t dot, uint32_t tgt) {
+    const uint32_t fi = nfrm - 1;
+    put(FR(fi, FR_ACT), 1);
+    put(FR(fi, FR_KIND), kind);
+    put(FR(fi, FR_DOT), dot);
+    put(FR(fi, FR_TGT), tgt);
+  }
+  __device__ __forceinline__ void act_forward(uint32_t kind, uint32_t dot) {
+    const uint32_t fi = nfrm - 1;
+    put(FR(fi, FR_ACT), 2);
+    put(FR(fi, FR_KIND), kind);
+    put(FR(fi, FR_DOT), dot);
+  }
+
+  // ============================================================ protocol
+  // key_deps.add_cmd (sequential.rs:74-118): latest write per key (no reads,
+  // no noops in these workloads); `past` merged; returns sorted unique deps in
+  // lanes [0, cnt) of `out` (a per-lane value)
+  __device__ __forceinline__ uint32_t add_cmd(uint32_t p, uint32_t dot, uint32_t keys, uint32_t nk, uint32_t pastv, uint32_t npast,
+                              uint32_t& outv) {
+    const uint32_t key0 = keys & 0xFFFFu, key1 = keys >> 16;
+    const uint32_t d0 = uni(kd(p, key0));
+    put(kd(p, key0), dot);
+    uint32_t d1 = 0;
+    if (nk > 1) {
+      d1 = uni(kd(p, key1));
+      put(kd(p, key1), dot);
+    }
+    // candidates: lanes [0, npast) the past deps, lane npast / npast + 1 the
+    // latest writes of the keys; the result is their sorted distinct set
+    const uint32_t v = lid < npast ? pastv : (lid == npast ? d0 : (lid == npast + 1 ? d1 : 0u));
+    const bool valid = v != 0;
+    bool first = valid;
+    const uint64_t vm = bal(valid);
+    for (uint64_t m = vm; m; m &= m - 1) {
+      const uint32_t j = ctz64(m);
+      if (j < lid && rl(v, j) == v) first = false;
+    }
+    const uint64_t fm = bal(first);
+    uint32_t rank = 0;
+    for (uint64_t m = fm; m; m &= m - 1) rank += rl(v, ctz64(m)) < v ? 1u : 0u;
+    outv = 0;
+    for (uint64_t m = fm; m; m &= m - 1) {
+      const uint32_t j = ctz64(m);
+      const uint32_t vj = rl(v, j), rj = rl(rank, j);
+      if (lid == rj) outv = vj;
+    }
+    return pop64(fm);
+  }
+
+  // Protocol::submit (atlas.rs:210-249, epaxos.rs:199-221)
+  __device__ __forceinline__ void h_submit(uint32_t p, uint32_t c) {
+    const uint32_t s = uni(P(p, PR_SEQ)) + 1u;
+    put(P(p, PR_SEQ), s);
+    if (s > FX_SEQ_MASK) { err = FX_ERR_DOT_RANGE; return; }
+    const uint32_t dot = FX_PACK_DOT(p + 1, s);
+    const uint32_t sl = slot_of(dot);
+    if (uni(S(sl, SL_DOT)) != 0) { err = FX_ERR_SIM_CAPACITY; return; }
+    const uint32_t idx = uni(CL(c, CL_ISSUED)) - 1u;
+    uint32_t nk = 0;
+    const uint32_t keys = gen_keys(c + 1, idx, nk);
+    // fresh slot
+    if (lid < SLOTW) S(sl, lid) = 0;
+    put(S(sl, SL_DOT), dot);
+    put(S(sl, SL_CLIENT), c);
+    put(S(sl, SL_IDX), idx);
+    put(S(sl, SL_KEYS), keys);
+    uint32_t depv = 0;
+    const uint32_t nd = add_cmd(p, dot, keys, nk, 0, 0, depv);
+    if (lid < nd) S(sl, SL_COLLECT + lid) = depv;
+    put(S(sl, SL_CNT), (nd << 8) | (nk << 20));
+    act_send(M_COLLECT, dot, (1u << n) - 1u);
+  }
+
+  // atlas.rs:251-325 / epaxos.rs:223-301
+  __device__ __forceinline__ void h_mcollect(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (uni(S(sl, SL_DOT)) != dot) { err = FX_ERR_SIM_LATE; return; }
+    const uint32_t ps = pst(sl, p);
+    if ((ps & 3u) != ST_START) return;
+    const uint32_t src = (dot >> FX_SEQ_BITS) - 1u;
+    const uint32_t quorum = uni(P(src, PR_FQ));
+    if (!((quorum >> p) & 1u)) {
+      set_pst(sl, p, (ps & ~3u) | ST_PAYLOAD);
+      if (ps & 4u) {  // buffered commit (atlas.rs:288-292)
+        set_pst(sl, p, ((ps & ~3u) | ST_PAYLOAD) & ~4u);
+        h_mcommit(p, ps >> 4, dot);
+      }
+      return;
+    }
+    const bool from_self = from == p;
+    const uint32_t cnt = uni(S(sl, SL_CNT));
+    const uint32_t ncol = (cnt >> 8) & 0xFFu, nk = (cnt >> 20) & 3u;
+    uint32_t depv = 0, nd = 0;
+    const uint32_t colv = lid < ncol ? S(sl, SL_COLLECT + lid) : 0u;
+    if (from_self) {
+      depv = colv;
+      nd = ncol;
+    } else {
+      nd = add_cmd(p, dot, uni(S(sl, SL_KEYS)), nk, colv, ncol, depv);
+    }
+    if (nd > AMAX) { err = FX_ERR_SIM_CAPACITY; return; }
+    set_pst(sl, p, (ps & ~3u) | ST_COLLECT);
+    // the ack's deps travel in the slot: ack deps of p
+    if (lid < AMAX) S(sl, SL_ACK + p * AMAX + lid) = lid < nd ? depv : 0u;
+    if (protocol == FX_PROTOCOL_EPAXOS && from_self) return;  // epaxos.rs:290-300
+    act_send(M_COLLECT_ACK, dot, 1u << from);
+  }
+
+  // atlas.rs:327-402 / epaxos.rs:303-368
+  __device__ __forceinline__ void h_mcollectack(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (uni(S(sl, SL_DOT)) != dot) { err = FX_ERR_SIM_LATE; return; }
+    if ((pst(sl, p) & 3u) != ST_COLLECT) return;
+    const uint32_t masks = uni(S(sl, SL_MASKS));
+    const uint32_t part = (masks & 0xFFu) | (1u << from);
+    put(S(sl, SL_MASKS), (masks & ~0xFFu) | part);
+    const uint32_t fq_eff = protocol == FX_PROTOCOL_EPAXOS ? fq - 1u : fq;
+    if (pop32(part) != fq_eff) return;
+    // QuorumDeps: union + per-dep report counts over the participants' acks.
+    // lane j of a participant block holds one reported dep: lanes
+    // [q*AMAX, q*AMAX + AMAX) for process q (<= 32 lanes)
+    const uint32_t q = lid / AMAX, j = lid % AMAX;
+    uint32_t v = 0;
+    if (lid < NMAX * AMAX && q < n && ((part >> q) & 1u)) v = S(sl, SL_ACK + q * AMAX + j);
+    const bool valid = v != 0;
+    // count and first occurrence
+    uint32_t cnt = 0;
+    bool first = valid;
+    const uint64_t vm = bal(valid);
+    for (uint64_t m = vm; m; m &= m - 1) {
+      const uint32_t l2 = ctz64(m);
+      const uint32_t v2 = rl(v, l2);
+      if (valid && v2 == v) {
+        ++cnt;
+        if (l2 < lid) first = false;
+      }
+    }
+    const uint64_t um = bal(first);  // one lane per distinct dep
+    const uint32_t nu = pop64(um);
+    if (nu > VMAX) { err = FX_ERR_SIM_CAPACITY; return; }
+    bool fast;
+    if (protocol == FX_PROTOCOL_ATLAS) {
+      // threshold = |quorum| - minority (atlas.rs:361-368)
+      const uint32_t threshold = fq - (n / 2u);
+      fast = !bal(first && cnt < threshold);
+    } else {
+      // check_equal (quorum.rs:72-103): every dep reported by every participant
+      fast = nu == 0 || !bal(first && cnt != fq_eff);
+    }
+    // value = union, ascending
+    uint32_t rank = 0;
+    for (uint64_t m = um; m; m &= m - 1) rank += rl(v, ctz64(m)) < v ? 1u : 0u;
+    if (first) S(sl, SL_VALUE + rank) = v;
+    const uint32_t c0 = uni(S(sl, SL_CNT));
+    put(S(sl, SL_CNT), (c0 & ~0xFFu) | nu | (fast ? 0u : (1u << 16)));  // slow: proposer ballot set
+    if (fast) put(P(p, PR_FAST), uni(P(p, PR_FAST)) + 1u);
+    else put(P(p, PR_SLOW), uni(P(p, PR_SLOW)) + 1u);
+    if (fast) {
+      act_send(M_COMMIT, dot, (1u << n) - 1u);
+    } else {
+      // synod.skip_prepare (single.rs:208-213): ballot = coordinator id
+      act_send(M_CONSENSUS, dot, uni(P(p, PR_WQ)));
+    }
+  }
+
+  // atlas.rs:404-475 / epaxos.rs:370-428
+  __device__ __forceinline__ void h_mcommit(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (uni(S(sl, SL_DOT)) != dot) { err = FX_ERR_SIM_LATE; return; }
+    const uint32_t ps = pst(sl, p);
+    if ((ps & 3u) == ST_START) {  // buffered_commits.insert
+      set_pst(sl, p, (ps & 0x0Bu) | 4u | (from << 4));
+      return;
+    }
+    if ((ps & 3u) == ST_COMMIT) return;
+    xinfo = dot;  // to_executors.push(GraphExecutionInfo::add(dot, cmd, value.deps))
+    set_pst(sl, p, (ps & ~3u) | ST_COMMIT);
+    const uint32_t masks = uni(S(sl, SL_MASKS));
+    put(S(sl, SL_MASKS), masks + (1u << 16));  // committed count
+    if (gc_ms) act_forward(M_COMMIT_DOT, dot);
+  }
+
+  // atlas.rs:477-524 / epaxos.rs:430-477
+  __device__ __forceinline__ void h_mconsensus(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (uni(S(sl, SL_DOT)) != dot) { err = FX_ERR_SIM_LATE; return; }
+    const uint32_t ps = pst(sl, p);
+    if ((ps & 3u) == ST_COMMIT) {  // chosen: reply with the chosen value
+      act_send(M_COMMIT, dot, 1u << from);
+      return;
+    }
+    set_pst(sl, p, ps | 8u);  // acceptor accepts (b >= ballot)
+    act_send(M_CONSENSUS_ACK, dot, 1u << from);
+  }
+
+  // atlas.rs:526-558 / epaxos.rs:479-517
+  __device__ __forceinline__ void h_mconsensusack(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (uni(S(sl, SL_DOT)) != dot) { err = FX_ERR_SIM_LATE; return; }
+    if (!((uni(S(sl, SL_CNT)) >> 16) & 1u)) return;  // proposer ballot != b
+    const uint32_t masks = uni(S(sl, SL_MASKS));
+    const uint32_t acc = ((masks >> 8) & 0xFFu) | (1u << from);
+    if (pop32(acc) == synod_f + 1u) {
+      put(S(sl, SL_MASKS), masks & ~0xFF00u);  // reset_state
+      if (!(pst(sl, p) & 8u)) { err = FX_ERR_SIM_LATE; return; }  // single.rs:346-349 panic
+      act_send(M_COMMIT, dot, (1u << n) - 1u);
+    } else {
+      put(S(sl, SL_MASKS), (masks & ~0xFF00u) | (acc << 8));
+    }
+  }
+
+  // MCommitDot: VClockGCTrack::add_to_clock (gc/clock.rs:43-48), AEClock with
+  // a 32-bit exception window per source
+  __device__ __forceinline__ void h_mcommitdot(uint32_t p, uint32_t dot) {
+    const uint32_t si = (dot >> FX_SEQ_BITS) - 1u, sq = dot & FX_SEQ_MASK;
+    uint32_t fr = uni(P(p, PR_GCF + si)), w = uni(P(p, PR_GCW + si));
+    if (sq <= fr) return;
+    const uint32_t off = sq - fr - 1u;
+    if (off >= 32u) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (off) {
+      w |= 1u << off;
+    } else {
+      const uint32_t win = w >> 1;
+      const uint32_t ones = __builtin_ctz(~win);
+      fr = fr + 1 + ones;
+      w = win >> ones;
+    }
+    put(P(p, PR_GCF + si), fr);
+    put(P(p, PR_GCW + si), w);
+  }
+
+  // MGarbageCollection (atlas.rs:657-679) + the MStable it forwards
+  // (atlas.rs:681-697): stable() over MaxSet clocks (gc/clock.rs:74-137)
+  __device__ __forceinline__ void h_mgc(uint32_t p, uint32_t from, uint32_t k) {
+    // update_clock_of(from, snapshot k of from); the snapshot must still be
+    // in from's ring of RS ticks
+    if (uni(P(from, PR_TICK)) - k > RS) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (lid < n) {
+      const uint32_t sv = snap(from, k, lid);
+      uint32_t& o = P(p, PR_OTH + from * NMAX + lid);
+      o = max(o, sv);
+    }
+    const uint32_t seen = uni(P(p, PR_SEEN)) | (1u << from);
+    put(P(p, PR_SEEN), seen);
+    uint32_t count = 0;
+    if (lid < n) {
+      uint32_t cur = 0;
+      if (pop32(seen) == n - 1u) {
+        cur = P(p, PR_GCF + lid);
+        for (uint32_t q = 0; q < n; ++q)
+          if ((seen >> q) & 1u) cur = min(cur, P(p, PR_OTH + q * NMAX + lid));
+      }
+      const uint32_t prev = P(p, PR_PREV + lid);
+      if (cur > prev) count = cur - prev;  // dots prev+1 ..= cur become stable
+      P(p, PR_PREV + lid) = max(cur, prev);
+    }
+    for (uint32_t o = 1; o < 8; o <<= 1) count += (uint32_t)__shfl_xor((int)count, (int)o, 64);
+    count = uni(count);
+    if (count) put(P(p, PR_STABLE), uni(P(p, PR_STABLE)) + count);
+  }
+
+  // periodic GarbageCollection (atlas.rs:699-714): frontier to all but me
+  __device__ __forceinline__ void h_gc_event(uint32_t p) {
+    const uint32_t k = uni(P(p, PR_TICK));
+    if (lid < n) snap(p, k, lid) = P(p, PR_GCF + lid);
+    put(P(p, PR_TICK), k + 1u);
+    act_send(M_GC, k, ((1u << n) - 1u) & ~(1u << p));
+  }
+
+  __device__ __forceinline__ void dispatch(uint32_t p, uint32_t from, uint32_t kind, uint32_t w2) {
+    switch (kind) {
+      case M_COLLECT: h_mcollect(p, from, w2); break;
+      case M_COLLECT_ACK: h_mcollectack(p, from, w2); break;
+      case M_COMMIT: h_mcommit(p, from, w2); break;
+      case M_CONSENSUS: h_mconsensus(p, from, w2); break;
+      case M_CONSENSUS_ACK: h_mconsensusack(p, from, w2); break;
+      case M_COMMIT_DOT: h_mcommitdot(p, w2); break;
+      case M_GC: h_mgc(p, from, w2); break;
+      default: err = FX_ERR_INVALID_ARG;
+    }
+  }
+
+  // ===================================================== GraphExecutor
+  __device__ __forceinline__ bool mine(uint64_t m) const { return (m & lbit) != 0; }
+  __device__ __forceinline__ uint32_t vcount_of(uint32_t d) { return uni(S(slot_of(d), SL_CNT)) & 0xFFu; }
+  __device__ __forceinline__ uint32_t value_at(uint32_t d, uint32_t j) { return uni(S(slot_of(d), SL_VALUE + j)); }
+
+  __device__ __forceinline__ void x_load(uint32_t p) {
+    xp = p;
+    sdot = rsel(xdot, p); srec = rsel(xrec, p); swait = rsel(xwait, p); stl = rsel(xtl, p);
+    sfr = rsel(xfr, p); cf = rsel(xcf, p); cw = rsel(xcw, p);
+    occ = (uint64_t)uni(P(p, PR_OCC)) | ((uint64_t)uni(P(p, PR_OCC + 1)) << 32);
+    wmask = (uint64_t)uni(P(p, PR_WMASK)) | ((uint64_t)uni(P(p, PR_WMASK + 1)) << 32);
+    epoch = uni(P(p, PR_EPOCH));
+    xk = uni(P(p, PR_EXEC));
+    tmask = 0;
+    phase = PH_IDLE;
+  }
+  __device__ __forceinline__ void x_store() {
+    const uint32_t p = xp;
+    rput(xdot, p, sdot); rput(xrec, p, srec); rput(xwait, p, swait); rput(xtl, p, stl);
+    rput(xfr, p, sfr); rput(xcf, p, cf); rput(xcw, p, cw);
+    put(P(p, PR_OCC), (uint32_t)occ);
+    put(P(p, PR_OCC + 1), (uint32_t)(occ >> 32));
+    put(P(p, PR_WMASK), (uint32_t)wmask);
+    put(P(p, PR_WMASK + 1), (uint32_t)(wmask >> 32));
+    put(P(p, PR_EPOCH), epoch);
+    put(P(p, PR_EXEC), xk);
+  }
+
+  // AEClock::contains for a per-lane dot / a uniform dot (tarjan.rs:131-132)
+  __device__ __forceinline__ bool contains_v(uint32_t d) const {
+    const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
+    const uint32_t fr = gather(cf, si & 63u), w = gather(cw, si & 63u);
+    const uint32_t sq = d & FX_SEQ_MASK, off = sq - fr - 1u;
+    return si < n && (sq <= fr || (off < 32u && ((w >> (off & 31u)) & 1u)));
+  }
+  __device__ __forceinline__ bool contains_u(uint32_t d) const {
+    const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
+    if (si >= n) return false;
+    const uint32_t fr = rl(cf, si), w = rl(cw, si);
+    const uint32_t sq = d & FX_SEQ_MASK, off = sq - fr - 1u;
+    return sq <= fr || (off < 32u && ((w >> off) & 1u));
+  }
+  // AEClock::add (tarjan.rs:293)
+  __device__ __forceinline__ void clk_add(uint32_t d) {
+    const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
+    if (si >= n) { err = FX_ERR_DOT_RANGE; return; }
+    uint32_t fr = rl(cf, si), w = rl(cw, si);
+    const uint32_t sq = d & FX_SEQ_MASK;
+    if (sq <= fr) return;
+    const uint32_t off = sq - fr - 1u;
+    if (off >= 32u) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (off != 0) {
+      w |= 1u << off;
+    } else {
+      const uint32_t win = w >> 1;
+      const uint32_t ones = __builtin_ctz(~win);
+      fr = fr + 1 + ones;
+      w = win >> ones;
+    }
+    if (lid == si) {
+      cf = fr;
+      cw = w;
+    }
+  }
+  __device__ __forceinline__ int find(uint32_t d) const {
+    const uint64_t m = bal(mine(occ) && sdot == d);
+    return m ? (int)ctz64(m) : -1;
+  }
+  __device__ __forceinline__ void new_epoch() {
+    epoch = epoch + 1;
+    if (epoch > EPOCH_MAX) {
+      if (mine(occ)) stl = tmk(tid(stl), tlow(stl), 0);
+      epoch = 1;
+    }
+  }
+
+  // one executed command: to_execute -> Command::execute -> to_clients ->
+  // AggregatePending (runner.rs:406-424), executor metrics, execution log
+  __device__ __forceinline__ void on_execute(uint32_t d, uint32_t start) {
+    const uint32_t p = xp;
+    if (xk < A.exec_cap && A.executed && lid == 0)
+      A.executed[((size_t)inst * n + p) * A.exec_cap + xk] = d;
+    ++xk;
+    const uint32_t delay = now - start;  // ExecutionDelay (graph/mod.rs:514-518)
+    if (lid == 0 && A.delay_hist) atomicAdd(&A.delay_hist[min(delay, A.delay_bins - 1u)], 1ull);
+    const uint32_t sl = slot_of(d);
+    if (uni(S(sl, SL_DOT)) != d) { err = FX_ERR_SIM_LATE; return; }
+    const uint32_t c = uni(S(sl, SL_CLIENT));
+    const uint32_t nk = (uni(S(sl, SL_CNT)) >> 20) & 3u;
+    if (uni(CL(c, CL_PROC)) == p) {  // pending.wait_for registered this rifl at p
+      const uint32_t pend = uni(CL(c, CL_PENDING));
+      if (pend < nk) { err = FX_ERR_SIM_LATE; return; }
+      put(CL(c, CL_PENDING), pend - nk);  // one ExecutorResult per key
+      if (pend == nk) {
+        const uint32_t fi = nfrm - 1;
+        const uint32_t nr = uni(FR(fi, FR_NREADY));
+        if (nr >= RDMAX) { err = FX_ERR_SIM_CAPACITY; return; }
+        put(FR(fi, FR_READY + nr), c);
+        put(FR(fi, FR_NREADY), nr + 1u);
+      }
+    }
+    const uint32_t masks = uni(S(sl, SL_MASKS));
+    if (((masks >> 24) & 0xFFu) + 1u == n) {
+      put(S(sl, SL_DOT), 0u);  // executed everywhere: free the slot
+    } else {
+      put(S(sl, SL_MASKS), masks + (1u << 24));
+    }
+  }
+
+  __device__ __forceinline__ void emit_one(uint32_t d, uint32_t start) {
+    if (lid == 0 && A.chain_hist) atomicAdd(&A.chain_hist[min(1u, A.chain_bins - 1u)], 1ull);
+    clk_add(d);
+    on_execute(d, start);
+  }
+
+  __device__ __forceinline__ int insert_vertex(uint32_t d) {
+    const uint64_t fre = ~occ;
+    if (!fre) { err = FX_ERR_SIM_CAPACITY; return -1; }
+    const uint32_t sl = ctz64(fre);
+    if (lid == sl) {
+      sdot = d;
+      srec = now;  // Vertex::start_time_ms (tarjan.rs:332-348)
+      swait = 0;
+      stl = 0;
+    }
+    occ |= 1ull << sl;
+    return (int)sl;
+  }
+
+  __device__ __forceinline__ void dfs_start(uint32_t r, bool intry) {
+    root = r;
+    in_try = intry;
+    emitted = 0;
+    missing = 0;
+    idc = 1;
+    const uint32_t tr = rl(stl, r);
+    if (lid == r) stl = tmk(1, 1, tep(tr));
+    nfr = 0;
+    fv = r;
+    fdi = 0;
+    fnc = vcount_of(rl(sdot, r));
+    phase = PH_DFS;
+  }
+
+  // SCC rooted at fv: stack vertices with id >= id(fv), saved in ascending
+  // dot order (SCC = BTreeSet<Dot>, tarjan.rs:15)
+  __device__ __forceinline__ void save_scc() {
+    const uint32_t idv = tid(rl(stl, fv));
+    const bool mem = mine(occ) && tid(stl) >= idv;
+    const uint64_t mm = bal(mem);
+    const uint32_t cnt = pop64(mm);
+    if (nwl + cnt > 65u) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (lid == 0 && A.chain_hist) atomicAdd(&A.chain_hist[min(cnt, A.chain_bins - 1u)], 1ull);
+    uint32_t rank = 0;
+    for (uint64_t m = mm; m; m &= m - 1) rank += rl(sdot, ctz64(m)) < sdot ? 1u : 0u;
+    for (uint32_t r = 0; r < cnt; ++r) {
+      const uint32_t lr = ctz64(bal(mem && rank == r));
+      const uint32_t d = rl(sdot, lr);
+      const uint32_t st = rl(srec, lr);
+      put(wl(nwl + r), d);
+      clk_add(d);
+      on_execute(d, st);
+      if (err) return;
+    }
+    nwl += cnt;
+    occ &= ~mm;
+    wmask &= ~mm;
+    tmask &= ~mm;
+    emitted = 1;
+  }
+
+  __device__ __forceinline__ void dfs_finish() {
+    // finalize (tarjan.rs:60-93); in try_pending a failed search that saved no
+    // SCC marks the stack vertices visited (mod.rs:621-629)
+    const bool mark = in_try && missing != 0 && !emitted;
+    if (mine(occ) && tid(stl) != 0) stl = tmk(0, 0, mark ? epoch : tep(stl));
+    if (missing) {  // index_pending (mod.rs:525-554)
+      if (lid == root) swait = missing;
+      wmask |= 1ull << root;
+    }
+    if (in_try) {
+      if (!missing || emitted) new_epoch();
+      phase = PH_TRY;
+    } else {
+      phase = PH_CHECK;
+    }
+  }
+
+  // one DFS edge or one frame pop (TarjanSCCFinder::strong_connect, iterative)
+  __device__ __forceinline__ void dfs_iter() {
+    if (fdi < fnc) {
+      const uint32_t vd = rl(sdot, fv);
+      const uint32_t dep = value_at(vd, fdi);
+      ++fdi;
+      if (dep == vd || contains_u(dep)) return;  // self or executed (tarjan.rs:128-145)
+      const int x = find(dep);
+      if (x < 0) {  // missing (tarjan.rs:148-157, shard_count == 1)
+        missing = dep;
+        dfs_finish();
+        return;
+      }
+      const uint32_t tx = rl(stl, (uint32_t)x);
+      if (tid(tx) == 0) {  // recurse (tarjan.rs:172-214)
+        ++idc;
+        if (idc > 127u) { err = FX_ERR_SIM_CAPACITY; return; }
+        if (lid == (uint32_t)x) stl = tmk(idc, idc, tep(tx));
+        if (lid == nfr) sfr = fv | (fdi << 8);
+        ++nfr;
+        fv = (uint32_t)x;
+        fdi = 0;
+        fnc = vcount_of(rl(sdot, fv));
+      } else {  // on the stack (tarjan.rs:215-225)
+        const uint32_t tv = rl(stl, fv);
+        if (tid(tx) < tlow(tv) && lid == fv) stl = tmk(tid(tv), tid(tx), tep(tv));
+      }
+    } else {
+      const uint32_t tv = rl(stl, fv);
+      const uint32_t lowv = tlow(tv);
+      if (tid(tv) == lowv) {  // SCC root (tarjan.rs:233-312)
+        save_scc();
+        if (err) return;
+      }
+      if (nfr == 0) {
+        dfs_finish();
+        return;
+      }
+      --nfr;
+      const uint32_t fw = rl(sfr, nfr);
+      fv = fw & 0xFFu;
+      fdi = fw >> 8;
+      fnc = vcount_of(rl(sdot, fv));
+      const uint32_t tp = rl(stl, fv);
+      if (lowv < tlow(tp) && lid == fv) stl = tmk(tid(tp), lowv, tep(tp));
+    }
+  }
+
+  // try_pending (mod.rs:589-642): next waiter, ascending (C2)
+  __device__ __forceinline__ void try_iter() {
+    if (!tmask) { phase = PH_CHECK; return; }
+    uint32_t best = ctz64(tmask), best_dot = rl(sdot, best);
+    for (uint64_t m = tmask & (tmask - 1); m; m &= m - 1) {
+      const uint32_t b = ctz64(m), v = rl(sdot, b);
+      if (v < best_dot) {
+        best_dot = v;
+        best = b;
+      }
+    }
+    tmask &= ~(1ull << best);
+    if (tep(rl(stl, best)) == epoch) return;
+    dfs_start(best, true);
+  }
+
+  // check_pending (mod.rs:556-587): LIFO over released dots
+  __device__ __forceinline__ void check_iter() {
+    if (nwl == 0 || !wmask) {
+      nwl = 0;
+      phase = PH_IDLE;
+      return;
+    }
+    --nwl;
+    const uint32_t x = uni(wl(nwl));
+    const uint64_t t = bal(mine(wmask) && swait == x);
+    if (!t) return;
+    wmask &= ~t;
+    tmask = t;
+    new_epoch();
+    phase = PH_TRY;
+  }
+
+  // GraphExecutor::handle(Add) (executor.rs:69-80) -> handle_add (mod.rs:213-275)
+  __device__ __forceinline__ void x_add(uint32_t p, uint32_t d) {
+    x_load(p);
+    nwl = 0;
+    if (find(d) >= 0) { err = FX_ERR_DOUBLE_INDEX; x_store(); return; }
+    const uint32_t vc = vcount_of(d);
+    const uint32_t depj = lid < vc ? S(slot_of(d), SL_VALUE + lid) : 0u;
+    const bool keep = lid < vc && depj != d && !contains_v(depj);
+    if (!bal(keep)) {  // fast path: a singleton SCC
+      emit_one(d, now);
+      if (wmask && !err) {
+        put(wl(0), d);
+        nwl = 1;
+        phase = PH_CHECK;
+      }
+    } else {
+      const int sl = insert_vertex(d);
+      if (sl >= 0) dfs_start((uint32_t)sl, false);
+    }
+    uint32_t guard = 0;
+    while (phase != PH_IDLE && !err) {
+      if (phase == PH_DFS) dfs_iter();
+      else if (phase == PH_TRY) try_iter();
+      else check_iter();
+      if (++guard > (1u << 22)) err = FX_ERR_SIM_CAPACITY;
+    }
+    x_store();
+  }
+
+  // =========================================== send_to_processes_and_executors
+  // push a frame for process p and run the handler (handle_send_to_proc /
+  // handle_submit_to_proc / handle_periodic_process_event), then the executor
+  __device__ __forceinline__ void frame_push() {
+    if (nfrm >= FMAX) { err = FX_ERR_SIM_CAPACITY; return; }
+    const uint32_t fi = nfrm++;
+    put(FR(fi, FR_ACT), 0);
+    put(FR(fi, FR_NEXT), 0);
+    put(FR(fi, FR_NREADY), 0);
+    xinfo = 0;
+  }
+  __device__ __forceinline__ void frame_after_handler(uint32_t p) {
+    if (xinfo && !err) {  // to_executors (<= 1 per handler), LIFO
+      const uint32_t d = xinfo;
+      xinfo = 0;
+      x_add(p, d);
+    }
+  }
+
+  // runs the frame stack of process p to completion (runner.rs:395-488)
+  __device__ __forceinline__ void frames_run(uint32_t p) {
+    uint32_t guard = 0;
+    while (nfrm > 0 && !err) {
+      if (++guard > 4096u) { err = FX_ERR_SIM_CAPACITY; return; }
+      const uint32_t fi = nfrm - 1;
+      const uint32_t act = uni(FR(fi, FR_ACT));
+      if (act == 2) {  // ToForward: deliver to self now
+        put(FR(fi, FR_ACT), 0);
+        const uint32_t kind = uni(FR(fi, FR_KIND)), dot = uni(FR(fi, FR_DOT));
+        frame_push();
+        if (err) return;
+        dispatch(p, p, kind, dot);
+        frame_after_handler(p);
+        continue;
+      }
+      if (act == 1) {  // ToSend: targets ascending (C4), self recurses in place
+        const uint32_t tgt = uni(FR(fi, FR_TGT));
+        const uint32_t kind = uni(FR(fi, FR_KIND)), dot = uni(FR(fi, FR_DOT));
+        uint32_t nx = uni(FR(fi, FR_NEXT));
+        bool recursed = false;
+        while (nx < n) {
+          const uint32_t to = nx++;
+          if (!((tgt >> to) & 1u)) continue;
+          if (to == p) {
+            put(FR(fi, FR_NEXT), nx);
+            frame_push();
+            if (err) return;
+            dispatch(p, p, kind, dot);
+            frame_after_handler(p);
+            recursed = true;
+            break;
+          }
+          send_p(p, to, kind, dot);
+          if (err) return;
+        }
+        if (recursed) continue;
+        put(FR(fi, FR_ACT), 0);
+      }
+      // ready results -> schedule_to_client (runner.rs:434-440)
+      const uint32_t nr = uni(FR(fi, FR_NREADY));
+      for (uint32_t r = 0; r < nr; ++r) {
+        const uint32_t c = uni(FR(fi, FR_READY + r));
+        schedule_timer(link_r(c), uni(dly(g.n * g.n + g.C + c)));
+      }
+      --nfrm;
+    }
+  }
+
+  // ======================================================= event loop
+  // Client::cmd_send: next command of client c (0-based) -> SubmitToProc
+  __device__ __forceinline__ bool client_send(uint32_t c) {
+    const uint32_t issued = uni(CL(c, CL_ISSUED));
+    if (issued >= cmds) return false;
+    put(CL(c, CL_ISSUED), issued + 1u);
+    put(CL(c, CL_START), now);  // Pending::start
+    schedule_timer(link_s(c), uni(dly(g.n * g.n + c)));
+    return true;
+  }
+
+  __device__ __forceinline__ void run_event(uint32_t link) {
+    if (link < g.NP) {  // P(p, q): SendToProc
+      const uint32_t p = link / (g.n - 1u), qi = link % (g.n - 1u);
+      const uint32_t q = qi < p ? qi : qi + 1u;
+      const uint32_t ht_ = uni(rh(link));
+      const uint32_t head = ht_ & 0xFFFFu, tail = ht_ >> 16;
+      const uint32_t e = head & (g.R - 1u);
+      const uint32_t w0 = uni(ring(link, e, 0)), w2 = uni(ring(link, e, 2));
+      const uint32_t kind = w0 >> 28;
+      const uint32_t nh = (head + 1u) & 0xFFFFu;
+      put(rh(link), nh | (tail << 16));
+      if (nh != tail) {
+        const uint32_t e2 = nh & (g.R - 1u);
+        head_set(link, uni(ring(link, e2, 0)) & 0x0FFFFFFFu, uni(ring(link, e2, 1)));
+      } else {
+        head_set(link, NONE, NONE);
+      }
+      note(3, q + 1, p + 1, ((uint64_t)kind << 32) | (kind == M_GC ? 0u : w2));
+      frame_push();
+      dispatch(q, p, kind, w2);
+      frame_after_handler(q);
+      frames_run(q);
+      return;
+    }
+    uint32_t x = link - g.NP;
+    if (x < g.n) {  // G(p): periodic GarbageCollection
+      const uint32_t p = x;
+      head_set(link, NONE, NONE);
+      note(0, p + 1, 0, 0);
+      frame_push();
+      h_gc_event(p);
+      frame_after_handler(p);
+      frames_run(p);
+      schedule_timer(link_g(p), gc_ms);  // next periodic event (runner.rs:328-329)
+      return;
+    }
+    x -= g.n;
+    if (x < g.n) {  // E(p): executed notification (a no-op for the GraphExecutor)
+      schedule_timer(link_e(x), en_ms);
+      return;
+    }
+    x -= g.n;
+    if (x < g.C) {  // S(c): SubmitToProc
+      const uint32_t c = x;
+      head_set(link, NONE, NONE);
+      const uint32_t p = uni(CL(c, CL_PROC));
+      note(2, p + 1, c + 1, uni(CL(c, CL_ISSUED)));
+      put(CL(c, CL_PENDING), g.K);  // AggregatePending::wait_for: key_count results
+      frame_push();
+      h_submit(p, c);
+      frame_after_handler(p);
+      frames_run(p);
+      return;
+    }
+    x -= g.C;
+    {  // R(c): SendToClient -> Client::cmd_recv + cmd_send (simulation.rs:132-149)
+      const uint32_t c = x;
+      head_set(link, NONE, NONE);
+      const uint32_t issued = uni(CL(c, CL_ISSUED));
+      note(4, c + 1, 0, issued);
+      const uint32_t lat = now - uni(CL(c, CL_START));  // latency.as_millis()
+      if (lid == 0) {
+        if (A.latency_log && issued - 1u < A.lat_cap)
+          A.latency_log[((size_t)inst * g.C + c) * A.lat_cap + issued - 1u] = lat;
+        if (A.lat_hist) {
+          const uint32_t region = CL(c, CL_REGION);
+          atomicAdd(&A.lat_hist[(size_t)region * A.lat_bins + min(lat, A.lat_bins - 1u)], 1ull);
+        }
+      }
+      if (!client_send(c)) {
+        ++clients_done;
+        if (clients_done == g.C) {
+          if (has_extra) {
+            final_ms = now + extra;
+            in_extra = true;
+          } else {
+            done = true;
+          }
+        }
+      }
+    }
+  }
+
+  // wave-wide min over the link heads: (time, seq) lexicographic
+  __device__ __forceinline__ uint32_t pop_min(uint32_t& t_out) {
+    uint64_t best = ~0ull;
+    uint32_t bl = NONE;
+#pragma unroll
+    for (uint32_t k = 0; k < HMAX; ++k) {
+      const uint64_t key = ((uint64_t)ht[k] << 32) | hs[k];
+      if (key < best) {
+        best = key;
+        bl = k * 64u + lid;
+      }
+    }
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t bh = (uint32_t)__shfl_xor((int)(uint32_t)(best >> 32), (int)o, 64);
+      const uint32_t blo = (uint32_t)__shfl_xor((int)(uint32_t)best, (int)o, 64);
+      const uint32_t ol = (uint32_t)__shfl_xor((int)bl, (int)o, 64);
+      const uint64_t ob = ((uint64_t)bh << 32) | blo;
+      if (ob < best || (ob == best && ol < bl)) {
+        best = ob;
+        bl = ol;
+      }
+    }
+    t_out = uni((uint32_t)(best >> 32));
+    return uni(bl);
+  }
+};
+
+__global__ __launch_bounds__(64) void k_sim(SimArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  const uint32_t inst = blockIdx.x;
+  if (inst >= a.instances) return;
+  Sim s;
+  s.lid = threadIdx.x;
+  s.lbit = 1ull << s.lid;
+  s.A = a;
+  s.g = a.g;
+  s.lds = smem;
+  s.inst = inst;
+  const fx_sim_spec& sp = a.specs[inst];
+  s.seed = sp.seed;
+  s.rng_inst = sp.instance;
+  s.protocol = sp.protocol;
+  s.n = a.g.n;
+  s.f = sp.f;
+  s.C = a.g.C;
+  s.gc_ms = sp.gc_interval_ms;
+  s.en_ms = sp.executed_notification_ms;
+  s.cmds = sp.commands_per_client;
+  s.conflict_ = sp.conflict_rate;
+  s.pool = sp.pool_size;
+  s.has_extra = sp.extra_sim_time_ms >= 0;
+  s.extra = s.has_extra ? (uint32_t)sp.extra_sim_time_ms : 0u;
+  const uint32_t n = s.n;
+  if (s.protocol == FX_PROTOCOL_ATLAS) {
+    s.fq = n / 2 + s.f;
+    s.wq = s.f + 1;
+    s.synod_f = s.f;
+  } else {
+    const uint32_t fe = n / 2;
+    s.fq = fe + (fe + 1) / 2;
+    s.wq = fe + 1;
+    s.synod_f = fe;  // EPaxos::allowed_faults
+  }
+  // ---------------------------------------------------------------- init
+  for (uint32_t i = s.lid; i < a.g.words; i += 64) smem[i] = 0;
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (uint32_t k = 0; k < HMAX; ++k) s.ht[k] = s.hs[k] = NONE;
+#pragma unroll
+  for (uint32_t k = 0; k < NMAX; ++k) s.xdot[k] = s.xrec[k] = s.xwait[k] = s.xtl[k] = s.xfr[k] = s.xcf[k] = s.xcw[k] = 0;
+  const uint32_t RP = a.RP;
+  // process regions, quorums (BaseProcess::discover over
+  // sort_processes_by_distance, base.rs:62-154, util.rs:153-185)
+  for (uint32_t p = 0; p < n; ++p) {
+    const uint32_t rp = sp.process_regions[p];
+    // lane q < n: position of process q in p's distance order
+    uint32_t pos = 0;
+    if (s.lid < n) {
+      const uint32_t rq = sp.process_regions[s.lid];
+      const uint32_t kq = a.rank[rp * RP + rq];
+      for (uint32_t q2 = 0; q2 < n; ++q2) {
+        const uint32_t r2 = sp.process_regions[q2];
+        const uint32_t k2 = a.rank[rp * RP + r2];
+        if (k2 < kq || (k2 == kq && q2 < s.lid)) ++pos;
+      }
+    }
+    const uint32_t fqm = (uint32_t)bal(s.lid < n && pos < s.fq);
+    const uint32_t wqm = (uint32_t)bal(s.lid < n && pos < s.wq);
+    s.put(s.P(p, PR_FQ), fqm);
+    s.put(s.P(p, PR_WQ), wqm);
+    s.put(s.P(p, PR_EPOCH), 1);
+    s.put(s.P(p, PR_REGION), rp);
+    if (s.lid < n) s.dly(p * n + s.lid) = a.ping[rp * RP + sp.process_regions[s.lid]] / 2u;
+  }
+  // clients: for region in client_regions, clients_per_region each (runner.rs:143-163)
+  {
+    uint32_t c = 0;
+    for (uint32_t r = 0; r < sp.num_client_regions; ++r) {
+      const uint32_t rc = sp.client_regions[r];
+      // closest process: minimal (rank, id)
+      uint32_t best = 0, bk = 0xFFFFFFFFu;
+      for (uint32_t p = 0; p < n; ++p) {
+        const uint32_t k = a.rank[rc * RP + sp.process_regions[p]];
+        if (k < bk) {
+          bk = k;
+          best = p;
+        }
+      }
+      for (uint32_t i = 0; i < sp.clients_per_region; ++i, ++c) {
+        s.put(s.CL(c, CL_PROC), best);
+        s.put(s.CL(c, CL_REGION), rc);
+        s.put(s.dly(n * n + c), a.ping[rc * RP + sp.process_regions[best]] / 2u);
+        s.put(s.dly(n * n + s.C + c), a.ping[sp.process_regions[best] * RP + rc] / 2u);
+      }
+    }
+  }
+  __builtin_amdgcn_s_barrier();
+  // periodic events (runner.rs:179-187), then clients (run(), C5 ascending)
+  if (s.gc_ms)
+    for (uint32_t p = 0; p < n; ++p) s.schedule_timer(s.link_g(p), s.gc_ms);
+  const bool sim_en = a.sim_exec_notif || s.has_extra;
+  for (uint32_t p = 0; p < n; ++p) {
+    if (sim_en) s.schedule_timer(s.link_e(p), s.en_ms);
+    else ++s.seq;  // keep the insertion numbering of the reference
+  }
+  for (uint32_t c = 0; c < s.C; ++c) {
+    s.client_send(c);
+    if (s.cmds == 0) s.err = FX_ERR_INVALID_ARG;
+  }
+  // ------------------------------------------------------------ loop
+  const uint64_t max_events = a.max_events ? a.max_events : 0xFFFFFFFFull;
+  while (!s.done && !s.err) {
+    uint32_t t = 0;
+    const uint32_t link = s.pop_min(t);
+    if (link == NONE || t == NONE) {
+      s.err = FX_ERR_SIM_LATE;  // "there should be a new action"
+      break;
+    }
+    if (t < s.now) {
+      s.err = FX_ERR_TIME_RANGE;
+      break;
+    }
+    s.now = t;
+    s.run_event(link);
+    if (s.in_extra && s.now > s.final_ms) s.done = true;
+    if (s.events >= max_events) s.err = FX_ERR_SIM_EVENTS;
+  }
+  // ----------------------------------------------------------- outputs
+  __builtin_amdgcn_s_barrier();
+  if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = s.P(s.lid, PR_EXEC);
+  if (a.stats) {
+    unsigned long long* st = a.stats + (size_t)inst * FX_SIM_STATS;
+    if (s.lid < NMAX) {
+      const bool v = s.lid < n;
+      st[FX_SIM_STAT_FAST + s.lid] = v ? s.P(s.lid, PR_FAST) : 0u;
+      st[FX_SIM_STAT_SLOW + s.lid] = v ? s.P(s.lid, PR_SLOW) : 0u;
+      st[FX_SIM_STAT_STABLE + s.lid] = v ? s.P(s.lid, PR_STABLE) : 0u;
+    }
+    if (s.lid == 0) {
+      st[FX_SIM_STAT_EVENTS] = s.events;
+      st[FX_SIM_STAT_END_MS] = s.now;
+      st[FX_SIM_STAT_TRACE] = s.trace;
+      st[FX_SIM_STAT_SEQ] = s.seq;
+    }
+  }
+  if (s.lid == 0) a.err[inst] = s.err;
+}
+
+}  // namespace sim
+
+using namespace sim;
+
+static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, Geo& g) {
+  const uint32_t n = sp.n;
+  if (n < 2 || n > NMAX) return false;
+  const uint32_t C = sp.clients_per_region * sp.num_client_regions;
+  if (C < 1 || C > CMAX) return false;
+  g.n = n;
+  g.C = C;
+  g.K = sp.keys_per_command;
+  g.W = wslots;
+  g.R = ring;
+  g.NP = n * (n - 1);
+  g.L = g.NP + 2 * n + 2 * C;
+  if (g.L > 64 * HMAX) return false;
+  g.ncli_keys = sp.pool_size + C + 1;
+  uint32_t o = 0;
+  g.off_ring = o; o += g.NP * g.R * 3;
+  g.off_rh = o; o += g.NP;
+  g.off_snap = o; o += n * RS * n;
+  g.off_slot = o; o += n * g.W * SLOTW;
+  g.off_kd = o; o += n * g.ncli_keys;
+  g.off_proc = o; o += n * PRW;
+  g.off_cli = o; o += C * CLW;
+  g.off_frame = o; o += FMAX * FRW;
+  g.off_wl = o; o += 72;
+  g.off_delay = o; o += n * n + 2 * C;
+  g.words = (o + 3) & ~3u;
+  return true;
+}
+
+}  // namespace fx
+
+using namespace fx;
+
+extern "C" {
+
+int fx_sim_plan(const fx_sim_spec* sp, uint32_t ring_entries, uint32_t dot_slots, uint32_t* lds_bytes) {
+  if (!sp || !lds_bytes) return FX_ERR_INVALID_ARG;
+  Geo g;
+  if (!sim_geometry(*sp, ring_entries, dot_slots, g)) return FX_ERR_UNSUPPORTED;
+  *lds_bytes = g.words * 4;
+  return FX_OK;
+}
+
+int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) {
+  if (!b || !o || !b->specs || !b->host_specs || !o->err || !b->planet_ping || !b->planet_rank) return FX_ERR_INVALID_ARG;
+  if (b->instances == 0) return FX_OK;
+  int dc = 0;
+  if (hipGetDeviceCount(&dc) != hipSuccess || dc <= 0) return FX_ERR_NO_DEVICE;
+  const uint32_t ring = b->ring_entries ? b->ring_entries : 32u;
+  const uint32_t W = b->dot_slots ? b->dot_slots : 8u;
+  if ((ring & (ring - 1)) || ring > 4096 || (W & (W - 1)) || W > 256) return FX_ERR_INVALID_ARG;
+  const fx_sim_spec& s0 = b->host_specs[0];
+  // every instance of a launch shares the geometry (protocol, n, clients, keys)
+  for (uint32_t i = 0; i < b->instances; ++i) {
+    const fx_sim_spec& s = b->host_specs[i];
+    if (s.protocol != FX_PROTOCOL_ATLAS && s.protocol != FX_PROTOCOL_EPAXOS) return FX_ERR_UNSUPPORTED;
+    if (s.n != s0.n || s.clients_per_region != s0.clients_per_region ||
+        s.num_client_regions != s0.num_client_regions || s.keys_per_command != s0.keys_per_command ||
+        s.pool_size != s0.pool_size)
+      return FX_ERR_INVALID_ARG;
+    if (s.read_only_pct != 0 || s.reorder_messages || s.nfr) return FX_ERR_UNSUPPORTED;
+    if (s.keys_per_command < 1 || s.keys_per_command > KMAX || s.pool_size < 1) return FX_ERR_INVALID_ARG;
+    if (s.f > s.n / 2) return FX_ERR_INVALID_ARG;
+    if (s.keys_per_command == 2 && s.conflict_rate >= 100) return FX_ERR_INVALID_ARG;  // workload.rs:49-51
+    for (uint32_t p = 0; p < s.n; ++p)
+      if (s.process_regions[p] >= b->planet_regions) return FX_ERR_INVALID_ARG;
+    for (uint32_t r = 0; r < s.num_client_regions; ++r)
+      if (s.client_regions[r] >= b->planet_regions) return FX_ERR_INVALID_ARG;
+    if (s.executed_notification_ms == 0 && s.extra_sim_time_ms >= 0) return FX_ERR_INVALID_ARG;
+  }
+  SimArgs a{};
+  if (!sim_geometry(s0, ring, W, a.g)) return FX_ERR_UNSUPPORTED;
+  const size_t lds = (size_t)a.g.words * 4;
+  if (lds > 160 * 1024) return FX_ERR_UNSUPPORTED;
+  if (a.g.ncli_keys > 0xFFFFu) return FX_ERR_UNSUPPORTED;
+  a.specs = b->specs;
+  a.instances = b->instances;
+  a.ping = b->planet_ping;
+  a.rank = b->planet_rank;
+  a.RP = b->planet_stride;
+  a.exec_cap = b->exec_cap;
+  a.lat_cap = b->lat_cap;
+  a.max_events = b->max_events;
+  a.sim_exec_notif = b->flags & FX_SIM_FLAG_EXEC_NOTIFICATIONS;
+  a.executed = o->executed;
+  a.executed_len = o->executed_len;
+  a.latency_log = o->latency_log;
+  a.lat_hist = (unsigned long long*)o->latency_hist;
+  a.lat_bins = o->lat_bins ? o->lat_bins : 1;
+  a.chain_hist = (unsigned long long*)o->chain_hist;
+  a.chain_bins = o->chain_bins ? o->chain_bins : 1;
+  a.delay_hist = (unsigned long long*)o->delay_hist;
+  a.delay_bins = o->delay_bins ? o->delay_bins : 1;
+  a.stats = (unsigned long long*)o->stats;
+  a.err = o->err;
+  static bool configured = false;
+  if (!configured) {
+    (void)hipFuncSetAttribute((const void*)sim::k_sim, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    configured = true;
+  }
+  hipLaunchKernelGGL(sim::k_sim, dim3(b->instances), dim3(64), lds, (hipStream_t)hip_stream, a);
+  return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
+}
+
+}  // extern "C"

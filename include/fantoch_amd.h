@@ -44,6 +44,11 @@ extern "C" {
 #define FX_ERR_TIME_RANGE 9    /* t_ms >= 2^24 relative to the stream base     */
 #define FX_ERR_NO_DEVICE 10    /* no GPU visible: the product never falls back */
 #define FX_ERR_LOG_FORMAT 11   /* malformed execution log (rw/mod.rs:90 `expect` panics) */
+#define FX_ERR_SIM_CAPACITY 12 /* a simulated instance outgrew a table of its launch geometry
+                                  (message ring, dot table, executor slots, clock window) */
+#define FX_ERR_SIM_LATE 13     /* a simulated message found no state for its dot, or a
+                                  reference assertion failed (runner.rs:239-241, single.rs:346-349) */
+#define FX_ERR_SIM_EVENTS 14   /* a simulated instance exceeded its event budget */
 
 /* ------------------------------------------------- packed stream format */
 /* A dot (fantoch/src/id.rs:21-27, Id<u8>{source, sequence}, derived Ord) is
@@ -332,6 +337,69 @@ typedef struct fx_sim_spec {
   uint8_t process_regions[FX_SIM_MAX_N];
   uint8_t client_regions[FX_SIM_MAX_CLIENT_REGIONS];
 } fx_sim_spec;
+
+/* A batch of instances on one GPU (fx_sim_run): one wavefront per instance.
+ * All instances of a batch share protocol family geometry: n, clients per
+ * region, number of client regions, keys per command and pool size (the
+ * conflict rate, f, seeds, regions and intervals may differ per instance).
+ * The GPU path simulates Atlas and EPaxos (GraphExecutor protocols) without
+ * read-only commands, NFR or message reordering (FX_ERR_UNSUPPORTED). */
+#define FX_SIM_FLAG_EXEC_NOTIFICATIONS 1u /* simulate the periodic executed notifications
+                                             even when they cannot change the outcome
+                                             (GraphExecutor::executed is None; they matter
+                                             only for where a run with extra time stops) */
+typedef struct fx_sim_batch {
+  const fx_sim_spec* specs;        /* [instances] device copy                          */
+  const fx_sim_spec* host_specs;   /* [instances] host copy (validation, geometry)     */
+  uint32_t instances;
+  uint32_t flags;                  /* FX_SIM_FLAG_*                                     */
+  const uint16_t* planet_ping;     /* device [planet_regions][planet_stride] ping (ms)  */
+  const uint8_t* planet_rank;      /* device [planet_regions][planet_stride]: position of
+                                      region b in region a's sorted order               */
+  uint32_t planet_regions, planet_stride;
+  uint32_t exec_cap;               /* executed dots kept per process (the rest counted) */
+  uint32_t lat_cap;                /* latencies kept per client (0 = no latency log)    */
+  uint32_t max_events;             /* per-instance event budget (0 = 2^32 - 1)          */
+  uint32_t ring_entries;           /* messages in flight per process link (power of 2; 0 = 32) */
+  uint32_t dot_slots;              /* live dots per coordinator (power of 2; 0 = 8)     */
+  uint32_t pad;
+} fx_sim_batch;
+
+/* per-instance counters (u64) */
+#define FX_SIM_STAT_FAST 0u     /* [n] ProtocolMetricsKind::FastPath per process  */
+#define FX_SIM_STAT_SLOW 8u     /* [n] SlowPath                                    */
+#define FX_SIM_STAT_STABLE 16u  /* [n] Stable (commands garbage-collected)         */
+#define FX_SIM_STAT_EVENTS 24u  /* actions processed (executed notifications excluded) */
+#define FX_SIM_STAT_END_MS 25u  /* simulation time when the run stopped            */
+#define FX_SIM_STAT_TRACE 26u   /* hash of the processed action sequence (debug)   */
+#define FX_SIM_STAT_SEQ 27u     /* schedule insertions                             */
+#define FX_SIM_STATS 32u
+
+typedef struct fx_sim_output {  /* device buffers; NULL where not wanted */
+  uint32_t* executed;           /* [instances][n][exec_cap] packed dots, execution order */
+  uint32_t* executed_len;       /* [instances][n] commands executed per process     */
+  uint32_t* latency_log;        /* [instances][clients][lat_cap] client latency (ms) */
+  uint64_t* latency_hist;       /* [planet_regions][lat_bins] per client region, accumulated */
+  uint64_t* chain_hist;         /* [chain_bins] ExecutorMetricsKind::ChainSize, accumulated */
+  uint64_t* delay_hist;         /* [delay_bins] ExecutionDelay (ms), accumulated    */
+  uint64_t* stats;              /* [instances][FX_SIM_STATS]                        */
+  uint32_t* err;                /* [instances] FX_* status                           */
+  uint32_t lat_bins, chain_bins, delay_bins, pad;
+} fx_sim_output;
+
+/* LDS bytes one instance of `spec` needs at the given table sizes
+ * (FX_ERR_UNSUPPORTED if it does not fit the GPU path). */
+int fx_sim_plan(const fx_sim_spec* spec, uint32_t ring_entries, uint32_t dot_slots, uint32_t* lds_bytes);
+/* Runs every instance to completion (Runner::run, runner.rs:202-231); asynchronous. */
+int fx_sim_run(const fx_sim_batch* batch, const fx_sim_output* out, void* hip_stream);
+
+/* Planet::from(dir) (fantoch/src/planet/mod.rs:38-54, dat.rs:20-94): regions
+ * in name order; ping[a][b] (ms, `as u64` of the average) and rank[a][b] = the
+ * position of b in a's (latency, name) order (Planet::sorted, mod.rs:122-140),
+ * row stride `cap`.  With ping == NULL only *num_regions is filled.  names:
+ * newline-separated region names (may be NULL). */
+int fx_planet_load(const char* dir, uint32_t cap, uint32_t* num_regions, char* names, uint32_t names_bytes,
+                   uint16_t* ping, uint8_t* rank);
 
 /* ------------------------------------------------------- execution log */
 /* Reader for the run mode's execution log: LengthDelimitedCodec frames

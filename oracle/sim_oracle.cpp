@@ -779,7 +779,8 @@ bool gen_cmd(const fx_sim_spec& spec, uint64_t client, uint64_t idx, Cmd& cmd) {
       key = spec.pool_size + (uint32_t)client;
     }
     ++draw;
-    if (draw > 64) return false;
+    if (draw >= 64 && keys.size() + (std::find(keys.begin(), keys.end(), key) == keys.end()) != spec.keys_per_command)
+      return false;
     if (std::find(keys.begin(), keys.end(), key) == keys.end()) keys.push_back(key);
   }
   std::sort(keys.begin(), keys.end());  // C11
@@ -935,7 +936,7 @@ class Runner {
   std::map<std::pair<uint64_t, uint64_t>, SchedAction> queue;  // (time ms, seq) -> action (C3)
   uint64_t seq = 0;
   uint64_t now_us = 0;
-  uint64_t events = 0, trace = 0, reorder_draws = 0;
+  uint64_t events = 0, trace = 0, reorder_draws = 0, exec_notifications = 0;
 
   uint64_t now_ms() const { return now_us / 1000; }
 
@@ -1011,8 +1012,9 @@ class Runner {
           break;
         }
         case SK::PeriodicExecutedNotification: {
-          // GraphExecutor / BasicExecutor::executed are None (executor/mod.rs:74-79)
-          note(1, a.to, 0, 0);
+          // GraphExecutor / BasicExecutor::executed are None (executor/mod.rs:74-79):
+          // counted apart, not part of the action trace
+          ++exec_notifications;
           SchedAction b;
           b.kind = SK::PeriodicExecutedNotification;
           b.to = a.to;

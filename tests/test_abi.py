@@ -177,3 +177,31 @@ def test_quorum_sizes_kats():
     assert _lib.quorum_sizes(A, 3, 1) == (2, 2)  # BASELINE configs[0]: d <= 2
     with pytest.raises(_lib.FxError):
         _lib.quorum_sizes(7, 5, 1)
+
+
+def test_product_planet_matches_the_oracle_parser():
+    """fx_planet_load (product, host C++) and the oracle's Planet parser read the
+    same latency_gcp/*.dat files into the same matrix and distance order."""
+    from fantoch_amd import sim as S
+    from oracle import oracle_lib as O
+    pl = S.Planet()
+    assert pl.regions == O.planet_regions()
+    lat, srt = O.planet_matrix()
+    R = pl.R
+    assert np.array_equal(pl.ping[:R, :R].astype(np.int64), lat)
+    for a in range(R):  # rank[a][b] = position of b in sorted(a)
+        assert [int(b) for b in np.argsort(pl.rank[a, :R])] == [int(x) for x in srt[a]]
+
+
+def test_sim_plan_sizes():
+    from fantoch_amd import sim as S
+    import ctypes
+    pl = S.Planet()
+    lib = _lib.load()
+    regs = pl.ids(S.GCP5[:5])
+    s = S.spec(S.EPAXOS, 5, 2, regs, regs)
+    b = ctypes.c_uint32()
+    assert lib.fx_sim_plan(ctypes.byref(s), 32, 8, ctypes.byref(b)) == 0
+    assert 8 * 1024 < b.value < 64 * 1024
+    s9 = S.spec(S.EPAXOS, 5, 2, regs, regs, clients_per_region=40)  # 200 clients: too many links
+    assert lib.fx_sim_plan(ctypes.byref(s9), 32, 8, ctypes.byref(b)) == _lib.FX_ERR_UNSUPPORTED

@@ -1,0 +1,137 @@
+"""GPU simulator (fx_sim_run) vs the simulator oracle, bit for bit: per-process
+execution order, per-command client latencies (so every latency histogram),
+fast/slow/stable counters, the action trace and where the run stopped.  GPU
+only; instances are small enough for the oracle to finish in seconds."""
+import numpy as np
+import pytest
+
+from fantoch_amd import _lib
+from fantoch_amd import sim as S
+from oracle import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+PLANET = None
+
+
+def planet():
+    global PLANET
+    if PLANET is None:
+        PLANET = S.Planet()
+    return PLANET
+
+
+def to_oracle(s):
+    o = O.SimSpec()
+    for name, _ in _lib.SimSpec._fields_:
+        v = getattr(s, name)
+        if name in ("process_regions", "client_regions"):
+            arr = getattr(o, name)
+            for i in range(len(v)):
+                arr[i] = v[i]
+        else:
+            setattr(o, name, v)
+    return o
+
+
+def client_regions(s):
+    out = []
+    for r in range(s.num_client_regions):
+        out += [s.client_regions[r]] * s.clients_per_region
+    return out
+
+
+def assert_instance_parity(res, i, s, o):
+    g_exec = res.executed(i)
+    for p in range(s.n):
+        assert np.array_equal(g_exec[p], o["executed"][p]), "process %d order differs" % (p + 1)
+    assert int(res.err[i]) == 0
+    assert [int(x) for x in res.fast(i)] == [int(x) for x in o["fast"]]
+    assert [int(x) for x in res.slow(i)] == [int(x) for x in o["slow"]]
+    assert [int(x) for x in res.stable(i)] == [int(x) for x in o["stable"]]
+    assert res.end_ms(i) == o["end_ms"]
+    assert res.events(i) == o["events"]
+    assert res.trace(i) == o["trace"]
+    # client latency histograms per region (clients_latencies, runner.rs:619-634)
+    lat = res.latencies(i)
+    regs = client_regions(s)
+    hist = np.zeros_like(o["latency"])
+    for c, r in enumerate(regs):
+        np.add.at(hist[r], np.minimum(lat[c, :s.commands_per_client], hist.shape[1] - 1), 1)
+    assert np.array_equal(hist, o["latency"])
+
+
+def run_and_compare(specs, **kw):
+    res = S.run(specs, planet(), **kw)
+    bad = [(i, int(e)) for i, e in enumerate(res.err) if e]
+    assert not bad, "instances failed: %s" % bad[:8]
+    orc = O.sim_batch([to_oracle(s) for s in specs], threads=8)
+    for i, (s, o) in enumerate(zip(specs, orc)):
+        assert o["status"] == 0
+        assert_instance_parity(res, i, s, o)
+    # batch histograms = sums of the oracle's
+    lat = sum(o["latency"] for o in orc)
+    assert np.array_equal(res.latency_hist[:, :lat.shape[1]], lat[:, :res.latency_hist.shape[1]])
+    assert np.array_equal(res.chain, sum(o["chain"] for o in orc)[:res.chain.shape[0]])
+    assert np.array_equal(res.delay, sum(o["delay"] for o in orc)[:res.delay.shape[0]])
+    return res, orc
+
+
+def test_config0_atlas_n3_gcp_reference_order():
+    """BASELINE configs[0]: Atlas n=3 f=1, GCP planet (simulation.rs gcp_planet
+    regions), 1 client per region, 2 % conflicts, 1000 commands per client."""
+    pl = planet()
+    regs = pl.ids(S.GCP5[:3])
+    s = S.spec(S.ATLAS, 3, 1, regs, regs, commands_per_client=1000, conflict_rate=2, seed=1)
+    res, orc = run_and_compare([s])
+    assert all(len(e) >= 2990 for e in res.executed(0))
+
+
+@pytest.mark.parametrize("protocol,n,f", [(S.EPAXOS, 5, 2), (S.ATLAS, 5, 1), (S.ATLAS, 5, 2)])
+def test_conflict_sweep_n5(protocol, n, f):
+    """configs[1] shape: seeds x conflict {0,2,10,50,100} %, n = 5 (100 commands)."""
+    pl = planet()
+    regs = pl.ids(S.GCP5[:n])
+    specs = [S.spec(protocol, n, f, regs, regs, commands_per_client=100, conflict_rate=c,
+                    seed=77, instance=i) for i, c in enumerate([0, 2, 10, 50, 100] * 4)]
+    run_and_compare(specs)
+
+
+def test_region_subsets_n7():
+    """configs[2] shape: Atlas n=7 f=1/2 over region subsets of the 20 GCP regions."""
+    import itertools
+    pl = planet()
+    subsets = list(itertools.combinations(range(pl.R), 7))[::9973][:12]
+    specs = [S.spec(S.ATLAS, 7, 1 + (i % 2), list(sub), list(sub), commands_per_client=60,
+                    conflict_rate=10, seed=5, instance=i) for i, sub in enumerate(subsets)]
+    run_and_compare(specs)
+
+
+def test_two_clients_per_region_two_keys():
+    pl = planet()
+    regs = pl.ids(S.GCP5[:5])
+    specs = [S.spec(S.EPAXOS, 5, 2, regs, regs, clients_per_region=2, commands_per_client=60,
+                    keys_per_command=2, conflict_rate=c, seed=3, instance=i)
+             for i, c in enumerate([0, 50, 90])]
+    run_and_compare(specs, dot_slots=16)
+
+
+def test_extra_time_and_client_regions_apart():
+    """Clients in regions without a process, extra simulated time after the
+    clients finish (runner.rs:285-311) and executed notifications simulated."""
+    pl = planet()
+    p = pl.ids(["asia-east1", "us-central1", "us-west1"])
+    c = pl.ids(["us-west1", "us-west2", "europe-west3"])
+    specs = [S.spec(S.ATLAS, 3, 1, p, c, commands_per_client=80, conflict_rate=100,
+                    gc_interval_ms=100, executed_notification_ms=50, extra_sim_time_ms=1000,
+                    seed=2, instance=i) for i in range(3)]
+    run_and_compare(specs, flags=_lib.FX_SIM_FLAG_EXEC_NOTIFICATIONS)
+    run_and_compare(specs)
+
+
+def test_no_gc():
+    pl = planet()
+    regs = pl.ids(S.GCP5[:5])
+    specs = [S.spec(S.EPAXOS, 5, 2, regs, regs, commands_per_client=80, conflict_rate=50,
+                    gc_interval_ms=0, seed=4, instance=i) for i in range(4)]
+    run_and_compare(specs)
