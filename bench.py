@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
-"""bench.py — executed commands/s of the batched GPU GraphExecutor (BASELINE.json configs[1]).
+"""bench.py — executed commands/s of batched Atlas/EPaxos simulations (BASELINE.json).
 
+--mode sim (default, bench_sim.py): BASELINE configs[1], the batched simulator
+itself — EPaxos n=5 f=2 on the GCP planet, 4096 seeds x conflict {0,2,10,50,100}%
+per GPU, every instance simulated end to end on the GPU (fx_sim_run).
+
+--mode executor: the GraphExecutor alone over synthetic commit streams.
 Workload (per GPU; weak scaling): EPaxos n=5, 4096 seeds x conflict rates
 {0,2,10,50,100}% = 20,480 instances, 1 client per process x 1,000 commands
 -> 5 commit streams of 5,000 Adds per instance (102,400 streams, 512M Adds).
@@ -39,13 +44,20 @@ LAYOUT = {0: "16 lanes per stream", 1: "one lane per stream", 2: "one lane per s
 
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["sim", "executor"], default="sim",
+                    help="sim: the batched simulator (BASELINE configs[1], the headline); "
+                         "executor: the GraphExecutor alone over synthetic commit streams")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--seeds", type=int, default=4096)
     ap.add_argument("--conflicts", type=str, default="0,2,10,50,100")
     ap.add_argument("--n", type=int, default=5)
-    ap.add_argument("--cmds", type=int, default=1000)
+    ap.add_argument("--cmds", type=int, default=None,
+                    help="commands per client (sim default 200 as fantoch_ps/src/bin/simulation.rs; "
+                         "executor default 1000)")
+    ap.add_argument("--protocol", choices=["epaxos", "atlas"], default="epaxos")
+    ap.add_argument("--f", type=int, default=2)
     ap.add_argument("--window", type=int, default=8)
     ap.add_argument("--cycle-pct", type=int, default=30)
     ap.add_argument("--seed", type=int, default=20250213)
@@ -53,7 +65,10 @@ def parse():
                     help="instances per conflict rate block (-1 = --seeds: conflict-major "
                          "enumeration, so a wavefront's streams share a rate; 0 = seed-major)")
     ap.add_argument("--tier", type=int, default=-1, help="executor tier (-1 = FX_TIER_DEFAULT)")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=5.0)
+    ap.add_argument("--ring-entries", type=int, default=16, help="sim: messages in flight per link")
+    ap.add_argument("--dot-slots", type=int, default=8, help="sim: live dots per coordinator")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=None,
+                    help="CPU work budget of the cpu_baseline sample (sim default 15, executor 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", type=str, default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args()
@@ -98,6 +113,13 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(launch_ranks(args))
+    if args.mode == "sim":
+        from bench_sim import main_sim
+        return main_sim(args)
+    if args.cmds is None:
+        args.cmds = 1000
+    if args.cpu_baseline_seconds is None:
+        args.cpu_baseline_seconds = 5.0
     import numpy as np
     import torch
     import torch.distributed as dist

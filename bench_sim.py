@@ -1,0 +1,314 @@
+"""bench.py --mode sim: BASELINE configs[1] on the GPU simulator (fx_sim_run).
+
+Workload per GPU (weak scaling): EPaxos n=5 f=2 (Config::new(5, 2)) on the GCP
+planet with fantoch_ps/src/bin/simulation.rs's regions (gcp_planet, first n),
+1 client per region, pool 1, 1 key per command, GC and executed
+notifications every 10 ms (the binary's config! macro), Runner::run(None);
+`--seeds` seeds x conflict {0,2,10,50,100}% instances, `--cmds` commands per
+client (default 200 as the binary).  Rank r simulates global instances
+[r P, (r + 1) P), P = seeds x rates, each with its own C6 RNG stream, the
+heaviest conflict rate first.  One step = every instance simulated from
+Runner::new to the end of Runner::run in one kernel launch (inputs resident
+in HBM); outputs = per-process execution orders, client latency histograms,
+protocol counters.
+
+value = commands executed by every process's GraphExecutor, summed over the
+instances of every rank, / the max-over-ranks time of the timed steps.
+"""
+import ctypes
+import json
+import os
+import time
+
+import numpy as np
+
+METRIC = "executed cmds/sec (node) for batched Atlas/EPaxos sims; % of HBM roofline"
+HBM_PEAK_GBPS = 8000.0
+
+
+def local_specs(S, args, rank, planet):
+    conflicts = sorted((int(c) for c in args.conflicts.split(",")), reverse=True)
+    regs = planet.ids(S.GCP5[:args.n])
+    proto = S.EPAXOS if args.protocol == "epaxos" else S.ATLAS
+    per = args.seeds * len(conflicts)
+    specs, rates = [], []
+    for ci, c in enumerate(conflicts):
+        for k in range(args.seeds):
+            g = rank * per + ci * args.seeds + k
+            specs.append(S.spec(proto, args.n, args.f, regs, regs, commands_per_client=args.cmds,
+                                conflict_rate=c, seed=args.seed, instance=g))
+            rates.append(c)
+    return specs, rates, conflicts
+
+
+def main_sim(args):
+    import torch
+    import torch.distributed as dist
+
+    from bench import host_cpus, measured_copy_gbps
+    from fantoch_amd import _lib
+    from fantoch_amd import metrics as fm
+    from fantoch_amd import sim as S
+
+    if args.cmds is None:
+        args.cmds = 200
+    if args.cpu_baseline_seconds is None:
+        args.cpu_baseline_seconds = 15.0
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    lib = _lib.load()
+    if lib.fx_device_count() <= 0:
+        raise SystemExit("no GPU visible to libfantoch_amd")
+
+    planet = S.Planet()
+    specs, rates, conflicts = local_specs(S, args, rank, planet)
+    N = len(specs)
+    n = args.n
+    C = n  # one client per region, clients in the process regions
+    exec_cap = C * args.cmds + 8
+    LAT_BINS, CHAIN_BINS, DELAY_BINS = 8192, 256, 8192
+    host = (_lib.SimSpec * N)(*specs)
+    stream = torch.cuda.current_stream(dev)
+    hs = ctypes.c_void_p(stream.cuda_stream)
+
+    spec_dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev)
+    ping = torch.from_numpy(planet.ping.astype(np.int16).view(np.int16)).to(dev)
+    rank_m = torch.from_numpy(planet.rank).to(dev)
+    executed = torch.empty(N * n * exec_cap, dtype=torch.int32, device=dev)
+    executed_len = torch.zeros(N * n, dtype=torch.int32, device=dev)
+    lat_hist = torch.zeros(planet.R * LAT_BINS, dtype=torch.int64, device=dev)
+    chain = torch.zeros(CHAIN_BINS, dtype=torch.int64, device=dev)
+    delay = torch.zeros(DELAY_BINS, dtype=torch.int64, device=dev)
+    stats = torch.zeros(N * _lib.FX_SIM_STATS, dtype=torch.int64, device=dev)
+    err = torch.zeros(N, dtype=torch.int32, device=dev)
+    batch = _lib.SimBatch(spec_dev.data_ptr(), ctypes.addressof(host), N, 0, ping.data_ptr(),
+                          rank_m.data_ptr(), planet.R, S.Planet.STRIDE, exec_cap, 0, 0,
+                          args.ring_entries, args.dot_slots, 0)
+    out = _lib.SimOutput(executed.data_ptr(), executed_len.data_ptr(), None, lat_hist.data_ptr(),
+                         chain.data_ptr(), delay.data_ptr(), stats.data_ptr(), err.data_ptr(),
+                         LAT_BINS, CHAIN_BINS, DELAY_BINS, 0)
+
+    def step():
+        lat_hist.zero_()
+        chain.zero_()
+        delay.zero_()
+        _lib.check(lib.fx_sim_run(ctypes.byref(batch), ctypes.byref(out), hs), "fx_sim_run")
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize(dev)
+    bad = int((err != 0).sum().item())
+    if bad:
+        raise SystemExit("%d simulated instances failed: %s" % (bad, torch.unique(err).tolist()))
+
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    kernel_ms = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        lat_hist.zero_()
+        chain.zero_()
+        delay.zero_()
+        ev0.record(stream)
+        _lib.check(lib.fx_sim_run(ctypes.byref(batch), ctypes.byref(out), hs), "fx_sim_run")
+        ev1.record(stream)
+        ev1.synchronize()
+        kernel_ms.append(ev0.elapsed_time(ev1))
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    st = stats.view(N, _lib.FX_SIM_STATS)
+    executed_local = int(executed_len.to(torch.int64).sum().item())
+    events_local = int(st[:, _lib.FX_SIM_STAT_EVENTS].sum().item())
+    deps_local = int(st[:, _lib.FX_SIM_STAT_DEPS].sum().item())
+    client_cmds_local = N * C * args.cmds
+    tot = torch.tensor([elapsed, executed_local, events_local, deps_local, client_cmds_local],
+                       dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = tot[:1].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tot[1:].clone()
+        dist.all_reduce(sm)
+        elapsed = float(mx.item())
+        executed_all, events_all, deps_all, client_all = [float(x) for x in sm.tolist()]
+        for h in (lat_hist, chain, delay):
+            dist.all_reduce(h)
+    else:
+        executed_all, events_all, deps_all, client_all = (float(executed_local), float(events_local),
+                                                          float(deps_local), float(client_cmds_local))
+
+    # per-instance rows (global id, conflict %, executed, fast, slow, status), one all_gather
+    gid = torch.arange(N, dtype=torch.int64, device=dev) + rank * N
+    rows = torch.stack([gid, torch.tensor(rates, dtype=torch.int64, device=dev),
+                        executed_len.view(N, n).to(torch.int64).sum(1),
+                        st[:, _lib.FX_SIM_STAT_FAST:_lib.FX_SIM_STAT_FAST + n].sum(1),
+                        st[:, _lib.FX_SIM_STAT_SLOW:_lib.FX_SIM_STAT_SLOW + n].sum(1),
+                        err.to(torch.int64)], 1)
+    if world > 1:
+        parts = [torch.empty_like(rows) for _ in range(world)]
+        dist.all_gather(parts, rows.contiguous())
+        rows = torch.cat(parts)
+    summary = {"fields": ["instance", "conflict_pct", "executed", "fast_paths", "slow_paths", "status"],
+               "instances": int(rows.shape[0]), "all_ok": bool((rows[:, 5] == 0).all().item()),
+               "executed_matches": int(rows[:, 2].sum().item()) == int(executed_all)}
+    fast_all, slow_all = int(rows[:, 3].sum().item()), int(rows[:, 4].sum().item())
+
+    value = executed_all * args.steps / elapsed
+    result = None
+    if rank == 0:
+        kavg = sum(kernel_ms) / len(kernel_ms)
+        dbar = deps_all / executed_all if executed_all else 0.0
+        # 32 + 4k + 8d bytes per executed command (k = 1)
+        alg_bytes = (36.0 + 8.0 * dbar) * executed_local
+        achieved = alg_bytes / (kavg * 1e-3) / 1e9
+        traffic = None
+        tj_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "sim_traffic_latest.json")
+        if os.path.exists(tj_path):
+            try:
+                tj = json.load(open(tj_path))
+                if tj.get("workload_key") == sim_key(args):
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        copy = measured_copy_gbps(torch, dev)
+        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic, "kernel": "k_sim",
+                "kernel_ms_avg": round(kavg, 3), "alg_bytes_per_launch": int(alg_bytes),
+                "alg_bytes_per_cmd": round(36.0 + 8.0 * dbar, 3),
+                "alg_bytes_definition": "SURVEY.md 8(d): 32 + 4k + 8d per executed command, k = 1, "
+                                        "d = mean deps of the executor Adds",
+                "measured_copy_gbps": copy,
+                "note": "the simulator is a chain of dependent LDS operations per event (no "
+                        "HBM-bound phase): events/s per wavefront is the figure that moves"}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline_sim(args, specs, rates, executed, executed_len, st, lat_hist, n, exec_cap,
+                                   planet)
+        lat = lat_hist.view(planet.R, LAT_BINS).cpu().numpy()
+        regions = S.GCP5[:n]
+        hist_stats = {"client_latency_ms": {r: fm.dense_stats(lat[planet.index[r]]) for r in regions},
+                      "chain_size": fm.dense_stats(chain.cpu().numpy()),
+                      "execution_delay_ms": fm.dense_stats(delay.cpu().numpy())}
+        result = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "cmds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: seeded closed-loop clients (canonical C6 RNG), GCP latency matrix",
+            "config": {
+                "workload": "%s n=%d f=%d, %d seeds x conflict {%s}%% per GPU, 1 client/region, "
+                            "%d cmds/client, GCP regions %s (BASELINE configs[1])"
+                            % (args.protocol.capitalize(), n, args.f, args.seeds, args.conflicts,
+                               args.cmds, ",".join(S.GCP5[:n])),
+                "instances_per_gpu": N, "client_cmds_per_gpu": client_cmds_local,
+                "parallelism": "instances sharded over %d GPU(s) (weak), one wavefront per "
+                               "simulated instance" % world,
+            },
+            "executed_per_step": int(executed_all),
+            "client_cmds_per_s": round(client_all * args.steps / elapsed, 1),
+            "sim_events_per_s": round(events_all * args.steps / elapsed, 1),
+            "fast_paths": fast_all, "slow_paths": slow_all,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "instance_summary": summary,
+            "histograms": hist_stats,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+def sim_key(args):
+    return "sim_%s_n%d_f%d_s%d_c%s_m%d_seed%d" % (args.protocol, args.n, args.f, args.seeds,
+                                                 args.conflicts.replace(",", "-"), args.cmds, args.seed)
+
+
+def cpu_baseline_sim(args, specs, rates, executed, executed_len, st, lat_hist, n, exec_cap, planet):
+    """The simulator oracle (oracle/sim_oracle.cpp, the C++ restatement of the
+    reference simulator) on a bounded sample of the same instances, one
+    instance per std::thread task like the reference binary's rayon par_iter,
+    on every usable host core; the GPU's outputs for the sample are checked
+    against it bit for bit (execution orders, counters, latency histograms)."""
+    import torch
+    from bench import host_cpus
+    from oracle import oracle_lib as O
+    from fantoch_amd import _lib
+
+    host = host_cpus()
+    threads = host["usable"]
+    to_o = lambda s: _to_oracle(_lib, O, s)
+    # calibrate: one instance of every rate, single-threaded
+    t0 = time.perf_counter()
+    firsts = {}
+    for i, r in enumerate(rates):
+        firsts.setdefault(r, i)
+    O.sim_batch([to_o(specs[i]) for i in firsts.values()], threads=1)
+    per_inst = (time.perf_counter() - t0) / len(firsts)
+    budget = max(len(firsts), int(args.cpu_baseline_seconds * threads / max(per_inst, 1e-4)))
+    k = min(len(specs), budget)
+    pick = np.unique(np.linspace(0, len(specs) - 1, k).round().astype(np.int64))
+    t0 = time.perf_counter()
+    res = O.sim_batch([to_o(specs[i]) for i in pick], threads=threads)
+    dt = time.perf_counter() - t0
+    executed_cpu = sum(int(sum(len(e) for e in r["executed"])) for r in res)
+    # parity on the sample
+    el = executed_len.view(len(specs), n).cpu().numpy()
+    stc = st.cpu().numpy()
+    ok = True
+    for j, i in enumerate(pick):
+        r = res[j]
+        ex = executed[i * n * exec_cap:(i + 1) * n * exec_cap].view(n, exec_cap).cpu().numpy().view(np.uint32)
+        for p in range(n):
+            if not np.array_equal(ex[p, :el[i, p]], r["executed"][p]):
+                ok = False
+        if [int(x) for x in stc[i, 0:n]] != [int(x) for x in r["fast"]] or \
+           [int(x) for x in stc[i, 8:8 + n]] != [int(x) for x in r["slow"]] or \
+           [int(x) for x in stc[i, 16:16 + n]] != [int(x) for x in r["stable"]] or \
+           int(stc[i, 26]) != r["trace"] or int(stc[i, 25]) != r["end_ms"]:
+            ok = False
+        if not ok:
+            break
+    return {"value": round(executed_cpu / dt, 1), "unit": "cmds/s", "cores": threads, "kind": "port",
+            "host": host,
+            "sample": "%d of %d instances spread over every conflict rate, simulated end to end by the "
+                      "C++ simulator oracle in %.2f s on %d threads (%d executed commands); GPU output "
+                      "on the sample %s the oracle bit-for-bit (execution orders, fast/slow/stable "
+                      "counters, action trace, end time)"
+                      % (len(pick), len(specs), dt, threads, executed_cpu,
+                         "matches" if ok else "DIFFERS FROM"),
+            "sample_parity": ok}
+
+
+def _to_oracle(_lib, O, s):
+    o = O.SimSpec()
+    for name, _ in _lib.SimSpec._fields_:
+        v = getattr(s, name)
+        if name in ("process_regions", "client_regions"):
+            arr = getattr(o, name)
+            for i in range(len(v)):
+                arr[i] = v[i]
+        else:
+            setattr(o, name, v)
+    return o

@@ -55,8 +55,7 @@ namespace sim {
 constexpr uint32_t NMAX = FX_SIM_MAX_N;  // processes
 constexpr uint32_t CMAX = 32;            // clients per instance
 constexpr uint32_t KMAX = 2;             // keys per command
-constexpr uint32_t VMAX = 16;            // deps of a committed value
-constexpr uint32_t AMAX = 4;             // deps of one MCollectAck
+constexpr uint32_t VMAX = 16;            // deps of a committed value (per-launch: K (n + 1))
 constexpr uint32_t RS = 32;              // GC frontier snapshots kept per process
 constexpr uint32_t FMAX = 12;            // frame stack depth
 constexpr uint32_t RDMAX = 16;           // ready results per frame
@@ -69,10 +68,10 @@ enum : uint32_t { M_COLLECT = 0, M_COLLECT_ACK = 1, M_COMMIT = 2, M_CONSENSUS = 
 enum : uint32_t { ST_START = 0, ST_PAYLOAD = 1, ST_COLLECT = 2, ST_COMMIT = 3 };
 enum : uint32_t { PH_IDLE = 0, PH_DFS = 1, PH_TRY = 2, PH_CHECK = 3 };
 
-// dot-table slot (u32 words)
+// dot-table slot (u32 words): fixed header, then (per-launch sizes, Geo)
+// collect deps [K] | value [vmax] | ack deps [n][amax]
 constexpr uint32_t SL_DOT = 0, SL_CLIENT = 1, SL_IDX = 2, SL_KEYS = 3, SL_PST = 4,  // 4,5: per-process state bytes
-    SL_MASKS = 6, SL_CNT = 7, SL_COLLECT = 8, SL_VALUE = SL_COLLECT + KMAX, SL_ACK = SL_VALUE + VMAX,
-    SLOTW = SL_ACK + NMAX * AMAX;
+    SL_MASKS = 6, SL_CNT = 7, SL_COLLECT = 8;
 // per-process state byte: status(2) | buffered commit(1) | accepted(1) | buffered-from(4)
 // SL_MASKS: participants(8) | proposer accepts(8) | committed count(8) | executed count(8)
 // SL_CNT:   value count(8) | collect count(8) | proposer ballot set(1) << 16 | nkeys << 20
@@ -91,8 +90,9 @@ constexpr uint32_t FR_ACT = 0, FR_KIND = 1, FR_DOT = 2, FR_TGT = 3, FR_NEXT = 4,
 
 struct Geo {  // launch-uniform geometry
   uint32_t n, C, K, W, R, L, NP, ncli_keys;
-  uint32_t off_ring, off_rh, off_snap, off_slot, off_kd, off_proc, off_cli, off_frame, off_wl, off_delay,
-      words;
+  uint32_t amax, vmax, sl_value, sl_ack, slotw;  // dot-slot layout (MCollectAck deps <= 2K, value <= K(n+1))
+  uint32_t off_ring, off_rh, off_snap, off_gcb, off_gck, off_slot, off_kd, off_proc, off_cli, off_frame, off_wl,
+      off_delay, words;
 };
 
 struct SimArgs {
@@ -176,7 +176,7 @@ struct Sim {
   uint32_t err = 0;
   uint32_t now = 0;       // ms
   uint32_t seq = 0;       // insertion counter (C3)
-  uint64_t events = 0, trace = 0;
+  uint64_t events = 0, trace = 0, deps_total = 0;
   uint32_t clients_done = 0;
   bool done = false, in_extra = false;
   uint32_t final_ms = 0;
@@ -203,7 +203,12 @@ struct Sim {
   __device__ __forceinline__ uint32_t slot_of(uint32_t d) const {
     return ((d >> FX_SEQ_BITS) - 1u) * g.W + (d & (g.W - 1u));
   }
-  __device__ __forceinline__ uint32_t& S(uint32_t sl, uint32_t w) { return lds[g.off_slot + sl * SLOTW + w]; }
+  __device__ __forceinline__ uint32_t& S(uint32_t sl, uint32_t w) { return lds[g.off_slot + sl * g.slotw + w]; }
+  // GC deliveries p -> q: base insertion seq of p's tick k (the tick's sends
+  // take consecutive seqs in ascending target order) and the next tick index
+  // link (p, q) delivers
+  __device__ __forceinline__ uint32_t& gcb(uint32_t p, uint32_t k) { return lds[g.off_gcb + p * RS + (k & (RS - 1u))]; }
+  __device__ __forceinline__ uint32_t& gck(uint32_t pl) { return lds[g.off_gck + pl]; }
   __device__ __forceinline__ uint32_t& kd(uint32_t p, uint32_t key) { return lds[g.off_kd + p * g.ncli_keys + key]; }
   __device__ __forceinline__ uint32_t& P(uint32_t p, uint32_t w) { return lds[g.off_proc + p * PRW + w]; }
   __device__ __forceinline__ uint32_t& CL(uint32_t c, uint32_t w) { return lds[g.off_cli + c * CLW + w]; }
@@ -230,10 +235,11 @@ struct Sim {
   __device__ __forceinline__ uint32_t link_p(uint32_t p, uint32_t q) const {  // 0-based p != q
     return p * (g.n - 1) + (q < p ? q : q - 1);
   }
-  __device__ __forceinline__ uint32_t link_g(uint32_t p) const { return g.NP + p; }
-  __device__ __forceinline__ uint32_t link_e(uint32_t p) const { return g.NP + g.n + p; }
-  __device__ __forceinline__ uint32_t link_s(uint32_t c) const { return g.NP + 2 * g.n + c; }
-  __device__ __forceinline__ uint32_t link_r(uint32_t c) const { return g.NP + 2 * g.n + g.C + c; }
+  __device__ __forceinline__ uint32_t link_gc(uint32_t p, uint32_t q) const { return g.NP + link_p(p, q); }
+  __device__ __forceinline__ uint32_t link_g(uint32_t p) const { return 2 * g.NP + p; }
+  __device__ __forceinline__ uint32_t link_e(uint32_t p) const { return 2 * g.NP + g.n + p; }
+  __device__ __forceinline__ uint32_t link_s(uint32_t c) const { return 2 * g.NP + 2 * g.n + c; }
+  __device__ __forceinline__ uint32_t link_r(uint32_t c) const { return 2 * g.NP + 2 * g.n + g.C + c; }
 
   __device__ __forceinline__ void head_set(uint32_t link, uint32_t t, uint32_t s) {
     const uint32_t ln = link & 63u, h = link >> 6;
@@ -286,7 +292,7 @@ struct Sim {
   __device__ __forceinline__ uint32_t gen_keys(uint32_t cid, uint32_t idx, uint32_t& nk) {
     uint32_t k0 = 0xFFFFu, k1 = 0xFFFFu;
     nk = 0;
-    for (uint32_t draw = 0; nk < g.K && draw < 64; ++draw) {
+    for (uint32_t draw = 0; nk < g.K && draw < 65536u; ++draw) {  // gen_unique_keys draws until distinct
       bool conflict;
       if (conflict_ == 0) conflict = false;
       else if (conflict_ >= 100) conflict = true;
@@ -370,7 +376,7 @@ struct Sim {
     uint32_t nk = 0;
     const uint32_t keys = gen_keys(c + 1, idx, nk);
     // fresh slot
-    if (lid < SLOTW) S(sl, lid) = 0;
+    if (lid < g.slotw) S(sl, lid) = 0;
     put(S(sl, SL_DOT), dot);
     put(S(sl, SL_CLIENT), c);
     put(S(sl, SL_IDX), idx);
@@ -409,10 +415,10 @@ struct Sim {
     } else {
       nd = add_cmd(p, dot, uni(S(sl, SL_KEYS)), nk, colv, ncol, depv);
     }
-    if (nd > AMAX) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (nd > g.amax) { err = FX_ERR_SIM_CAPACITY; return; }
     set_pst(sl, p, (ps & ~3u) | ST_COLLECT);
     // the ack's deps travel in the slot: ack deps of p
-    if (lid < AMAX) S(sl, SL_ACK + p * AMAX + lid) = lid < nd ? depv : 0u;
+    if (lid < g.amax) S(sl, g.sl_ack + p * g.amax + lid) = lid < nd ? depv : 0u;
     if (protocol == FX_PROTOCOL_EPAXOS && from_self) return;  // epaxos.rs:290-300
     act_send(M_COLLECT_ACK, dot, 1u << from);
   }
@@ -429,10 +435,10 @@ struct Sim {
     if (pop32(part) != fq_eff) return;
     // QuorumDeps: union + per-dep report counts over the participants' acks.
     // lane j of a participant block holds one reported dep: lanes
-    // [q*AMAX, q*AMAX + AMAX) for process q (<= 32 lanes)
-    const uint32_t q = lid / AMAX, j = lid % AMAX;
+    // [q*amax, q*amax + amax) for process q (<= 32 lanes)
+    const uint32_t q = lid / g.amax, j = lid % g.amax;
     uint32_t v = 0;
-    if (lid < NMAX * AMAX && q < n && ((part >> q) & 1u)) v = S(sl, SL_ACK + q * AMAX + j);
+    if (q < n && ((part >> q) & 1u)) v = S(sl, g.sl_ack + q * g.amax + j);
     const bool valid = v != 0;
     // count and first occurrence
     uint32_t cnt = 0;
@@ -448,7 +454,7 @@ struct Sim {
     }
     const uint64_t um = bal(first);  // one lane per distinct dep
     const uint32_t nu = pop64(um);
-    if (nu > VMAX) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (nu > g.vmax) { err = FX_ERR_SIM_CAPACITY; return; }
     bool fast;
     if (protocol == FX_PROTOCOL_ATLAS) {
       // threshold = |quorum| - minority (atlas.rs:361-368)
@@ -461,7 +467,7 @@ struct Sim {
     // value = union, ascending
     uint32_t rank = 0;
     for (uint64_t m = um; m; m &= m - 1) rank += rl(v, ctz64(m)) < v ? 1u : 0u;
-    if (first) S(sl, SL_VALUE + rank) = v;
+    if (first) S(sl, g.sl_value + rank) = v;
     const uint32_t c0 = uni(S(sl, SL_CNT));
     put(S(sl, SL_CNT), (c0 & ~0xFFu) | nu | (fast ? 0u : (1u << 16)));  // slow: proposer ballot set
     if (fast) put(P(p, PR_FAST), uni(P(p, PR_FAST)) + 1u);
@@ -570,12 +576,24 @@ struct Sim {
     if (count) put(P(p, PR_STABLE), uni(P(p, PR_STABLE)) + count);
   }
 
-  // periodic GarbageCollection (atlas.rs:699-714): frontier to all but me
+  // periodic GarbageCollection (atlas.rs:699-714): MGarbageCollection with
+  // the committed frontier to all but me.  No handler runs at p in between
+  // (self is not a target), so the n - 1 sends take consecutive insertion
+  // seqs in ascending target order; link (p, q) queues nothing but reads its
+  // deliveries off p's tick ring: tick k reaches q at (k + 1) gc + d(p, q)
+  // with seq base(k) + rank of q.
   __device__ __forceinline__ void h_gc_event(uint32_t p) {
     const uint32_t k = uni(P(p, PR_TICK));
     if (lid < n) snap(p, k, lid) = P(p, PR_GCF + lid);
+    put(gcb(p, k), seq);
     put(P(p, PR_TICK), k + 1u);
-    act_send(M_GC, k, ((1u << n) - 1u) & ~(1u << p));
+    for (uint32_t q = 0, r = 0; q < n; ++q) {
+      if (q == p) continue;
+      const uint32_t pl = link_p(p, q);
+      if (uni(gck(pl)) == k) head_set(g.NP + pl, now + uni(dly(p * g.n + q)), seq + r);
+      ++r;
+    }
+    seq += n - 1u;
   }
 
   __device__ __forceinline__ void dispatch(uint32_t p, uint32_t from, uint32_t kind, uint32_t w2) {
@@ -594,7 +612,7 @@ struct Sim {
   // ===================================================== GraphExecutor
   __device__ __forceinline__ bool mine(uint64_t m) const { return (m & lbit) != 0; }
   __device__ __forceinline__ uint32_t vcount_of(uint32_t d) { return uni(S(slot_of(d), SL_CNT)) & 0xFFu; }
-  __device__ __forceinline__ uint32_t value_at(uint32_t d, uint32_t j) { return uni(S(slot_of(d), SL_VALUE + j)); }
+  __device__ __forceinline__ uint32_t value_at(uint32_t d, uint32_t j) { return uni(S(slot_of(d), g.sl_value + j)); }
 
   __device__ __forceinline__ void x_load(uint32_t p) {
     xp = p;
@@ -866,7 +884,8 @@ struct Sim {
     nwl = 0;
     if (find(d) >= 0) { err = FX_ERR_DOUBLE_INDEX; x_store(); return; }
     const uint32_t vc = vcount_of(d);
-    const uint32_t depj = lid < vc ? S(slot_of(d), SL_VALUE + lid) : 0u;
+    deps_total += vc;
+    const uint32_t depj = lid < vc ? S(slot_of(d), g.sl_value + lid) : 0u;
     const bool keep = lid < vc && depj != d && !contains_v(depj);
     if (!bal(keep)) {  // fast path: a singleton SCC
       emit_one(d, now);
@@ -985,7 +1004,7 @@ struct Sim {
       } else {
         head_set(link, NONE, NONE);
       }
-      note(3, q + 1, p + 1, ((uint64_t)kind << 32) | (kind == M_GC ? 0u : w2));
+      note(3, q + 1, p + 1, ((uint64_t)kind << 32) | w2);
       frame_push();
       dispatch(q, p, kind, w2);
       frame_after_handler(q);
@@ -993,14 +1012,27 @@ struct Sim {
       return;
     }
     uint32_t x = link - g.NP;
+    if (x < g.NP) {  // GC delivery p -> q (MGarbageCollection; its MStable is applied in place)
+      const uint32_t pl = x;
+      const uint32_t p = pl / (g.n - 1u), qi = pl % (g.n - 1u);
+      const uint32_t q = qi < p ? qi : qi + 1u;
+      const uint32_t k = uni(gck(pl));
+      note(3, q + 1, p + 1, (uint64_t)M_GC << 32);
+      h_mgc(q, p, k);
+      put(gck(pl), k + 1u);
+      if (k + 1u < uni(P(p, PR_TICK))) {
+        head_set(link, (k + 2u) * gc_ms + uni(dly(p * g.n + q)), uni(gcb(p, k + 1u)) + qi);
+      } else {
+        head_set(link, NONE, NONE);
+      }
+      return;
+    }
+    x -= g.NP;
     if (x < g.n) {  // G(p): periodic GarbageCollection
       const uint32_t p = x;
       head_set(link, NONE, NONE);
       note(0, p + 1, 0, 0);
-      frame_push();
       h_gc_event(p);
-      frame_after_handler(p);
-      frames_run(p);
       schedule_timer(link_g(p), gc_ms);  // next periodic event (runner.rs:328-329)
       return;
     }
@@ -1051,34 +1083,40 @@ struct Sim {
     }
   }
 
-  // wave-wide min over the link heads: (time, seq) lexicographic
+  // wave-wide min over the link heads, (time, seq) lexicographic: each lane's
+  // local minimum, then two DPP min-scans (time, then seq among the lanes at
+  // that time); the link is unique because insertion seqs are
+  __device__ __forceinline__ static uint32_t dpp_min(uint32_t v) {
+    // inclusive min-scan over the wavefront (row_shr 1/2/4/8, row_bcast 15/31);
+    // lane 63 ends with the minimum
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x111, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x112, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x114, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x118, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x142, 0xA, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x143, 0xC, 0xF, false));
+    return rl(v, 63);
+  }
   __device__ __forceinline__ uint32_t pop_min(uint32_t& t_out) {
-    uint64_t best = ~0ull;
-    uint32_t bl = NONE;
+    uint32_t bt = ht[0], bs = hs[0], bk = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < HMAX; ++k) {
-      const uint64_t key = ((uint64_t)ht[k] << 32) | hs[k];
-      if (key < best) {
-        best = key;
-        bl = k * 64u + lid;
-      }
+    for (uint32_t k = 1; k < HMAX; ++k) {
+      const bool lt = ht[k] < bt || (ht[k] == bt && hs[k] < bs);
+      bt = lt ? ht[k] : bt;
+      bs = lt ? hs[k] : bs;
+      bk = lt ? k : bk;
     }
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-      const uint32_t bh = (uint32_t)__shfl_xor((int)(uint32_t)(best >> 32), (int)o, 64);
-      const uint32_t blo = (uint32_t)__shfl_xor((int)(uint32_t)best, (int)o, 64);
-      const uint32_t ol = (uint32_t)__shfl_xor((int)bl, (int)o, 64);
-      const uint64_t ob = ((uint64_t)bh << 32) | blo;
-      if (ob < best || (ob == best && ol < bl)) {
-        best = ob;
-        bl = ol;
-      }
-    }
-    t_out = uni((uint32_t)(best >> 32));
-    return uni(bl);
+    const uint32_t tmin = dpp_min(bt);
+    const uint32_t smin = dpp_min(bt == tmin ? bs : NONE);
+    t_out = tmin;
+    if (tmin == NONE) return NONE;
+    const uint64_t w = bal(bt == tmin && bs == smin);
+    const uint32_t l = ctz64(w);
+    return rl(bk, l) * 64u + l;
   }
 };
 
-__global__ __launch_bounds__(64) void k_sim(SimArgs a) {
+__global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
@@ -1214,6 +1252,7 @@ __global__ __launch_bounds__(64) void k_sim(SimArgs a) {
       st[FX_SIM_STAT_END_MS] = s.now;
       st[FX_SIM_STAT_TRACE] = s.trace;
       st[FX_SIM_STAT_SEQ] = s.seq;
+      st[FX_SIM_STAT_DEPS] = s.deps_total;
     }
   }
   if (s.lid == 0) a.err[inst] = s.err;
@@ -1234,14 +1273,25 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   g.W = wslots;
   g.R = ring;
   g.NP = n * (n - 1);
-  g.L = g.NP + 2 * n + 2 * C;
+  g.L = 2 * g.NP + 2 * n + 2 * C;
   if (g.L > 64 * HMAX) return false;
   g.ncli_keys = sp.pool_size + C + 1;
+  // an MCollectAck carries the coordinator's deps plus the replica's latest
+  // write per key (<= 2K); a committed value is their union over the fast
+  // quorum (<= K (n + 1): the coordinator's past plus one latest per member)
+  g.amax = 2 * g.K;
+  g.vmax = std::min<uint32_t>(VMAX, g.K * (n + 1));
+  g.sl_value = SL_COLLECT + g.K;
+  g.sl_ack = g.sl_value + g.vmax;
+  g.slotw = g.sl_ack + n * g.amax;
+  if (n * g.amax > 64 || g.slotw > 64) return false;
   uint32_t o = 0;
   g.off_ring = o; o += g.NP * g.R * 3;
   g.off_rh = o; o += g.NP;
   g.off_snap = o; o += n * RS * n;
-  g.off_slot = o; o += n * g.W * SLOTW;
+  g.off_gcb = o; o += n * RS;
+  g.off_gck = o; o += g.NP;
+  g.off_slot = o; o += n * g.W * g.slotw;
   g.off_kd = o; o += n * g.ncli_keys;
   g.off_proc = o; o += n * PRW;
   g.off_cli = o; o += C * CLW;
@@ -1271,7 +1321,7 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   if (b->instances == 0) return FX_OK;
   int dc = 0;
   if (hipGetDeviceCount(&dc) != hipSuccess || dc <= 0) return FX_ERR_NO_DEVICE;
-  const uint32_t ring = b->ring_entries ? b->ring_entries : 32u;
+  const uint32_t ring = b->ring_entries ? b->ring_entries : 16u;
   const uint32_t W = b->dot_slots ? b->dot_slots : 8u;
   if ((ring & (ring - 1)) || ring > 4096 || (W & (W - 1)) || W > 256) return FX_ERR_INVALID_ARG;
   const fx_sim_spec& s0 = b->host_specs[0];
@@ -1287,6 +1337,8 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
     if (s.keys_per_command < 1 || s.keys_per_command > KMAX || s.pool_size < 1) return FX_ERR_INVALID_ARG;
     if (s.f > s.n / 2) return FX_ERR_INVALID_ARG;
     if (s.keys_per_command == 2 && s.conflict_rate >= 100) return FX_ERR_INVALID_ARG;  // workload.rs:49-51
+    // two distinct keys from {client key} U pool: the reference's draw loop never ends
+    if (s.keys_per_command == 2 && s.conflict_rate == 0) return FX_ERR_INVALID_ARG;
     for (uint32_t p = 0; p < s.n; ++p)
       if (s.process_regions[p] >= b->planet_regions) return FX_ERR_INVALID_ARG;
     for (uint32_t r = 0; r < s.num_client_regions; ++r)

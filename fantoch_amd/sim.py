@@ -121,7 +121,7 @@ class Result:
 
 
 def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bins=256,
-        delay_bins=8192, ring_entries=32, dot_slots=8, max_events=0, flags=0, stream=None):
+        delay_bins=8192, ring_entries=16, dot_slots=8, max_events=0, flags=0, stream=None):
     """Simulates every instance of `specs` on the GPU; returns a Result."""
     lib = _lib.load()
     planet = planet or Planet()

@@ -373,6 +373,7 @@ typedef struct fx_sim_batch {
 #define FX_SIM_STAT_END_MS 25u  /* simulation time when the run stopped            */
 #define FX_SIM_STAT_TRACE 26u   /* hash of the processed action sequence (debug)   */
 #define FX_SIM_STAT_SEQ 27u     /* schedule insertions                             */
+#define FX_SIM_STAT_DEPS 28u    /* deps of every executor Add (sum over processes) */
 #define FX_SIM_STATS 32u
 
 typedef struct fx_sim_output {  /* device buffers; NULL where not wanted */

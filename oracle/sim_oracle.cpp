@@ -778,9 +778,8 @@ bool gen_cmd(const fx_sim_spec& spec, uint64_t client, uint64_t idx, Cmd& cmd) {
     } else {  // the client's own key
       key = spec.pool_size + (uint32_t)client;
     }
-    ++draw;
-    if (draw >= 64 && keys.size() + (std::find(keys.begin(), keys.end(), key) == keys.end()) != spec.keys_per_command)
-      return false;
+    ++draw;  // the reference draws until it has keys_per_command distinct keys
+    if (draw > 65536u) return false;
     if (std::find(keys.begin(), keys.end(), key) == keys.end()) keys.push_back(key);
   }
   std::sort(keys.begin(), keys.end());  // C11

@@ -112,7 +112,7 @@ def test_two_clients_per_region_two_keys():
     regs = pl.ids(S.GCP5[:5])
     specs = [S.spec(S.EPAXOS, 5, 2, regs, regs, clients_per_region=2, commands_per_client=60,
                     keys_per_command=2, conflict_rate=c, seed=3, instance=i)
-             for i, c in enumerate([0, 50, 90])]
+             for i, c in enumerate([10, 50, 90])]
     run_and_compare(specs, dot_slots=16)
 
 
