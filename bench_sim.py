@@ -275,7 +275,7 @@ def cpu_baseline_sim(args, specs, rates, executed, executed_len, st, lat_hist, n
     executed_cpu = sum(int(sum(len(e) for e in r["executed"])) for r in res)
     # parity on the sample
     el = executed_len.view(len(specs), n).cpu().numpy()
-    stc = st.cpu().numpy()
+    stc = st.cpu().numpy().view(np.uint64)
     ok = True
     for j, i in enumerate(pick):
         r = res[j]

@@ -64,7 +64,8 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 
 // message kinds (numbering of the oracle's trace, sim_oracle.cpp MK)
 enum : uint32_t { M_COLLECT = 0, M_COLLECT_ACK = 1, M_COMMIT = 2, M_CONSENSUS = 3, M_CONSENSUS_ACK = 4,
-                  M_COMMIT_DOT = 5, M_GC = 6, M_STABLE = 7 };
+                  M_COMMIT_DOT = 5, M_GC = 6, M_STABLE = 7,
+                  M_SUBMIT = 8 /* SubmitToProc (handle_submit_to_proc), not a message */ };
 enum : uint32_t { ST_START = 0, ST_PAYLOAD = 1, ST_COLLECT = 2, ST_COMMIT = 3 };
 enum : uint32_t { PH_IDLE = 0, PH_DFS = 1, PH_TRY = 2, PH_CHECK = 3 };
 
@@ -183,6 +184,9 @@ struct Sim {
 
   // link heads owned by this lane: time, seq (time NONE = empty)
   uint32_t ht[HMAX], hs[HMAX];
+  // GC state (see h_mcommitdot): lane 8 p + s; gckv: lane pl = next tick of GC link pl
+  uint32_t gf = 0, gw = 0, gprev = 0, gseen = 0, gtick = 0, gstable = 0, gckv = 0;
+  uint32_t goth[NMAX];
 
   // executor state of every process (lane-owned slot l / clock of source l + 1)
   uint32_t xdot[NMAX], xrec[NMAX], xwait[NMAX], xtl[NMAX], xfr[NMAX], xcf[NMAX], xcw[NMAX];
@@ -526,54 +530,60 @@ struct Sim {
     }
   }
 
-  // MCommitDot: VClockGCTrack::add_to_clock (gc/clock.rs:43-48), AEClock with
-  // a 32-bit exception window per source
+  // ------------------------------------------------------------------ GC
+  // VClockGCTrack state (gc/clock.rs:21-138) lives in registers, lane
+  // 8 p + s holding process p's view of source s + 1: the committed clock
+  // (AEClock: frontier + 32-bit exception window), the join of every other
+  // process's reported frontier (goth[from]), the previous stable frontier;
+  // p's tick count, reporter mask and Stable count are replicated over p's
+  // lanes.  GC handlers are then lane-parallel VALU work.
+  __device__ __forceinline__ bool gc_lane(uint32_t p) const { return (lid >> 3) == p && (lid & 7u) < n; }
+
+  // MCommitDot: add_to_clock (gc/clock.rs:43-48)
   __device__ __forceinline__ void h_mcommitdot(uint32_t p, uint32_t dot) {
     const uint32_t si = (dot >> FX_SEQ_BITS) - 1u, sq = dot & FX_SEQ_MASK;
-    uint32_t fr = uni(P(p, PR_GCF + si)), w = uni(P(p, PR_GCW + si));
-    if (sq <= fr) return;
-    const uint32_t off = sq - fr - 1u;
-    if (off >= 32u) { err = FX_ERR_SIM_CAPACITY; return; }
-    if (off) {
-      w |= 1u << off;
-    } else {
-      const uint32_t win = w >> 1;
-      const uint32_t ones = __builtin_ctz(~win);
-      fr = fr + 1 + ones;
-      w = win >> ones;
+    bool bad = false;
+    if (lid == p * 8u + si && sq > gf) {
+      const uint32_t off = sq - gf - 1u;
+      if (off >= 32u) {
+        bad = true;
+      } else if (off) {
+        gw |= 1u << off;
+      } else {
+        const uint32_t win = gw >> 1;
+        const uint32_t ones = __builtin_ctz(~win);
+        gf = gf + 1 + ones;
+        gw = win >> ones;
+      }
     }
-    put(P(p, PR_GCF + si), fr);
-    put(P(p, PR_GCW + si), w);
+    if (bal(bad)) err = FX_ERR_SIM_CAPACITY;
   }
 
   // MGarbageCollection (atlas.rs:657-679) + the MStable it forwards
-  // (atlas.rs:681-697): stable() over MaxSet clocks (gc/clock.rs:74-137)
-  __device__ __forceinline__ void h_mgc(uint32_t p, uint32_t from, uint32_t k) {
-    // update_clock_of(from, snapshot k of from); the snapshot must still be
-    // in from's ring of RS ticks
-    if (uni(P(from, PR_TICK)) - k > RS) { err = FX_ERR_SIM_CAPACITY; return; }
-    if (lid < n) {
-      const uint32_t sv = snap(from, k, lid);
-      uint32_t& o = P(p, PR_OTH + from * NMAX + lid);
-      o = max(o, sv);
+  // (atlas.rs:681-697): update_clock_of(from, snapshot k of from), then
+  // stable() over MaxSet clocks (gc/clock.rs:74-137); the Stable count is
+  // the size of the newly stable ranges (every process holds info for every
+  // dot it committed, so cmds.gc removes all of them)
+  __device__ __forceinline__ void h_mgc(uint32_t q, uint32_t from, uint32_t k) {
+    if (rl(gtick, from * 8u) - k > RS) { err = FX_ERR_SIM_CAPACITY; return; }  // snapshot overwritten
+    const bool mine = gc_lane(q);
+    const uint32_t sv = mine ? snap(from, k, lid & 7u) : 0u;
+    const uint32_t o = max(rsel(goth, from), sv);
+    if (mine) rput(goth, from, o);
+    const uint32_t seen = rl(gseen, q * 8u) | (1u << from);
+    if (mine) gseen = seen;
+    uint32_t cur = 0;
+    if (pop32(seen) == n - 1u) {
+      cur = gf;
+#pragma unroll
+      for (uint32_t f2 = 0; f2 < NMAX; ++f2)
+        if ((seen >> f2) & 1u) cur = min(cur, goth[f2]);
     }
-    const uint32_t seen = uni(P(p, PR_SEEN)) | (1u << from);
-    put(P(p, PR_SEEN), seen);
-    uint32_t count = 0;
-    if (lid < n) {
-      uint32_t cur = 0;
-      if (pop32(seen) == n - 1u) {
-        cur = P(p, PR_GCF + lid);
-        for (uint32_t q = 0; q < n; ++q)
-          if ((seen >> q) & 1u) cur = min(cur, P(p, PR_OTH + q * NMAX + lid));
-      }
-      const uint32_t prev = P(p, PR_PREV + lid);
-      if (cur > prev) count = cur - prev;  // dots prev+1 ..= cur become stable
-      P(p, PR_PREV + lid) = max(cur, prev);
-    }
-    for (uint32_t o = 1; o < 8; o <<= 1) count += (uint32_t)__shfl_xor((int)count, (int)o, 64);
-    count = uni(count);
-    if (count) put(P(p, PR_STABLE), uni(P(p, PR_STABLE)) + count);
+    const uint32_t cnt = cur > gprev ? cur - gprev : 0u;  // dots prev+1 ..= cur become stable
+    if (mine) gprev = max(cur, gprev);
+    uint32_t sum = 0;
+    for (uint32_t s2 = 0; s2 < n; ++s2) sum += rl(cnt, q * 8u + s2);
+    if (mine) gstable += sum;
   }
 
   // periodic GarbageCollection (atlas.rs:699-714): MGarbageCollection with
@@ -583,30 +593,17 @@ struct Sim {
   // deliveries off p's tick ring: tick k reaches q at (k + 1) gc + d(p, q)
   // with seq base(k) + rank of q.
   __device__ __forceinline__ void h_gc_event(uint32_t p) {
-    const uint32_t k = uni(P(p, PR_TICK));
-    if (lid < n) snap(p, k, lid) = P(p, PR_GCF + lid);
+    const uint32_t k = rl(gtick, p * 8u);
+    if (gc_lane(p)) snap(p, k, lid & 7u) = gf;
+    if ((lid >> 3) == p) gtick = k + 1u;
     put(gcb(p, k), seq);
-    put(P(p, PR_TICK), k + 1u);
     for (uint32_t q = 0, r = 0; q < n; ++q) {
       if (q == p) continue;
       const uint32_t pl = link_p(p, q);
-      if (uni(gck(pl)) == k) head_set(g.NP + pl, now + uni(dly(p * g.n + q)), seq + r);
+      if (rl(gckv, pl) == k) head_set(g.NP + pl, now + uni(dly(p * g.n + q)), seq + r);
       ++r;
     }
     seq += n - 1u;
-  }
-
-  __device__ __forceinline__ void dispatch(uint32_t p, uint32_t from, uint32_t kind, uint32_t w2) {
-    switch (kind) {
-      case M_COLLECT: h_mcollect(p, from, w2); break;
-      case M_COLLECT_ACK: h_mcollectack(p, from, w2); break;
-      case M_COMMIT: h_mcommit(p, from, w2); break;
-      case M_CONSENSUS: h_mconsensus(p, from, w2); break;
-      case M_CONSENSUS_ACK: h_mconsensusack(p, from, w2); break;
-      case M_COMMIT_DOT: h_mcommitdot(p, w2); break;
-      case M_GC: h_mgc(p, from, w2); break;
-      default: err = FX_ERR_INVALID_ARG;
-    }
   }
 
   // ===================================================== GraphExecutor
@@ -909,8 +906,6 @@ struct Sim {
   }
 
   // =========================================== send_to_processes_and_executors
-  // push a frame for process p and run the handler (handle_send_to_proc /
-  // handle_submit_to_proc / handle_periodic_process_event), then the executor
   __device__ __forceinline__ void frame_push() {
     if (nfrm >= FMAX) { err = FX_ERR_SIM_CAPACITY; return; }
     const uint32_t fi = nfrm++;
@@ -919,51 +914,70 @@ struct Sim {
     put(FR(fi, FR_NREADY), 0);
     xinfo = 0;
   }
-  __device__ __forceinline__ void frame_after_handler(uint32_t p) {
-    if (xinfo && !err) {  // to_executors (<= 1 per handler), LIFO
-      const uint32_t d = xinfo;
-      xinfo = 0;
-      x_add(p, d);
-    }
-  }
 
-  // runs the frame stack of process p to completion (runner.rs:395-488)
-  __device__ __forceinline__ void frames_run(uint32_t p) {
+  // handle_send_to_proc(from, p, msg) / handle_submit_to_proc, each followed
+  // by send_to_processes_and_executors(p) (runner.rs:351-377, 395-488), with
+  // every self-delivery they cause, in the reference's recursion order.  One
+  // call site for the handlers and one for the executor keep the inlined
+  // kernel small: the loop either runs the pending handler (pushing its frame
+  // and running the executor on what it committed), or advances the top
+  // frame's action, or schedules the frame's ready results and pops it.
+  __device__ __forceinline__ void run_handlers(uint32_t p, uint32_t from, uint32_t kind, uint32_t w2) {
+    bool pend = true;
     uint32_t guard = 0;
-    while (nfrm > 0 && !err) {
+    while (!err) {
       if (++guard > 4096u) { err = FX_ERR_SIM_CAPACITY; return; }
+      if (pend) {
+        pend = false;
+        frame_push();
+        if (err) return;
+        switch (kind) {
+          case M_SUBMIT: h_submit(p, w2); break;
+          case M_COLLECT: h_mcollect(p, from, w2); break;
+          case M_COLLECT_ACK: h_mcollectack(p, from, w2); break;
+          case M_COMMIT: h_mcommit(p, from, w2); break;
+          case M_CONSENSUS: h_mconsensus(p, from, w2); break;
+          case M_CONSENSUS_ACK: h_mconsensusack(p, from, w2); break;
+          case M_COMMIT_DOT: h_mcommitdot(p, w2); break;
+          default: err = FX_ERR_INVALID_ARG;
+        }
+        if (xinfo && !err) {  // to_executors (<= 1 per handler), LIFO
+          const uint32_t d = xinfo;
+          xinfo = 0;
+          x_add(p, d);
+        }
+        continue;
+      }
+      if (nfrm == 0) return;
       const uint32_t fi = nfrm - 1;
       const uint32_t act = uni(FR(fi, FR_ACT));
       if (act == 2) {  // ToForward: deliver to self now
         put(FR(fi, FR_ACT), 0);
-        const uint32_t kind = uni(FR(fi, FR_KIND)), dot = uni(FR(fi, FR_DOT));
-        frame_push();
-        if (err) return;
-        dispatch(p, p, kind, dot);
-        frame_after_handler(p);
+        from = p;
+        kind = uni(FR(fi, FR_KIND));
+        w2 = uni(FR(fi, FR_DOT));
+        pend = true;
         continue;
       }
       if (act == 1) {  // ToSend: targets ascending (C4), self recurses in place
         const uint32_t tgt = uni(FR(fi, FR_TGT));
-        const uint32_t kind = uni(FR(fi, FR_KIND)), dot = uni(FR(fi, FR_DOT));
+        const uint32_t k2 = uni(FR(fi, FR_KIND)), dot = uni(FR(fi, FR_DOT));
         uint32_t nx = uni(FR(fi, FR_NEXT));
-        bool recursed = false;
         while (nx < n) {
           const uint32_t to = nx++;
           if (!((tgt >> to) & 1u)) continue;
           if (to == p) {
             put(FR(fi, FR_NEXT), nx);
-            frame_push();
-            if (err) return;
-            dispatch(p, p, kind, dot);
-            frame_after_handler(p);
-            recursed = true;
+            from = p;
+            kind = k2;
+            w2 = dot;
+            pend = true;
             break;
           }
-          send_p(p, to, kind, dot);
+          send_p(p, to, k2, dot);
           if (err) return;
         }
-        if (recursed) continue;
+        if (pend) continue;
         put(FR(fi, FR_ACT), 0);
       }
       // ready results -> schedule_to_client (runner.rs:434-440)
@@ -1005,10 +1019,7 @@ struct Sim {
         head_set(link, NONE, NONE);
       }
       note(3, q + 1, p + 1, ((uint64_t)kind << 32) | w2);
-      frame_push();
-      dispatch(q, p, kind, w2);
-      frame_after_handler(q);
-      frames_run(q);
+      run_handlers(q, p, kind, w2);
       return;
     }
     uint32_t x = link - g.NP;
@@ -1016,11 +1027,11 @@ struct Sim {
       const uint32_t pl = x;
       const uint32_t p = pl / (g.n - 1u), qi = pl % (g.n - 1u);
       const uint32_t q = qi < p ? qi : qi + 1u;
-      const uint32_t k = uni(gck(pl));
+      const uint32_t k = rl(gckv, pl);
       note(3, q + 1, p + 1, (uint64_t)M_GC << 32);
       h_mgc(q, p, k);
-      put(gck(pl), k + 1u);
-      if (k + 1u < uni(P(p, PR_TICK))) {
+      if (lid == pl) gckv = k + 1u;
+      if (k + 1u < rl(gtick, p * 8u)) {
         head_set(link, (k + 2u) * gc_ms + uni(dly(p * g.n + q)), uni(gcb(p, k + 1u)) + qi);
       } else {
         head_set(link, NONE, NONE);
@@ -1048,10 +1059,7 @@ struct Sim {
       const uint32_t p = uni(CL(c, CL_PROC));
       note(2, p + 1, c + 1, uni(CL(c, CL_ISSUED)));
       put(CL(c, CL_PENDING), g.K);  // AggregatePending::wait_for: key_count results
-      frame_push();
-      h_submit(p, c);
-      frame_after_handler(p);
-      frames_run(p);
+      run_handlers(p, p, M_SUBMIT, c);
       return;
     }
     x -= g.C;
@@ -1158,6 +1166,8 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
 #pragma unroll
   for (uint32_t k = 0; k < HMAX; ++k) s.ht[k] = s.hs[k] = NONE;
 #pragma unroll
+  for (uint32_t k = 0; k < NMAX; ++k) s.goth[k] = 0;
+#pragma unroll
   for (uint32_t k = 0; k < NMAX; ++k) s.xdot[k] = s.xrec[k] = s.xwait[k] = s.xtl[k] = s.xfr[k] = s.xcf[k] = s.xcw[k] = 0;
   const uint32_t RP = a.RP;
   // process regions, quorums (BaseProcess::discover over
@@ -1245,7 +1255,11 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
       const bool v = s.lid < n;
       st[FX_SIM_STAT_FAST + s.lid] = v ? s.P(s.lid, PR_FAST) : 0u;
       st[FX_SIM_STAT_SLOW + s.lid] = v ? s.P(s.lid, PR_SLOW) : 0u;
-      st[FX_SIM_STAT_STABLE + s.lid] = v ? s.P(s.lid, PR_STABLE) : 0u;
+      st[FX_SIM_STAT_STABLE + s.lid] = 0u;
+    }
+    for (uint32_t p = 0; p < n; ++p) {
+      const uint32_t stb = rl(s.gstable, p * 8u);
+      if (s.lid == 0) st[FX_SIM_STAT_STABLE + p] = stb;
     }
     if (s.lid == 0) {
       st[FX_SIM_STAT_EVENTS] = s.events;
