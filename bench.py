@@ -42,7 +42,7 @@ LAYOUT = {0: "16 lanes per stream", 1: "one lane per stream", 2: "one lane per s
              "for sparse ones, both kernels concurrent"}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", choices=["sim", "executor"], default="sim",
                     help="sim: the batched simulator (BASELINE configs[1], the headline); "
@@ -71,7 +71,7 @@ def parse():
                     help="CPU work budget of the cpu_baseline sample (sim default 15, executor 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", type=str, default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def measured_copy_gbps(torch, dev, nbytes=2 << 30, reps=10):

@@ -56,10 +56,11 @@ constexpr uint32_t NMAX = FX_SIM_MAX_N;  // processes
 constexpr uint32_t CMAX = 32;            // clients per instance
 constexpr uint32_t KMAX = 2;             // keys per command
 constexpr uint32_t VMAX = 16;            // deps of a committed value (per-launch: K (n + 1))
-constexpr uint32_t RS = 32;              // GC frontier snapshots kept per process
+constexpr uint32_t RT = 16;              // GC tick log entries per (process, source)
+constexpr uint32_t RC = 8;               // GC frontier change log entries per (process, source)
 constexpr uint32_t FMAX = 12;            // frame stack depth
 constexpr uint32_t RDMAX = 16;           // ready results per frame
-constexpr uint32_t HMAX = 3;             // link heads per lane (links <= 192)
+constexpr uint32_t HMAX = 2;             // link heads per lane (links <= 128; a template parameter)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 
 // message kinds (numbering of the oracle's trace, sim_oracle.cpp MK)
@@ -78,10 +79,9 @@ constexpr uint32_t SL_DOT = 0, SL_CLIENT = 1, SL_IDX = 2, SL_KEYS = 3, SL_PST = 
 // SL_CNT:   value count(8) | collect count(8) | proposer ballot set(1) << 16 | nkeys << 20
 
 // per-process words
-constexpr uint32_t PR_SEQ = 0, PR_FAST = 1, PR_SLOW = 2, PR_STABLE = 3, PR_EXEC = 4, PR_OCC = 5,  // 5,6
+constexpr uint32_t PR_SEQ = 0, PR_FAST = 1, PR_SLOW = 2, PR_EXEC = 4, PR_OCC = 5,  // 5,6
     PR_WMASK = 7,                                                                                // 7,8
-    PR_EPOCH = 9, PR_TICK = 10, PR_GCF = 11, PR_GCW = PR_GCF + NMAX, PR_OTH = PR_GCW + NMAX,
-    PR_SEEN = PR_OTH + NMAX * NMAX, PR_PREV = PR_SEEN + 1, PR_FQ = PR_PREV + NMAX, PR_WQ = PR_FQ + 1,
+    PR_EPOCH = 9, PR_FQ = 10, PR_WQ = PR_FQ + 1,
     PR_REGION = PR_WQ + 1, PRW = PR_REGION + 1;
 // per-client words
 constexpr uint32_t CL_PROC = 0, CL_ISSUED = 1, CL_START = 2, CL_PENDING = 3, CL_REGION = 4, CLW = 5;
@@ -92,7 +92,7 @@ constexpr uint32_t FR_ACT = 0, FR_KIND = 1, FR_DOT = 2, FR_TGT = 3, FR_NEXT = 4,
 struct Geo {  // launch-uniform geometry
   uint32_t n, C, K, W, R, L, NP, ncli_keys;
   uint32_t amax, vmax, sl_value, sl_ack, slotw;  // dot-slot layout (MCollectAck deps <= 2K, value <= K(n+1))
-  uint32_t off_ring, off_rh, off_snap, off_gcb, off_gck, off_slot, off_kd, off_proc, off_cli, off_frame, off_wl,
+  uint32_t off_ring, off_rh, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_proc, off_cli, off_frame, off_wl,
       off_delay, words;
 };
 
@@ -162,6 +162,7 @@ __device__ __forceinline__ uint32_t tep(uint32_t t) { return t >> 14; }
 __device__ __forceinline__ uint32_t tmk(uint32_t id, uint32_t low, uint32_t ep) { return id | (low << 7) | (ep << 14); }
 constexpr uint32_t EPOCH_MAX = 0xFFFFu;
 
+template <uint32_t HM>
 struct Sim {
   // ---------------------------------------------------------------- context
   uint32_t lid;
@@ -183,10 +184,10 @@ struct Sim {
   uint32_t final_ms = 0;
 
   // link heads owned by this lane: time, seq (time NONE = empty)
-  uint32_t ht[HMAX], hs[HMAX];
-  // GC state (see h_mcommitdot): lane 8 p + s; gckv: lane pl = next tick of GC link pl
-  uint32_t gf = 0, gw = 0, gprev = 0, gseen = 0, gtick = 0, gstable = 0, gckv = 0;
-  uint32_t goth[NMAX];
+  uint32_t ht[HM], hs[HM];
+  // GC state of lane 8 p + s (see h_mcommitdot): committed frontier + window
+  // of source s + 1 at process p, tick-log and change-log counters
+  uint32_t gf = 0, gw = 0, gnt = 0, glk = 0, gkm = 0, gnc = 0;
 
   // executor state of every process (lane-owned slot l / clock of source l + 1)
   uint32_t xdot[NMAX], xrec[NMAX], xwait[NMAX], xtl[NMAX], xfr[NMAX], xcf[NMAX], xcw[NMAX];
@@ -201,9 +202,11 @@ struct Sim {
     return lds[g.off_ring + (link * g.R + e) * 3 + w];
   }
   __device__ __forceinline__ uint32_t& rh(uint32_t link) { return lds[g.off_rh + link]; }  // head | tail << 16
-  __device__ __forceinline__ uint32_t& snap(uint32_t p, uint32_t k, uint32_t s) {
-    return lds[g.off_snap + (p * RS + (k & (RS - 1))) * g.n + s];
-  }
+  // GC logs of (process p, source s): tick log entry i = (tick count, frontier
+  // before the change), change log entry i = (time, frontier after)
+  __device__ __forceinline__ uint32_t* gct(uint32_t p, uint32_t s) { return &lds[g.off_gct + (p * g.n + s) * RT * 2]; }
+  __device__ __forceinline__ uint32_t* gcc(uint32_t p, uint32_t s) { return &lds[g.off_gcc + (p * g.n + s) * RC * 2]; }
+  __device__ __forceinline__ uint32_t* gcr(uint32_t p, uint32_t s) { return &lds[g.off_gcr + (p * g.n + s) * 4]; }
   __device__ __forceinline__ uint32_t slot_of(uint32_t d) const {
     return ((d >> FX_SEQ_BITS) - 1u) * g.W + (d & (g.W - 1u));
   }
@@ -211,8 +214,6 @@ struct Sim {
   // GC deliveries p -> q: base insertion seq of p's tick k (the tick's sends
   // take consecutive seqs in ascending target order) and the next tick index
   // link (p, q) delivers
-  __device__ __forceinline__ uint32_t& gcb(uint32_t p, uint32_t k) { return lds[g.off_gcb + p * RS + (k & (RS - 1u))]; }
-  __device__ __forceinline__ uint32_t& gck(uint32_t pl) { return lds[g.off_gck + pl]; }
   __device__ __forceinline__ uint32_t& kd(uint32_t p, uint32_t key) { return lds[g.off_kd + p * g.ncli_keys + key]; }
   __device__ __forceinline__ uint32_t& P(uint32_t p, uint32_t w) { return lds[g.off_proc + p * PRW + w]; }
   __device__ __forceinline__ uint32_t& CL(uint32_t c, uint32_t w) { return lds[g.off_cli + c * CLW + w]; }
@@ -239,17 +240,15 @@ struct Sim {
   __device__ __forceinline__ uint32_t link_p(uint32_t p, uint32_t q) const {  // 0-based p != q
     return p * (g.n - 1) + (q < p ? q : q - 1);
   }
-  __device__ __forceinline__ uint32_t link_gc(uint32_t p, uint32_t q) const { return g.NP + link_p(p, q); }
-  __device__ __forceinline__ uint32_t link_g(uint32_t p) const { return 2 * g.NP + p; }
-  __device__ __forceinline__ uint32_t link_e(uint32_t p) const { return 2 * g.NP + g.n + p; }
-  __device__ __forceinline__ uint32_t link_s(uint32_t c) const { return 2 * g.NP + 2 * g.n + c; }
-  __device__ __forceinline__ uint32_t link_r(uint32_t c) const { return 2 * g.NP + 2 * g.n + g.C + c; }
+  __device__ __forceinline__ uint32_t link_e(uint32_t p) const { return g.NP + p; }
+  __device__ __forceinline__ uint32_t link_s(uint32_t c) const { return g.NP + g.n + c; }
+  __device__ __forceinline__ uint32_t link_r(uint32_t c) const { return g.NP + g.n + g.C + c; }
 
   __device__ __forceinline__ void head_set(uint32_t link, uint32_t t, uint32_t s) {
     const uint32_t ln = link & 63u, h = link >> 6;
     if (lid == ln) {
 #pragma unroll
-      for (uint32_t k = 0; k < HMAX; ++k)
+      for (uint32_t k = 0; k < HM; ++k)
         if (h == k) {
           ht[k] = t;
           hs[k] = s;
@@ -531,12 +530,23 @@ struct Sim {
   }
 
   // ------------------------------------------------------------------ GC
-  // VClockGCTrack state (gc/clock.rs:21-138) lives in registers, lane
-  // 8 p + s holding process p's view of source s + 1: the committed clock
-  // (AEClock: frontier + 32-bit exception window), the join of every other
-  // process's reported frontier (goth[from]), the previous stable frontier;
-  // p's tick count, reporter mask and Stable count are replicated over p's
-  // lanes.  GC handlers are then lane-parallel VALU work.
+  // The GC traffic (periodic GarbageCollection, atlas.rs:699-714, and the
+  // MGarbageCollection / MStable it causes, atlas.rs:657-697, gc/clock.rs:
+  // 21-138) only feeds the GC track, which nothing else reads, and under C3 it
+  // follows every other action of its millisecond.  Its only output, the
+  // Stable count, is therefore a function of the committed frontiers'
+  // history, evaluated once at the end (gc_finish) instead of as ~90 % of the
+  // events:
+  //  * tick k of process p (time (k + 1) gc) reports p's committed frontier
+  //    as of that millisecond; it reaches q at (k + 1) gc + d(p, q);
+  //  * every reported frontier only grows and q's own frontier only grows, so
+  //    q's Stable count = sum over sources of min(q's frontier at its last
+  //    delivery, the frontier in the last delivery from each other process),
+  //    or 0 if some process has not reported yet.
+  // Lane 8 p + s keeps the committed clock of source s + 1 at p (AEClock:
+  // frontier + 32-bit exception window) and two logs of its frontier: one
+  // entry per tick interval in which it moved (the value a tick before the
+  // move reports) and the last RC moves with their times.
   __device__ __forceinline__ bool gc_lane(uint32_t p) const { return (lid >> 3) == p && (lid & 7u) < n; }
 
   // MCommitDot: add_to_clock (gc/clock.rs:43-48)
@@ -550,60 +560,129 @@ struct Sim {
       } else if (off) {
         gw |= 1u << off;
       } else {
+        const uint32_t old = gf;
         const uint32_t win = gw >> 1;
         const uint32_t ones = __builtin_ctz(~win);
         gf = gf + 1 + ones;
         gw = win >> ones;
+        if (gc_ms) {
+          const uint32_t kt = now ? (now - 1u) / gc_ms : 0u;  // ticks strictly before now
+          if (gnt == 0 || kt != glk) {
+            uint32_t* tl = gct(p, si);
+            const uint32_t e = gnt & (RT - 1u);
+            if (gnt >= RT) gkm = tl[e * 2];  // newest dropped entry
+            tl[e * 2] = kt;
+            tl[e * 2 + 1] = old;
+            ++gnt;
+            glk = kt;
+          }
+          uint32_t* cl = gcc(p, si);
+          const uint32_t e2 = gnc & (RC - 1u);
+          cl[e2 * 2] = now;
+          cl[e2 * 2 + 1] = gf;
+          ++gnc;
+        }
       }
     }
     if (bal(bad)) err = FX_ERR_SIM_CAPACITY;
   }
 
-  // MGarbageCollection (atlas.rs:657-679) + the MStable it forwards
-  // (atlas.rs:681-697): update_clock_of(from, snapshot k of from), then
-  // stable() over MaxSet clocks (gc/clock.rs:74-137); the Stable count is
-  // the size of the newly stable ranges (every process holds info for every
-  // dot it committed, so cmds.gc removes all of them)
-  __device__ __forceinline__ void h_mgc(uint32_t q, uint32_t from, uint32_t k) {
-    if (rl(gtick, from * 8u) - k > RS) { err = FX_ERR_SIM_CAPACITY; return; }  // snapshot overwritten
-    const bool mine = gc_lane(q);
-    const uint32_t sv = mine ? snap(from, k, lid & 7u) : 0u;
-    const uint32_t o = max(rsel(goth, from), sv);
-    if (mine) rput(goth, from, o);
-    const uint32_t seen = rl(gseen, q * 8u) | (1u << from);
-    if (mine) gseen = seen;
-    uint32_t cur = 0;
-    if (pop32(seen) == n - 1u) {
-      cur = gf;
-#pragma unroll
-      for (uint32_t f2 = 0; f2 < NMAX; ++f2)
-        if ((seen >> f2) & 1u) cur = min(cur, goth[f2]);
+  // frontier of source s at p reported by tick k; false if the log lost it
+  __device__ __forceinline__ bool gc_tick_value(uint32_t p, uint32_t s, uint32_t k, uint32_t& v) {
+    const uint32_t* r = gcr(p, s);
+    const uint32_t nt = r[1], km = r[2];
+    if (nt > RT && k < km) return false;
+    const uint32_t* tl = gct(p, s);
+    const uint32_t cnt = min(nt, RT);
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint32_t e = (nt - cnt + i) & (RT - 1u);
+      if (tl[e * 2] > k) {
+        v = tl[e * 2 + 1];
+        return true;
+      }
     }
-    const uint32_t cnt = cur > gprev ? cur - gprev : 0u;  // dots prev+1 ..= cur become stable
-    if (mine) gprev = max(cur, gprev);
-    uint32_t sum = 0;
-    for (uint32_t s2 = 0; s2 < n; ++s2) sum += rl(cnt, q * 8u + s2);
-    if (mine) gstable += sum;
+    v = r[0];
+    return true;
+  }
+  // frontier of source s at p after every action up to time x
+  __device__ __forceinline__ bool gc_value_at(uint32_t p, uint32_t s, uint32_t x, uint32_t& v) {
+    const uint32_t nc = gcr(p, s)[3];
+    const uint32_t* cl = gcc(p, s);
+    const uint32_t cnt = min(nc, RC);
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const uint32_t e = (nc - 1u - i) & (RC - 1u);
+      if (cl[e * 2] <= x) {
+        v = cl[e * 2 + 1];
+        return true;
+      }
+    }
+    v = 0;
+    return nc <= RC;
   }
 
-  // periodic GarbageCollection (atlas.rs:699-714): MGarbageCollection with
-  // the committed frontier to all but me.  No handler runs at p in between
-  // (self is not a target), so the n - 1 sends take consecutive insertion
-  // seqs in ascending target order; link (p, q) queues nothing but reads its
-  // deliveries off p's tick ring: tick k reaches q at (k + 1) gc + d(p, q)
-  // with seq base(k) + rank of q.
-  __device__ __forceinline__ void h_gc_event(uint32_t p) {
-    const uint32_t k = rl(gtick, p * 8u);
-    if (gc_lane(p)) snap(p, k, lid & 7u) = gf;
-    if ((lid >> 3) == p) gtick = k + 1u;
-    put(gcb(p, k), seq);
-    for (uint32_t q = 0, r = 0; q < n; ++q) {
-      if (q == p) continue;
-      const uint32_t pl = link_p(p, q);
-      if (rl(gckv, pl) == k) head_set(g.NP + pl, now + uni(dly(p * g.n + q)), seq + r);
-      ++r;
+  // first GC action after time x: its time, and (ticks first, then
+  // deliveries by (from, to)) the delivery it is, or NONE for a tick
+  __device__ __forceinline__ uint32_t gc_next_after(uint32_t x, uint32_t& pair) {
+    const uint32_t tick = (x / gc_ms + 1u) * gc_ms;
+    uint32_t tv = NONE;
+    const uint32_t p = lid >> 3, q = lid & 7u;
+    if (p < n && q < n && p != q) {
+      const uint32_t d = dly(p * g.n + q);
+      tv = x < gc_ms + d ? gc_ms + d : ((x - d) / gc_ms + 1u) * gc_ms + d;
     }
-    seq += n - 1u;
+    uint32_t tmin = tv;
+    for (uint32_t o = 1; o < 64; o <<= 1) tmin = min(tmin, (uint32_t)__shfl_xor((int)tmin, (int)o));
+    tmin = uni(tmin);
+    if (tick <= tmin) {
+      pair = NONE;
+      return tick;
+    }
+    pair = ctz64(bal(tv == tmin));
+    return tmin;
+  }
+
+  // Stable counts at the end of the run: the GC actions processed are those
+  // before time tc, plus the delivery `pair` (8 from + to) at tc if the run
+  // stopped on it
+  __device__ __forceinline__ void gc_finish(uint32_t tc, uint32_t pair, unsigned long long* st) {
+    if (gc_lane(lid >> 3)) {
+      uint32_t* r = gcr(lid >> 3, lid & 7u);
+      r[0] = gf;
+      r[1] = gnt;
+      r[2] = gkm;
+      r[3] = gnc;
+    }
+    for (uint32_t q = 0; q < n; ++q) {
+      // lane p: deliveries p -> q processed, m
+      uint32_t m = 0;
+      const bool pl = lid < n && lid != q;
+      if (pl) {
+        const uint32_t d = dly(lid * g.n + q);
+        if (tc > d) m = (tc - d - 1u) / gc_ms;
+        if (pair == lid * 8u + q && tc >= d + gc_ms && (tc - d) % gc_ms == 0) ++m;
+      }
+      uint32_t stable = 0;
+      if (!bal(pl && m == 0)) {
+        uint32_t tl = pl ? m * gc_ms + dly(lid * g.n + q) : 0u;
+        for (uint32_t o = 1; o < 64; o <<= 1) tl = max(tl, (uint32_t)__shfl_xor((int)tl, (int)o));
+        tl = uni(tl);
+        uint32_t cur = 0;
+        bool ok = true;
+        if (lid < n) ok = gc_value_at(q, lid, tl, cur);
+        for (uint32_t p = 0; p < n; ++p) {
+          if (p == q) continue;
+          const uint32_t kl = rl(m, p) - 1u;
+          uint32_t v = 0;
+          if (lid < n) {
+            ok = ok && gc_tick_value(p, lid, kl, v);
+            cur = min(cur, v);
+          }
+        }
+        if (bal(lid < n && !ok)) err = FX_ERR_SIM_CAPACITY;
+        for (uint32_t s2 = 0; s2 < n; ++s2) stable += rl(cur, s2);
+      }
+      if (st && lid == 0) st[FX_SIM_STAT_STABLE + q] = stable;
+    }
   }
 
   // ===================================================== GraphExecutor
@@ -1023,31 +1102,6 @@ struct Sim {
       return;
     }
     uint32_t x = link - g.NP;
-    if (x < g.NP) {  // GC delivery p -> q (MGarbageCollection; its MStable is applied in place)
-      const uint32_t pl = x;
-      const uint32_t p = pl / (g.n - 1u), qi = pl % (g.n - 1u);
-      const uint32_t q = qi < p ? qi : qi + 1u;
-      const uint32_t k = rl(gckv, pl);
-      note(3, q + 1, p + 1, (uint64_t)M_GC << 32);
-      h_mgc(q, p, k);
-      if (lid == pl) gckv = k + 1u;
-      if (k + 1u < rl(gtick, p * 8u)) {
-        head_set(link, (k + 2u) * gc_ms + uni(dly(p * g.n + q)), uni(gcb(p, k + 1u)) + qi);
-      } else {
-        head_set(link, NONE, NONE);
-      }
-      return;
-    }
-    x -= g.NP;
-    if (x < g.n) {  // G(p): periodic GarbageCollection
-      const uint32_t p = x;
-      head_set(link, NONE, NONE);
-      note(0, p + 1, 0, 0);
-      h_gc_event(p);
-      schedule_timer(link_g(p), gc_ms);  // next periodic event (runner.rs:328-329)
-      return;
-    }
-    x -= g.n;
     if (x < g.n) {  // E(p): executed notification (a no-op for the GraphExecutor)
       schedule_timer(link_e(x), en_ms);
       return;
@@ -1108,7 +1162,7 @@ struct Sim {
   __device__ __forceinline__ uint32_t pop_min(uint32_t& t_out) {
     uint32_t bt = ht[0], bs = hs[0], bk = 0;
 #pragma unroll
-    for (uint32_t k = 1; k < HMAX; ++k) {
+    for (uint32_t k = 1; k < HM; ++k) {
       const bool lt = ht[k] < bt || (ht[k] == bt && hs[k] < bs);
       bt = lt ? ht[k] : bt;
       bs = lt ? hs[k] : bs;
@@ -1124,11 +1178,12 @@ struct Sim {
   }
 };
 
+template <uint32_t HM>
 __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
-  Sim s;
+  Sim<HM> s;
   s.lid = threadIdx.x;
   s.lbit = 1ull << s.lid;
   s.A = a;
@@ -1164,9 +1219,7 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
   for (uint32_t i = s.lid; i < a.g.words; i += 64) smem[i] = 0;
   __builtin_amdgcn_s_barrier();
 #pragma unroll
-  for (uint32_t k = 0; k < HMAX; ++k) s.ht[k] = s.hs[k] = NONE;
-#pragma unroll
-  for (uint32_t k = 0; k < NMAX; ++k) s.goth[k] = 0;
+  for (uint32_t k = 0; k < HM; ++k) s.ht[k] = s.hs[k] = NONE;
 #pragma unroll
   for (uint32_t k = 0; k < NMAX; ++k) s.xdot[k] = s.xrec[k] = s.xwait[k] = s.xtl[k] = s.xfr[k] = s.xcf[k] = s.xcw[k] = 0;
   const uint32_t RP = a.RP;
@@ -1217,8 +1270,8 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
   }
   __builtin_amdgcn_s_barrier();
   // periodic events (runner.rs:179-187), then clients (run(), C5 ascending)
-  if (s.gc_ms)
-    for (uint32_t p = 0; p < n; ++p) s.schedule_timer(s.link_g(p), s.gc_ms);
+  // (the periodic GC events are evaluated in gc_finish; their insertion
+  // seqs only shift the numbering, C3)
   const bool sim_en = a.sim_exec_notif || s.has_extra;
   for (uint32_t p = 0; p < n; ++p) {
     if (sim_en) s.schedule_timer(s.link_e(p), s.en_ms);
@@ -1230,6 +1283,7 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
   }
   // ------------------------------------------------------------ loop
   const uint64_t max_events = a.max_events ? a.max_events : 0xFFFFFFFFull;
+  uint32_t gc_pair = NONE;
   while (!s.done && !s.err) {
     uint32_t t = 0;
     const uint32_t link = s.pop_min(t);
@@ -1240,6 +1294,17 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
     if (t < s.now) {
       s.err = FX_ERR_TIME_RANGE;
       break;
+    }
+    if (s.in_extra && t > s.final_ms && s.gc_ms) {
+      // the run stops at the first action after final_ms: a GC action
+      // before t (C3: at t, t's other actions go first) ends it instead
+      uint32_t pair = NONE;
+      const uint32_t tg = s.gc_next_after(s.final_ms, pair);
+      if (tg < t) {
+        s.now = tg;
+        gc_pair = pair;
+        break;
+      }
     }
     s.now = t;
     s.run_event(link);
@@ -1257,10 +1322,7 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
       st[FX_SIM_STAT_SLOW + s.lid] = v ? s.P(s.lid, PR_SLOW) : 0u;
       st[FX_SIM_STAT_STABLE + s.lid] = 0u;
     }
-    for (uint32_t p = 0; p < n; ++p) {
-      const uint32_t stb = rl(s.gstable, p * 8u);
-      if (s.lid == 0) st[FX_SIM_STAT_STABLE + p] = stb;
-    }
+    if (s.gc_ms && !s.err) s.gc_finish(s.now, gc_pair, st);
     if (s.lid == 0) {
       st[FX_SIM_STAT_EVENTS] = s.events;
       st[FX_SIM_STAT_END_MS] = s.now;
@@ -1287,7 +1349,7 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   g.W = wslots;
   g.R = ring;
   g.NP = n * (n - 1);
-  g.L = 2 * g.NP + 2 * n + 2 * C;
+  g.L = g.NP + n + 2 * C;
   if (g.L > 64 * HMAX) return false;
   g.ncli_keys = sp.pool_size + C + 1;
   // an MCollectAck carries the coordinator's deps plus the replica's latest
@@ -1302,9 +1364,9 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   uint32_t o = 0;
   g.off_ring = o; o += g.NP * g.R * 3;
   g.off_rh = o; o += g.NP;
-  g.off_snap = o; o += n * RS * n;
-  g.off_gcb = o; o += n * RS;
-  g.off_gck = o; o += g.NP;
+  g.off_gct = o; o += n * n * RT * 2;
+  g.off_gcc = o; o += n * n * RC * 2;
+  g.off_gcr = o; o += n * n * 4;
   g.off_slot = o; o += n * g.W * g.slotw;
   g.off_kd = o; o += n * g.ncli_keys;
   g.off_proc = o; o += n * PRW;
@@ -1386,10 +1448,15 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   a.err = o->err;
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute((const void*)sim::k_sim, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     configured = true;
   }
-  hipLaunchKernelGGL(sim::k_sim, dim3(b->instances), dim3(64), lds, (hipStream_t)hip_stream, a);
+  // link heads per lane: one when every link fits a lane
+  if (a.g.L <= 64)
+    hipLaunchKernelGGL(sim::k_sim<1>, dim3(b->instances), dim3(64), lds, (hipStream_t)hip_stream, a);
+  else
+    hipLaunchKernelGGL(sim::k_sim<2>, dim3(b->instances), dim3(64), lds, (hipStream_t)hip_stream, a);
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 

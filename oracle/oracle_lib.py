@@ -293,6 +293,21 @@ class _OutBufs:
                 "status": int(o.status), "monitor_hash": self.monitor_hash}
 
 
+def spec_from(s):
+    """Copies a product-side fx_sim_spec (any ctypes struct with the same field
+    names) into the oracle's SimSpec."""
+    o = SimSpec()
+    for name, _ in SimSpec._fields_:
+        v = getattr(s, name)
+        if name in ("process_regions", "client_regions"):
+            arr = getattr(o, name)
+            for i in range(len(v)):
+                arr[i] = v[i]
+        else:
+            setattr(o, name, v)
+    return o
+
+
 def sim_run(spec, exec_cap=None, lat_bins=8192, chain_bins=256, delay_bins=8192,
             planet_dir=PLANET_DIR):
     """Runs one simulated instance (Runner::run) through the C++ oracle."""

@@ -32,7 +32,9 @@
 // Canonicalisation, replacing the reference's
 // unordered iteration and unseeded randomness:
 //   C1/C2  inside the DependencyGraph (graph_oracle.hpp)
-//   C3     Schedule ties are FIFO by insertion (the BinaryHeap compares time only)
+//   C3     Schedule ties (the BinaryHeap compares time only): protocol and client
+//          actions first, FIFO by insertion; then the GC traffic (periodic GC events
+//          by process id, then MGarbageCollection deliveries by (from, to))
 //   C4     a message's targets are visited in ascending process id (HashSet order)
 //   C5     clients start in ascending client id (HashMap order)
 //   C6     every draw of rand::thread_rng is a counter-based hash of
@@ -60,6 +62,7 @@
 #include <stdexcept>
 #include <string>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "../include/fantoch_amd.h"
@@ -932,15 +935,27 @@ class Runner {
   std::vector<Process> procs;  // index = process id
   std::vector<uint32_t> process_region;
   std::vector<Client> clients;
-  std::map<std::pair<uint64_t, uint64_t>, SchedAction> queue;  // (time ms, seq) -> action (C3)
+  // (time ms, class, seq) -> action.  C3: ties at one time go first to the
+  // protocol/client actions in insertion (FIFO) order, then to the GC traffic
+  // (periodic GC events by process id, then MGarbageCollection deliveries by
+  // (from, to)).  GC actions touch only the GC track, which no other action
+  // reads, so this is one of the reference's legal tie orders (its
+  // BinaryHeap orders equal times arbitrarily), and the one that lets the GC
+  // traffic be evaluated apart from the event order (sim_wave.hip).
+  std::map<std::tuple<uint64_t, uint64_t, uint64_t>, SchedAction> queue;
   uint64_t seq = 0;
   uint64_t now_us = 0;
-  uint64_t events = 0, trace = 0, reorder_draws = 0, exec_notifications = 0;
+  uint64_t events = 0, trace = 0, reorder_draws = 0, exec_notifications = 0, gc_events = 0;
 
   uint64_t now_ms() const { return now_us / 1000; }
 
   void schedule(uint64_t delay_ms, SchedAction a) {  // Schedule::schedule (schedule.rs:38-49)
-    queue.emplace(std::make_pair(now_ms() + delay_ms, seq++), std::move(a));
+    uint64_t cls = 0;
+    if (a.kind == SK::PeriodicProcessEvent)
+      cls = (1ull << 20) | ((uint64_t)a.to << 8);
+    else if (a.kind == SK::SendToProc && a.msg.kind == MK::MGarbageCollection)
+      cls = (2ull << 20) | ((uint64_t)a.from << 8) | a.to;
+    queue.emplace(std::make_tuple(now_ms() + delay_ms, cls, seq++), std::move(a));
   }
 
   uint32_t region_of_process(uint32_t p) const { return process_region[p - 1]; }
@@ -993,14 +1008,14 @@ class Runner {
     while (status != DONE) {
       if (queue.empty()) throw std::logic_error("there should be a new action");
       auto it = queue.begin();
-      const uint64_t t = it->first.first;
+      const uint64_t t = std::get<0>(it->first);
       SchedAction a = std::move(it->second);
       queue.erase(it);
       if (t * 1000 < now_us) throw std::logic_error("time went backwards");
       now_us = t * 1000;  // SimTime::set_millis
       switch (a.kind) {
         case SK::PeriodicProcessEvent: {
-          note(0, a.to, 0, 0);
+          ++gc_events;  // GC traffic is counted apart, not part of the action trace
           procs[a.to].handle_gc_event();
           send_to_processes_and_executors(a.to);
           SchedAction b;
@@ -1030,7 +1045,10 @@ class Runner {
           break;
         }
         case SK::SendToProc: {
-          note(3, a.to, a.from, (uint64_t)a.msg.kind << 32 | FX_PACK_DOT(a.msg.dot.source, a.msg.dot.sequence));
+          if (a.msg.kind == MK::MGarbageCollection)
+            ++gc_events;
+          else
+            note(3, a.to, a.from, (uint64_t)a.msg.kind << 32 | FX_PACK_DOT(a.msg.dot.source, a.msg.dot.sequence));
           handle_send_to_proc(a.from, a.to, a.msg);
           break;
         }
