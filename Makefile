@@ -20,6 +20,13 @@ all: $(LIB) $(ORACLE) $(CPPTEST)
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
 
+# phase-cycle profile build of the simulator (tools/sim_phase.py; FX_LIB=...)
+PROF_LIB := fantoch_amd/build_prof/libfantoch_amd.so
+prof: $(PROF_LIB)
+$(PROF_LIB): $(SRCS) $(HDRS)
+	@mkdir -p fantoch_amd/build_prof
+	$(HIPCC) $(HIPFLAGS) -DFX_SIM_PROFILE -shared -o $@ $(SRCS)
+
 ORACLE_SRCS := oracle/graph_oracle.cpp oracle/sim_oracle.cpp
 $(ORACLE): $(ORACLE_SRCS) oracle/graph_oracle.hpp include/fantoch_amd.h
 	@mkdir -p oracle/build

@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfantoch_amd.so")
+# FX_LIB selects another build of the same library (tools: the FX_SIM_PROFILE build)
+LIB_PATH = os.environ.get("FX_LIB") or os.path.join(HERE, "libfantoch_amd.so")
 
 # status codes (fantoch_amd.h)
 FX_OK = 0

@@ -63,6 +63,16 @@ constexpr uint32_t RDMAX = 16;           // ready results per frame
 constexpr uint32_t HMAX = 2;             // link heads per lane (links <= 128; a template parameter)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 
+// FX_SIM_PROFILE builds (make prof): shader-clock cycles per event phase in
+// the stats rows (slots 0-15 cycles, 16-23 counts) instead of the counters
+#ifdef FX_SIM_PROFILE
+#define PROF_T0() const uint64_t prof_t0_ = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(cat) prof[cat] += __builtin_amdgcn_s_memtime() - prof_t0_
+#else
+#define PROF_T0() (void)0
+#define PROF_ADD(cat) (void)0
+#endif
+
 // message kinds (numbering of the oracle's trace, sim_oracle.cpp MK)
 enum : uint32_t { M_COLLECT = 0, M_COLLECT_ACK = 1, M_COMMIT = 2, M_CONSENSUS = 3, M_CONSENSUS_ACK = 4,
                   M_COMMIT_DOT = 5, M_GC = 6, M_STABLE = 7,
@@ -195,6 +205,9 @@ struct Sim {
   uint32_t sdot, srec, swait, stl, sfr, cf, cw;
   uint64_t occ, wmask, tmask;
   uint32_t xk, epoch, nwl, phase, root, idc, nfr, missing, fv, fdi, fnc, in_try, emitted, xp;
+#ifdef FX_SIM_PROFILE
+  uint64_t prof[24] = {};
+#endif
 
   // ------------------------------------------------------------ LDS views
   __device__ __forceinline__ uint32_t& W(uint32_t i) { return lds[i]; }
@@ -261,7 +274,12 @@ struct Sim {
     head_set(link, now + delay, seq);
     ++seq;
   }
-  __device__ __forceinline__ void send_p(uint32_t from, uint32_t to, uint32_t kind, uint32_t w2) {  // 0-based processes
+  __device__ __forceinline__ void send_p(uint32_t from, uint32_t to, uint32_t kind, uint32_t w2) {
+    PROF_T0();
+    send_p_(from, to, kind, w2);
+    PROF_ADD(3);
+  }
+  __device__ __forceinline__ void send_p_(uint32_t from, uint32_t to, uint32_t kind, uint32_t w2) {  // 0-based processes
     const uint32_t link = link_p(from, to);
     const uint32_t t = now + uni(dly(from * g.n + to));
     const uint32_t ht_ = uni(rh(link));
@@ -285,6 +303,11 @@ struct Sim {
 
   // -------------------------------------------------------------- trace
   __device__ __forceinline__ void note(uint64_t kind, uint64_t a, uint64_t b, uint64_t c) {
+    PROF_T0();
+    note_(kind, a, b, c);
+    PROF_ADD(6);
+  }
+  __device__ __forceinline__ void note_(uint64_t kind, uint64_t a, uint64_t b, uint64_t c) {
     ++events;
     trace = mix64(trace ^ ((uint64_t)now << 24) ^ (kind << 20) ^ (a << 12) ^ (b << 4)) + c;
   }
@@ -1002,6 +1025,11 @@ struct Sim {
   // and running the executor on what it committed), or advances the top
   // frame's action, or schedules the frame's ready results and pops it.
   __device__ __forceinline__ void run_handlers(uint32_t p, uint32_t from, uint32_t kind, uint32_t w2) {
+    PROF_T0();
+    run_handlers_(p, from, kind, w2);
+    PROF_ADD(7);
+  }
+  __device__ __forceinline__ void run_handlers_(uint32_t p, uint32_t from, uint32_t kind, uint32_t w2) {
     bool pend = true;
     uint32_t guard = 0;
     while (!err) {
@@ -1010,6 +1038,7 @@ struct Sim {
         pend = false;
         frame_push();
         if (err) return;
+        PROF_T0();
         switch (kind) {
           case M_SUBMIT: h_submit(p, w2); break;
           case M_COLLECT: h_mcollect(p, from, w2); break;
@@ -1020,10 +1049,16 @@ struct Sim {
           case M_COMMIT_DOT: h_mcommitdot(p, w2); break;
           default: err = FX_ERR_INVALID_ARG;
         }
+#ifdef FX_SIM_PROFILE
+        prof[8 + min(kind, 7u)] += __builtin_amdgcn_s_memtime() - prof_t0_;
+        prof[16 + min(kind, 7u)] += 1;
+#endif
         if (xinfo && !err) {  // to_executors (<= 1 per handler), LIFO
           const uint32_t d = xinfo;
           xinfo = 0;
+          PROF_T0();
           x_add(p, d);
+          PROF_ADD(2);
         }
         continue;
       }
@@ -1117,6 +1152,7 @@ struct Sim {
       return;
     }
     x -= g.C;
+    PROF_T0();
     {  // R(c): SendToClient -> Client::cmd_recv + cmd_send (simulation.rs:132-149)
       const uint32_t c = x;
       head_set(link, NONE, NONE);
@@ -1143,6 +1179,7 @@ struct Sim {
         }
       }
     }
+    PROF_ADD(4);
   }
 
   // wave-wide min over the link heads, (time, seq) lexicographic: each lane's
@@ -1286,7 +1323,14 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
   uint32_t gc_pair = NONE;
   while (!s.done && !s.err) {
     uint32_t t = 0;
+#ifdef FX_SIM_PROFILE
+    const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t link = s.pop_min(t);
+#ifdef FX_SIM_PROFILE
+    const uint64_t pt1 = __builtin_amdgcn_s_memtime();
+    s.prof[0] += pt1 - pt0;
+#endif
     if (link == NONE || t == NONE) {
       s.err = FX_ERR_SIM_LATE;  // "there should be a new action"
       break;
@@ -1308,6 +1352,9 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
     }
     s.now = t;
     s.run_event(link);
+#ifdef FX_SIM_PROFILE
+    s.prof[1] += __builtin_amdgcn_s_memtime() - pt1;
+#endif
     if (s.in_extra && s.now > s.final_ms) s.done = true;
     if (s.events >= max_events) s.err = FX_ERR_SIM_EVENTS;
   }
@@ -1325,6 +1372,9 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
     if (s.gc_ms && !s.err) s.gc_finish(s.now, gc_pair, st);
     if (s.lid == 0) {
       st[FX_SIM_STAT_EVENTS] = s.events;
+#ifdef FX_SIM_PROFILE
+      for (uint32_t i = 0; i < 24; ++i) st[i] = s.prof[i];
+#endif
       st[FX_SIM_STAT_END_MS] = s.now;
       st[FX_SIM_STAT_TRACE] = s.trace;
       st[FX_SIM_STAT_SEQ] = s.seq;
