@@ -48,7 +48,7 @@ def parse(argv=None):
                     help="sim: the batched simulator (BASELINE configs[1], the headline); "
                          "executor: the GraphExecutor alone over synthetic commit streams")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--seeds", type=int, default=4096)
     ap.add_argument("--conflicts", type=str, default="0,2,10,50,100")

@@ -51,7 +51,7 @@ def main_sim(args):
     from fantoch_amd import sim as S
 
     if args.cmds is None:
-        args.cmds = 200
+        args.cmds = 1000  # 1 client per region, 1k commands
     if args.cpu_baseline_seconds is None:
         args.cpu_baseline_seconds = 15.0
     world = int(os.environ.get("WORLD_SIZE", "1"))

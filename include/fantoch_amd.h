@@ -368,10 +368,11 @@ typedef struct fx_sim_batch {
 /* per-instance counters (u64) */
 #define FX_SIM_STAT_FAST 0u     /* [n] ProtocolMetricsKind::FastPath per process  */
 #define FX_SIM_STAT_SLOW 8u     /* [n] SlowPath                                    */
-#define FX_SIM_STAT_STABLE 16u  /* [n] Stable (commands garbage-collected)         */
-#define FX_SIM_STAT_EVENTS 24u  /* actions processed (executed notifications excluded) */
+#define FX_SIM_STAT_STABLE 16u  /* [n] Stable (commands garbage-collected; evaluated from the
+                                   committed-frontier history at the end of the run) */
+#define FX_SIM_STAT_EVENTS 24u  /* actions processed (executed notifications and GC traffic excluded) */
 #define FX_SIM_STAT_END_MS 25u  /* simulation time when the run stopped            */
-#define FX_SIM_STAT_TRACE 26u   /* hash of the processed action sequence (debug)   */
+#define FX_SIM_STAT_TRACE 26u   /* hash of the processed action sequence, GC traffic excluded (debug) */
 #define FX_SIM_STAT_SEQ 27u     /* schedule insertions                             */
 #define FX_SIM_STAT_DEPS 28u    /* deps of every executor Add (sum over processes) */
 #define FX_SIM_STATS 32u

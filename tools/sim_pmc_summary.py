@@ -52,7 +52,7 @@ def main():
     import bench_sim
     args = bench.parse(sys.argv[3:])
     if args.cmds is None:
-        args.cmds = 200  # bench_sim.main_sim's default
+        args.cmds = 1000  # bench_sim.main_sim default
     key = bench_sim.sim_key(args)
     res = {"kernel": KERNEL, "workload_key": key}
     c = {}
