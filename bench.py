@@ -54,7 +54,7 @@ def parse(argv=None):
     ap.add_argument("--conflicts", type=str, default="0,2,10,50,100")
     ap.add_argument("--n", type=int, default=5)
     ap.add_argument("--cmds", type=int, default=None,
-                    help="commands per client (sim default 200 as fantoch_ps/src/bin/simulation.rs; "
+                    help="commands per client (sim default 1000, SURVEY.md §8(a) C2; "
                          "executor default 1000)")
     ap.add_argument("--protocol", choices=["epaxos", "atlas"], default="epaxos")
     ap.add_argument("--f", type=int, default=2)

@@ -56,8 +56,9 @@ constexpr uint32_t NMAX = FX_SIM_MAX_N;  // processes
 constexpr uint32_t CMAX = 32;            // clients per instance
 constexpr uint32_t KMAX = 2;             // keys per command
 constexpr uint32_t VMAX = 16;            // deps of a committed value (per-launch: K (n + 1))
-constexpr uint32_t RT = 16;              // GC tick log entries per (process, source)
-constexpr uint32_t RC = 8;               // GC frontier change log entries per (process, source)
+// GC log entries per (process, source), per launch (Geo::rt, Geo::rc): the
+// tick log needs one entry per GC interval in which the frontier moved over the
+// last max-distance + interval, the change log the moves of the last interval
 constexpr uint32_t FMAX = 12;            // frame stack depth
 constexpr uint32_t RDMAX = 16;           // ready results per frame
 constexpr uint32_t HMAX = 2;             // link heads per lane (links <= 128; a template parameter)
@@ -88,22 +89,11 @@ constexpr uint32_t SL_DOT = 0, SL_CLIENT = 1, SL_IDX = 2, SL_KEYS = 3, SL_PST = 
 // SL_MASKS: participants(8) | proposer accepts(8) | committed count(8) | executed count(8)
 // SL_CNT:   value count(8) | collect count(8) | proposer ballot set(1) << 16 | nkeys << 20
 
-// per-process words
-constexpr uint32_t PR_SEQ = 0, PR_FAST = 1, PR_SLOW = 2, PR_EXEC = 4, PR_OCC = 5,  // 5,6
-    PR_WMASK = 7,                                                                                // 7,8
-    PR_EPOCH = 9, PR_FQ = 10, PR_WQ = PR_FQ + 1,
-    PR_REGION = PR_WQ + 1, PRW = PR_REGION + 1;
-// per-client words
-constexpr uint32_t CL_PROC = 0, CL_ISSUED = 1, CL_START = 2, CL_PENDING = 3, CL_REGION = 4, CLW = 5;
-// frame words
-constexpr uint32_t FR_ACT = 0, FR_KIND = 1, FR_DOT = 2, FR_TGT = 3, FR_NEXT = 4, FR_NREADY = 5, FR_READY = 6,
-                   FRW = FR_READY + RDMAX;
 
 struct Geo {  // launch-uniform geometry
-  uint32_t n, C, K, W, R, L, NP, ncli_keys;
+  uint32_t n, C, K, W, R, L, NP, ncli_keys, rt, rc;
   uint32_t amax, vmax, sl_value, sl_ack, slotw;  // dot-slot layout (MCollectAck deps <= 2K, value <= K(n+1))
-  uint32_t off_ring, off_rh, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_proc, off_cli, off_frame, off_wl,
-      off_delay, words;
+  uint32_t off_ring, off_rh, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_frame, off_wl, words;
 };
 
 struct SimArgs {
@@ -198,11 +188,27 @@ struct Sim {
   // GC state of lane 8 p + s (see h_mcommitdot): committed frontier + window
   // of source s + 1 at process p, tick-log and change-log counters
   uint32_t gf = 0, gw = 0, gnt = 0, glk = 0, gkm = 0, gnc = 0;
+  // Small per-process / per-client tables live in lanes (a wave-uniform
+  // index reads them with v_readlane instead of an LDS round trip):
+  // lane p: proposal seq, Fast / Slow counters, executed count, the
+  // executor's occupancy and waiting masks, fast | write quorum << 8
+  uint32_t pseq = 0, pfast = 0, pslow = 0, pexec = 0, pocc0 = 0, pocc1 = 0, pwm0 = 0, pwm1 = 0, pq = 0;
+  // lane c: process | region << 8, commands issued, start time, results pending
+  uint32_t cpr = 0, ciss = 0, cst = 0, cpend = 0;
+  // link delays (runner.rs:575-595): lane 8 p + q for p -> q; lane c for
+  // client c -> its process (dcs) and back (dcr)
+  uint32_t dpq = 0, dcs = 0, dcr = 0;
+  // handler frame stack, frame fi in lane fi: action (0 none, 1 ToSend) |
+  // kind << 2 | targets << 8 | next target << 16 | ready results << 20; dot
+  uint32_t frw = 0, frd = 0;
+  // executed clocks of the executors: lane 8 p + s = source s + 1 at process p
+  uint32_t ecf = 0, ecw = 0;
 
   // executor state of every process (lane-owned slot l / clock of source l + 1)
-  uint32_t xdot[NMAX], xrec[NMAX], xwait[NMAX], xtl[NMAX], xfr[NMAX], xcf[NMAX], xcw[NMAX];
-  // executor working copy (the process being run)
-  uint32_t sdot, srec, swait, stl, sfr, cf, cw;
+  uint32_t xdot[NMAX], xrec[NMAX], xwait[NMAX];
+  // executor working copy (the process being run); the Tarjan words and the
+  // DFS frames only live during one handle_add
+  uint32_t sdot, srec, swait, stl, sfr;
   uint64_t occ, wmask, tmask;
   uint32_t xk, epoch, nwl, phase, root, idc, nfr, missing, fv, fdi, fnc, in_try, emitted, xp;
 #ifdef FX_SIM_PROFILE
@@ -217,8 +223,8 @@ struct Sim {
   __device__ __forceinline__ uint32_t& rh(uint32_t link) { return lds[g.off_rh + link]; }  // head | tail << 16
   // GC logs of (process p, source s): tick log entry i = (tick count, frontier
   // before the change), change log entry i = (time, frontier after)
-  __device__ __forceinline__ uint32_t* gct(uint32_t p, uint32_t s) { return &lds[g.off_gct + (p * g.n + s) * RT * 2]; }
-  __device__ __forceinline__ uint32_t* gcc(uint32_t p, uint32_t s) { return &lds[g.off_gcc + (p * g.n + s) * RC * 2]; }
+  __device__ __forceinline__ uint32_t* gct(uint32_t p, uint32_t s) { return &lds[g.off_gct + (p * g.n + s) * g.rt * 2]; }
+  __device__ __forceinline__ uint32_t* gcc(uint32_t p, uint32_t s) { return &lds[g.off_gcc + (p * g.n + s) * g.rc * 2]; }
   __device__ __forceinline__ uint32_t* gcr(uint32_t p, uint32_t s) { return &lds[g.off_gcr + (p * g.n + s) * 4]; }
   __device__ __forceinline__ uint32_t slot_of(uint32_t d) const {
     return ((d >> FX_SEQ_BITS) - 1u) * g.W + (d & (g.W - 1u));
@@ -228,12 +234,8 @@ struct Sim {
   // take consecutive seqs in ascending target order) and the next tick index
   // link (p, q) delivers
   __device__ __forceinline__ uint32_t& kd(uint32_t p, uint32_t key) { return lds[g.off_kd + p * g.ncli_keys + key]; }
-  __device__ __forceinline__ uint32_t& P(uint32_t p, uint32_t w) { return lds[g.off_proc + p * PRW + w]; }
-  __device__ __forceinline__ uint32_t& CL(uint32_t c, uint32_t w) { return lds[g.off_cli + c * CLW + w]; }
-  __device__ __forceinline__ uint32_t& FR(uint32_t fi, uint32_t w) { return lds[g.off_frame + fi * FRW + w]; }
+  __device__ __forceinline__ uint32_t& FRR(uint32_t fi, uint32_t r) { return lds[g.off_frame + fi * RDMAX + r]; }
   __device__ __forceinline__ uint32_t& wl(uint32_t i) { return lds[g.off_wl + i]; }
-  // link delays: [0, n*n) process->process, then client->process [C], process->client [C]
-  __device__ __forceinline__ uint32_t& dly(uint32_t i) { return lds[g.off_delay + i]; }
 
   __device__ __forceinline__ uint32_t pst(uint32_t sl, uint32_t p) {
     return (uni(S(sl, SL_PST + (p >> 2))) >> ((p & 3u) * 8u)) & 0xFFu;
@@ -247,6 +249,10 @@ struct Sim {
   // store a uniform value from lane 0 (every lane computed the same)
   __device__ __forceinline__ void put(uint32_t& dst, uint32_t v) {
     if (lid == 0) dst = v;
+  }
+  // set lane `lane` of a lane table
+  __device__ __forceinline__ void lset(uint32_t& reg, uint32_t lane, uint32_t v) {
+    if (lid == lane) reg = v;
   }
 
   // ------------------------------------------------------------- links
@@ -281,7 +287,7 @@ struct Sim {
   }
   __device__ __forceinline__ void send_p_(uint32_t from, uint32_t to, uint32_t kind, uint32_t w2) {  // 0-based processes
     const uint32_t link = link_p(from, to);
-    const uint32_t t = now + uni(dly(from * g.n + to));
+    const uint32_t t = now + rl(dpq, from * 8u + to);
     const uint32_t ht_ = uni(rh(link));
     const uint32_t head = ht_ & 0xFFFFu, tail = ht_ >> 16;
     if (((tail - head) & 0xFFFFu) >= g.R) {
@@ -342,16 +348,9 @@ struct Sim {
 
   __device__ __forceinline__ void act_send(uint32_t kind, uint32_t dot, uint32_t tgt) {
     const uint32_t fi = nfrm - 1;
-    put(FR(fi, FR_ACT), 1);
-    put(FR(fi, FR_KIND), kind);
-    put(FR(fi, FR_DOT), dot);
-    put(FR(fi, FR_TGT), tgt);
-  }
-  __device__ __forceinline__ void act_forward(uint32_t kind, uint32_t dot) {
-    const uint32_t fi = nfrm - 1;
-    put(FR(fi, FR_ACT), 2);
-    put(FR(fi, FR_KIND), kind);
-    put(FR(fi, FR_DOT), dot);
+    const uint32_t w = rl(frw, fi);
+    lset(frw, fi, (w & (31u << 20)) | 1u | (kind << 2) | (tgt << 8));
+    lset(frd, fi, dot);
   }
 
   // ============================================================ protocol
@@ -392,13 +391,13 @@ struct Sim {
 
   // Protocol::submit (atlas.rs:210-249, epaxos.rs:199-221)
   __device__ __forceinline__ void h_submit(uint32_t p, uint32_t c) {
-    const uint32_t s = uni(P(p, PR_SEQ)) + 1u;
-    put(P(p, PR_SEQ), s);
+    const uint32_t s = rl(pseq, p) + 1u;
+    lset(pseq, p, s);
     if (s > FX_SEQ_MASK) { err = FX_ERR_DOT_RANGE; return; }
     const uint32_t dot = FX_PACK_DOT(p + 1, s);
     const uint32_t sl = slot_of(dot);
     if (uni(S(sl, SL_DOT)) != 0) { err = FX_ERR_SIM_CAPACITY; return; }
-    const uint32_t idx = uni(CL(c, CL_ISSUED)) - 1u;
+    const uint32_t idx = rl(ciss, c) - 1u;
     uint32_t nk = 0;
     const uint32_t keys = gen_keys(c + 1, idx, nk);
     // fresh slot
@@ -421,7 +420,7 @@ struct Sim {
     const uint32_t ps = pst(sl, p);
     if ((ps & 3u) != ST_START) return;
     const uint32_t src = (dot >> FX_SEQ_BITS) - 1u;
-    const uint32_t quorum = uni(P(src, PR_FQ));
+    const uint32_t quorum = rl(pq, src) & 0xFFu;
     if (!((quorum >> p) & 1u)) {
       set_pst(sl, p, (ps & ~3u) | ST_PAYLOAD);
       if (ps & 4u) {  // buffered commit (atlas.rs:288-292)
@@ -496,13 +495,15 @@ struct Sim {
     if (first) S(sl, g.sl_value + rank) = v;
     const uint32_t c0 = uni(S(sl, SL_CNT));
     put(S(sl, SL_CNT), (c0 & ~0xFFu) | nu | (fast ? 0u : (1u << 16)));  // slow: proposer ballot set
-    if (fast) put(P(p, PR_FAST), uni(P(p, PR_FAST)) + 1u);
-    else put(P(p, PR_SLOW), uni(P(p, PR_SLOW)) + 1u);
+    if (lid == p) {
+      if (fast) ++pfast;
+      else ++pslow;
+    }
     if (fast) {
       act_send(M_COMMIT, dot, (1u << n) - 1u);
     } else {
       // synod.skip_prepare (single.rs:208-213): ballot = coordinator id
-      act_send(M_CONSENSUS, dot, uni(P(p, PR_WQ)));
+      act_send(M_CONSENSUS, dot, rl(pq, p) >> 8);
     }
   }
 
@@ -520,7 +521,10 @@ struct Sim {
     set_pst(sl, p, (ps & ~3u) | ST_COMMIT);
     const uint32_t masks = uni(S(sl, SL_MASKS));
     put(S(sl, SL_MASKS), masks + (1u << 16));  // committed count
-    if (gc_ms) act_forward(M_COMMIT_DOT, dot);
+    // Forward(MCommitDot) to self: it only moves the GC track's committed
+    // clock (gc/clock.rs:43-48), which nothing but the GC evaluation reads,
+    // so it is applied in place
+    if (gc_ms) h_mcommitdot(p, dot);
   }
 
   // atlas.rs:477-524 / epaxos.rs:430-477
@@ -569,7 +573,7 @@ struct Sim {
   // Lane 8 p + s keeps the committed clock of source s + 1 at p (AEClock:
   // frontier + 32-bit exception window) and two logs of its frontier: one
   // entry per tick interval in which it moved (the value a tick before the
-  // move reports) and the last RC moves with their times.
+  // move reports) and its last moves with their times (Geo::rt, Geo::rc entries).
   __device__ __forceinline__ bool gc_lane(uint32_t p) const { return (lid >> 3) == p && (lid & 7u) < n; }
 
   // MCommitDot: add_to_clock (gc/clock.rs:43-48)
@@ -592,15 +596,15 @@ struct Sim {
           const uint32_t kt = now ? (now - 1u) / gc_ms : 0u;  // ticks strictly before now
           if (gnt == 0 || kt != glk) {
             uint32_t* tl = gct(p, si);
-            const uint32_t e = gnt & (RT - 1u);
-            if (gnt >= RT) gkm = tl[e * 2];  // newest dropped entry
+            const uint32_t e = gnt & (g.rt - 1u);
+            if (gnt >= g.rt) gkm = tl[e * 2];  // newest dropped entry
             tl[e * 2] = kt;
             tl[e * 2 + 1] = old;
             ++gnt;
             glk = kt;
           }
           uint32_t* cl = gcc(p, si);
-          const uint32_t e2 = gnc & (RC - 1u);
+          const uint32_t e2 = gnc & (g.rc - 1u);
           cl[e2 * 2] = now;
           cl[e2 * 2 + 1] = gf;
           ++gnc;
@@ -614,11 +618,11 @@ struct Sim {
   __device__ __forceinline__ bool gc_tick_value(uint32_t p, uint32_t s, uint32_t k, uint32_t& v) {
     const uint32_t* r = gcr(p, s);
     const uint32_t nt = r[1], km = r[2];
-    if (nt > RT && k < km) return false;
+    if (nt > g.rt && k < km) return false;
     const uint32_t* tl = gct(p, s);
-    const uint32_t cnt = min(nt, RT);
+    const uint32_t cnt = min(nt, g.rt);
     for (uint32_t i = 0; i < cnt; ++i) {
-      const uint32_t e = (nt - cnt + i) & (RT - 1u);
+      const uint32_t e = (nt - cnt + i) & (g.rt - 1u);
       if (tl[e * 2] > k) {
         v = tl[e * 2 + 1];
         return true;
@@ -631,16 +635,16 @@ struct Sim {
   __device__ __forceinline__ bool gc_value_at(uint32_t p, uint32_t s, uint32_t x, uint32_t& v) {
     const uint32_t nc = gcr(p, s)[3];
     const uint32_t* cl = gcc(p, s);
-    const uint32_t cnt = min(nc, RC);
+    const uint32_t cnt = min(nc, g.rc);
     for (uint32_t i = 0; i < cnt; ++i) {
-      const uint32_t e = (nc - 1u - i) & (RC - 1u);
+      const uint32_t e = (nc - 1u - i) & (g.rc - 1u);
       if (cl[e * 2] <= x) {
         v = cl[e * 2 + 1];
         return true;
       }
     }
     v = 0;
-    return nc <= RC;
+    return nc <= g.rc;
   }
 
   // first GC action after time x: its time, and (ticks first, then
@@ -650,7 +654,7 @@ struct Sim {
     uint32_t tv = NONE;
     const uint32_t p = lid >> 3, q = lid & 7u;
     if (p < n && q < n && p != q) {
-      const uint32_t d = dly(p * g.n + q);
+      const uint32_t d = dpq;
       tv = x < gc_ms + d ? gc_ms + d : ((x - d) / gc_ms + 1u) * gc_ms + d;
     }
     uint32_t tmin = tv;
@@ -679,14 +683,15 @@ struct Sim {
       // lane p: deliveries p -> q processed, m
       uint32_t m = 0;
       const bool pl = lid < n && lid != q;
+      const uint32_t dq = gather(dpq, (lid * 8u + q) & 63u);  // lane p: d(p, q)
       if (pl) {
-        const uint32_t d = dly(lid * g.n + q);
+        const uint32_t d = dq;
         if (tc > d) m = (tc - d - 1u) / gc_ms;
         if (pair == lid * 8u + q && tc >= d + gc_ms && (tc - d) % gc_ms == 0) ++m;
       }
       uint32_t stable = 0;
       if (!bal(pl && m == 0)) {
-        uint32_t tl = pl ? m * gc_ms + dly(lid * g.n + q) : 0u;
+        uint32_t tl = pl ? m * gc_ms + dq : 0u;
         for (uint32_t o = 1; o < 64; o <<= 1) tl = max(tl, (uint32_t)__shfl_xor((int)tl, (int)o));
         tl = uni(tl);
         uint32_t cur = 0;
@@ -715,38 +720,42 @@ struct Sim {
 
   __device__ __forceinline__ void x_load(uint32_t p) {
     xp = p;
-    sdot = rsel(xdot, p); srec = rsel(xrec, p); swait = rsel(xwait, p); stl = rsel(xtl, p);
-    sfr = rsel(xfr, p); cf = rsel(xcf, p); cw = rsel(xcw, p);
-    occ = (uint64_t)uni(P(p, PR_OCC)) | ((uint64_t)uni(P(p, PR_OCC + 1)) << 32);
-    wmask = (uint64_t)uni(P(p, PR_WMASK)) | ((uint64_t)uni(P(p, PR_WMASK + 1)) << 32);
-    epoch = uni(P(p, PR_EPOCH));
-    xk = uni(P(p, PR_EXEC));
+    sdot = rsel(xdot, p); srec = rsel(xrec, p); swait = rsel(xwait, p);
+    // Tarjan ids are reset at the end of every search (finalize) and the
+    // visited marks only matter inside one try_pending: a fresh epoch per call
+    stl = 0;
+    sfr = 0;
+    epoch = 1;
+    occ = (uint64_t)rl(pocc0, p) | ((uint64_t)rl(pocc1, p) << 32);
+    wmask = (uint64_t)rl(pwm0, p) | ((uint64_t)rl(pwm1, p) << 32);
+    xk = rl(pexec, p);
     tmask = 0;
     phase = PH_IDLE;
   }
   __device__ __forceinline__ void x_store() {
     const uint32_t p = xp;
-    rput(xdot, p, sdot); rput(xrec, p, srec); rput(xwait, p, swait); rput(xtl, p, stl);
-    rput(xfr, p, sfr); rput(xcf, p, cf); rput(xcw, p, cw);
-    put(P(p, PR_OCC), (uint32_t)occ);
-    put(P(p, PR_OCC + 1), (uint32_t)(occ >> 32));
-    put(P(p, PR_WMASK), (uint32_t)wmask);
-    put(P(p, PR_WMASK + 1), (uint32_t)(wmask >> 32));
-    put(P(p, PR_EPOCH), epoch);
-    put(P(p, PR_EXEC), xk);
+    rput(xdot, p, sdot); rput(xrec, p, srec); rput(xwait, p, swait);
+    if (lid == p) {
+      pocc0 = (uint32_t)occ;
+      pocc1 = (uint32_t)(occ >> 32);
+      pwm0 = (uint32_t)wmask;
+      pwm1 = (uint32_t)(wmask >> 32);
+      pexec = xk;
+    }
   }
 
   // AEClock::contains for a per-lane dot / a uniform dot (tarjan.rs:131-132)
   __device__ __forceinline__ bool contains_v(uint32_t d) const {
     const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
-    const uint32_t fr = gather(cf, si & 63u), w = gather(cw, si & 63u);
+    const uint32_t ln = (xp * 8u + si) & 63u;
+    const uint32_t fr = gather(ecf, ln), w = gather(ecw, ln);
     const uint32_t sq = d & FX_SEQ_MASK, off = sq - fr - 1u;
     return si < n && (sq <= fr || (off < 32u && ((w >> (off & 31u)) & 1u)));
   }
   __device__ __forceinline__ bool contains_u(uint32_t d) const {
     const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
     if (si >= n) return false;
-    const uint32_t fr = rl(cf, si), w = rl(cw, si);
+    const uint32_t fr = rl(ecf, xp * 8u + si), w = rl(ecw, xp * 8u + si);
     const uint32_t sq = d & FX_SEQ_MASK, off = sq - fr - 1u;
     return sq <= fr || (off < 32u && ((w >> off) & 1u));
   }
@@ -754,7 +763,7 @@ struct Sim {
   __device__ __forceinline__ void clk_add(uint32_t d) {
     const uint32_t si = (d >> FX_SEQ_BITS) - 1u;
     if (si >= n) { err = FX_ERR_DOT_RANGE; return; }
-    uint32_t fr = rl(cf, si), w = rl(cw, si);
+    uint32_t fr = rl(ecf, xp * 8u + si), w = rl(ecw, xp * 8u + si);
     const uint32_t sq = d & FX_SEQ_MASK;
     if (sq <= fr) return;
     const uint32_t off = sq - fr - 1u;
@@ -767,9 +776,9 @@ struct Sim {
       fr = fr + 1 + ones;
       w = win >> ones;
     }
-    if (lid == si) {
-      cf = fr;
-      cw = w;
+    if (lid == xp * 8u + si) {
+      ecf = fr;
+      ecw = w;
     }
   }
   __device__ __forceinline__ int find(uint32_t d) const {
@@ -797,16 +806,17 @@ struct Sim {
     if (uni(S(sl, SL_DOT)) != d) { err = FX_ERR_SIM_LATE; return; }
     const uint32_t c = uni(S(sl, SL_CLIENT));
     const uint32_t nk = (uni(S(sl, SL_CNT)) >> 20) & 3u;
-    if (uni(CL(c, CL_PROC)) == p) {  // pending.wait_for registered this rifl at p
-      const uint32_t pend = uni(CL(c, CL_PENDING));
+    if ((rl(cpr, c) & 0xFFu) == p) {  // pending.wait_for registered this rifl at p
+      const uint32_t pend = rl(cpend, c);
       if (pend < nk) { err = FX_ERR_SIM_LATE; return; }
-      put(CL(c, CL_PENDING), pend - nk);  // one ExecutorResult per key
+      lset(cpend, c, pend - nk);  // one ExecutorResult per key
       if (pend == nk) {
         const uint32_t fi = nfrm - 1;
-        const uint32_t nr = uni(FR(fi, FR_NREADY));
+        const uint32_t w = rl(frw, fi);
+        const uint32_t nr = (w >> 20) & 31u;
         if (nr >= RDMAX) { err = FX_ERR_SIM_CAPACITY; return; }
-        put(FR(fi, FR_READY + nr), c);
-        put(FR(fi, FR_NREADY), nr + 1u);
+        put(FRR(fi, nr), c);
+        lset(frw, fi, w + (1u << 20));
       }
     }
     const uint32_t masks = uni(S(sl, SL_MASKS));
@@ -1011,9 +1021,7 @@ struct Sim {
   __device__ __forceinline__ void frame_push() {
     if (nfrm >= FMAX) { err = FX_ERR_SIM_CAPACITY; return; }
     const uint32_t fi = nfrm++;
-    put(FR(fi, FR_ACT), 0);
-    put(FR(fi, FR_NEXT), 0);
-    put(FR(fi, FR_NREADY), 0);
+    lset(frw, fi, 0);
     xinfo = 0;
   }
 
@@ -1046,7 +1054,6 @@ struct Sim {
           case M_COMMIT: h_mcommit(p, from, w2); break;
           case M_CONSENSUS: h_mconsensus(p, from, w2); break;
           case M_CONSENSUS_ACK: h_mconsensusack(p, from, w2); break;
-          case M_COMMIT_DOT: h_mcommitdot(p, w2); break;
           default: err = FX_ERR_INVALID_ARG;
         }
 #ifdef FX_SIM_PROFILE
@@ -1064,24 +1071,15 @@ struct Sim {
       }
       if (nfrm == 0) return;
       const uint32_t fi = nfrm - 1;
-      const uint32_t act = uni(FR(fi, FR_ACT));
-      if (act == 2) {  // ToForward: deliver to self now
-        put(FR(fi, FR_ACT), 0);
-        from = p;
-        kind = uni(FR(fi, FR_KIND));
-        w2 = uni(FR(fi, FR_DOT));
-        pend = true;
-        continue;
-      }
-      if (act == 1) {  // ToSend: targets ascending (C4), self recurses in place
-        const uint32_t tgt = uni(FR(fi, FR_TGT));
-        const uint32_t k2 = uni(FR(fi, FR_KIND)), dot = uni(FR(fi, FR_DOT));
-        uint32_t nx = uni(FR(fi, FR_NEXT));
+      const uint32_t w = rl(frw, fi);
+      if (w & 3u) {  // ToSend: targets ascending (C4), self recurses in place
+        const uint32_t tgt = (w >> 8) & 0xFFu, k2 = (w >> 2) & 15u, dot = rl(frd, fi);
+        uint32_t nx = (w >> 16) & 15u;
         while (nx < n) {
           const uint32_t to = nx++;
           if (!((tgt >> to) & 1u)) continue;
           if (to == p) {
-            put(FR(fi, FR_NEXT), nx);
+            lset(frw, fi, (w & ~(15u << 16)) | (nx << 16));
             from = p;
             kind = k2;
             w2 = dot;
@@ -1092,13 +1090,12 @@ struct Sim {
           if (err) return;
         }
         if (pend) continue;
-        put(FR(fi, FR_ACT), 0);
       }
       // ready results -> schedule_to_client (runner.rs:434-440)
-      const uint32_t nr = uni(FR(fi, FR_NREADY));
+      const uint32_t nr = (w >> 20) & 31u;
       for (uint32_t r = 0; r < nr; ++r) {
-        const uint32_t c = uni(FR(fi, FR_READY + r));
-        schedule_timer(link_r(c), uni(dly(g.n * g.n + g.C + c)));
+        const uint32_t c = uni(FRR(fi, r));
+        schedule_timer(link_r(c), rl(dcr, c));
       }
       --nfrm;
     }
@@ -1107,11 +1104,13 @@ struct Sim {
   // ======================================================= event loop
   // Client::cmd_send: next command of client c (0-based) -> SubmitToProc
   __device__ __forceinline__ bool client_send(uint32_t c) {
-    const uint32_t issued = uni(CL(c, CL_ISSUED));
+    const uint32_t issued = rl(ciss, c);
     if (issued >= cmds) return false;
-    put(CL(c, CL_ISSUED), issued + 1u);
-    put(CL(c, CL_START), now);  // Pending::start
-    schedule_timer(link_s(c), uni(dly(g.n * g.n + c)));
+    if (lid == c) {
+      ciss = issued + 1u;
+      cst = now;  // Pending::start
+    }
+    schedule_timer(link_s(c), rl(dcs, c));
     return true;
   }
 
@@ -1145,9 +1144,9 @@ struct Sim {
     if (x < g.C) {  // S(c): SubmitToProc
       const uint32_t c = x;
       head_set(link, NONE, NONE);
-      const uint32_t p = uni(CL(c, CL_PROC));
-      note(2, p + 1, c + 1, uni(CL(c, CL_ISSUED)));
-      put(CL(c, CL_PENDING), g.K);  // AggregatePending::wait_for: key_count results
+      const uint32_t p = rl(cpr, c) & 0xFFu;
+      note(2, p + 1, c + 1, rl(ciss, c));
+      lset(cpend, c, g.K);  // AggregatePending::wait_for: key_count results
       run_handlers(p, p, M_SUBMIT, c);
       return;
     }
@@ -1156,14 +1155,14 @@ struct Sim {
     {  // R(c): SendToClient -> Client::cmd_recv + cmd_send (simulation.rs:132-149)
       const uint32_t c = x;
       head_set(link, NONE, NONE);
-      const uint32_t issued = uni(CL(c, CL_ISSUED));
+      const uint32_t issued = rl(ciss, c);
       note(4, c + 1, 0, issued);
-      const uint32_t lat = now - uni(CL(c, CL_START));  // latency.as_millis()
+      const uint32_t lat = now - rl(cst, c);  // latency.as_millis()
+      const uint32_t region = rl(cpr, c) >> 8;
       if (lid == 0) {
         if (A.latency_log && issued - 1u < A.lat_cap)
           A.latency_log[((size_t)inst * g.C + c) * A.lat_cap + issued - 1u] = lat;
         if (A.lat_hist) {
-          const uint32_t region = CL(c, CL_REGION);
           atomicAdd(&A.lat_hist[(size_t)region * A.lat_bins + min(lat, A.lat_bins - 1u)], 1ull);
         }
       }
@@ -1216,7 +1215,7 @@ struct Sim {
 };
 
 template <uint32_t HM>
-__global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
+__global__ __launch_bounds__(64, 3) void k_sim(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
@@ -1258,7 +1257,7 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
 #pragma unroll
   for (uint32_t k = 0; k < HM; ++k) s.ht[k] = s.hs[k] = NONE;
 #pragma unroll
-  for (uint32_t k = 0; k < NMAX; ++k) s.xdot[k] = s.xrec[k] = s.xwait[k] = s.xtl[k] = s.xfr[k] = s.xcf[k] = s.xcw[k] = 0;
+  for (uint32_t k = 0; k < NMAX; ++k) s.xdot[k] = s.xrec[k] = s.xwait[k] = 0;
   const uint32_t RP = a.RP;
   // process regions, quorums (BaseProcess::discover over
   // sort_processes_by_distance, base.rs:62-154, util.rs:153-185)
@@ -1277,11 +1276,8 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
     }
     const uint32_t fqm = (uint32_t)bal(s.lid < n && pos < s.fq);
     const uint32_t wqm = (uint32_t)bal(s.lid < n && pos < s.wq);
-    s.put(s.P(p, PR_FQ), fqm);
-    s.put(s.P(p, PR_WQ), wqm);
-    s.put(s.P(p, PR_EPOCH), 1);
-    s.put(s.P(p, PR_REGION), rp);
-    if (s.lid < n) s.dly(p * n + s.lid) = a.ping[rp * RP + sp.process_regions[s.lid]] / 2u;
+    s.lset(s.pq, p, fqm | (wqm << 8));
+    if (s.lid >= p * 8u && s.lid < p * 8u + n) s.dpq = a.ping[rp * RP + sp.process_regions[s.lid - p * 8u]] / 2u;
   }
   // clients: for region in client_regions, clients_per_region each (runner.rs:143-163)
   {
@@ -1298,10 +1294,11 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
         }
       }
       for (uint32_t i = 0; i < sp.clients_per_region; ++i, ++c) {
-        s.put(s.CL(c, CL_PROC), best);
-        s.put(s.CL(c, CL_REGION), rc);
-        s.put(s.dly(n * n + c), a.ping[rc * RP + sp.process_regions[best]] / 2u);
-        s.put(s.dly(n * n + s.C + c), a.ping[sp.process_regions[best] * RP + rc] / 2u);
+        if (s.lid == c) {
+          s.cpr = best | (rc << 8);
+          s.dcs = a.ping[rc * RP + sp.process_regions[best]] / 2u;
+          s.dcr = a.ping[sp.process_regions[best] * RP + rc] / 2u;
+        }
       }
     }
   }
@@ -1360,13 +1357,13 @@ __global__ __launch_bounds__(64, 2) void k_sim(SimArgs a) {
   }
   // ----------------------------------------------------------- outputs
   __builtin_amdgcn_s_barrier();
-  if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = s.P(s.lid, PR_EXEC);
+  if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = s.pexec;
   if (a.stats) {
     unsigned long long* st = a.stats + (size_t)inst * FX_SIM_STATS;
     if (s.lid < NMAX) {
       const bool v = s.lid < n;
-      st[FX_SIM_STAT_FAST + s.lid] = v ? s.P(s.lid, PR_FAST) : 0u;
-      st[FX_SIM_STAT_SLOW + s.lid] = v ? s.P(s.lid, PR_SLOW) : 0u;
+      st[FX_SIM_STAT_FAST + s.lid] = v ? s.pfast : 0u;
+      st[FX_SIM_STAT_SLOW + s.lid] = v ? s.pslow : 0u;
       st[FX_SIM_STAT_STABLE + s.lid] = 0u;
     }
     if (s.gc_ms && !s.err) s.gc_finish(s.now, gc_pair, st);
@@ -1414,16 +1411,19 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   uint32_t o = 0;
   g.off_ring = o; o += g.NP * g.R * 3;
   g.off_rh = o; o += g.NP;
-  g.off_gct = o; o += n * n * RT * 2;
-  g.off_gcc = o; o += n * n * RC * 2;
+  // GC logs: 8 / 4 entries per client per region (commits of one source
+  // arrive about once per client round trip)
+  const uint32_t cpr = (C + n - 1) / n;
+  g.rt = 8;
+  while (g.rt < 8 * cpr && g.rt < 64) g.rt <<= 1;
+  g.rc = g.rt / 2;
+  g.off_gct = o; o += n * n * g.rt * 2;
+  g.off_gcc = o; o += n * n * g.rc * 2;
   g.off_gcr = o; o += n * n * 4;
   g.off_slot = o; o += n * g.W * g.slotw;
   g.off_kd = o; o += n * g.ncli_keys;
-  g.off_proc = o; o += n * PRW;
-  g.off_cli = o; o += C * CLW;
-  g.off_frame = o; o += FMAX * FRW;
+  g.off_frame = o; o += FMAX * RDMAX;
   g.off_wl = o; o += 72;
-  g.off_delay = o; o += n * n + 2 * C;
   g.words = (o + 3) & ~3u;
   return true;
 }
