@@ -93,7 +93,7 @@ constexpr uint32_t SL_DOT = 0, SL_CLIENT = 1, SL_IDX = 2, SL_KEYS = 3, SL_PST = 
 struct Geo {  // launch-uniform geometry
   uint32_t n, C, K, W, R, L, NP, ncli_keys, rt, rc;
   uint32_t amax, vmax, sl_value, sl_ack, slotw;  // dot-slot layout (MCollectAck deps <= 2K, value <= K(n+1))
-  uint32_t off_ring, off_rh, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_frame, off_wl, words;
+  uint32_t off_ring, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_frame, off_wl, words;
 };
 
 struct SimArgs {
@@ -201,6 +201,8 @@ struct Sim {
   // handler frame stack, frame fi in lane fi: action (0 none, 1 ToSend) |
   // kind << 2 | targets << 8 | next target << 16 | ready results << 20; dot
   uint32_t frw = 0, frd = 0;
+  // message ring of process link l (< n (n - 1) <= 56): head | tail << 16 in lane l
+  uint32_t rhv = 0;
   // executed clocks of the executors: lane 8 p + s = source s + 1 at process p
   uint32_t ecf = 0, ecw = 0;
 
@@ -220,7 +222,6 @@ struct Sim {
   __device__ __forceinline__ uint32_t& ring(uint32_t link, uint32_t e, uint32_t w) {
     return lds[g.off_ring + (link * g.R + e) * 3 + w];
   }
-  __device__ __forceinline__ uint32_t& rh(uint32_t link) { return lds[g.off_rh + link]; }  // head | tail << 16
   // GC logs of (process p, source s): tick log entry i = (tick count, frontier
   // before the change), change log entry i = (time, frontier after)
   __device__ __forceinline__ uint32_t* gct(uint32_t p, uint32_t s) { return &lds[g.off_gct + (p * g.n + s) * g.rt * 2]; }
@@ -288,7 +289,7 @@ struct Sim {
   __device__ __forceinline__ void send_p_(uint32_t from, uint32_t to, uint32_t kind, uint32_t w2) {  // 0-based processes
     const uint32_t link = link_p(from, to);
     const uint32_t t = now + rl(dpq, from * 8u + to);
-    const uint32_t ht_ = uni(rh(link));
+    const uint32_t ht_ = rl(rhv, link);
     const uint32_t head = ht_ & 0xFFFFu, tail = ht_ >> 16;
     if (((tail - head) & 0xFFFFu) >= g.R) {
       err = FX_ERR_SIM_CAPACITY;
@@ -302,7 +303,7 @@ struct Sim {
     put(ring(link, e, 0), t | (kind << 28));
     put(ring(link, e, 1), seq);
     put(ring(link, e, 2), w2);
-    put(rh(link), head | (((tail + 1u) & 0xFFFFu) << 16));
+    lset(rhv, link, head | (((tail + 1u) & 0xFFFFu) << 16));
     if (head == tail) head_set(link, t, seq);
     ++seq;
   }
@@ -1118,13 +1119,13 @@ struct Sim {
     if (link < g.NP) {  // P(p, q): SendToProc
       const uint32_t p = link / (g.n - 1u), qi = link % (g.n - 1u);
       const uint32_t q = qi < p ? qi : qi + 1u;
-      const uint32_t ht_ = uni(rh(link));
+      const uint32_t ht_ = rl(rhv, link);
       const uint32_t head = ht_ & 0xFFFFu, tail = ht_ >> 16;
       const uint32_t e = head & (g.R - 1u);
       const uint32_t w0 = uni(ring(link, e, 0)), w2 = uni(ring(link, e, 2));
       const uint32_t kind = w0 >> 28;
       const uint32_t nh = (head + 1u) & 0xFFFFu;
-      put(rh(link), nh | (tail << 16));
+      lset(rhv, link, nh | (tail << 16));
       if (nh != tail) {
         const uint32_t e2 = nh & (g.R - 1u);
         head_set(link, uni(ring(link, e2, 0)) & 0x0FFFFFFFu, uni(ring(link, e2, 1)));
@@ -1410,7 +1411,6 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   if (n * g.amax > 64 || g.slotw > 64) return false;
   uint32_t o = 0;
   g.off_ring = o; o += g.NP * g.R * 3;
-  g.off_rh = o; o += g.NP;
   // GC logs: 8 / 4 entries per client per region (commits of one source
   // arrive about once per client round trip)
   const uint32_t cpr = (C + n - 1) / n;
