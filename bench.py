@@ -44,7 +44,7 @@ LAYOUT = {0: "16 lanes per stream", 1: "one lane per stream", 2: "one lane per s
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["sim", "executor"], default="sim",
+    ap.add_argument("--mode", choices=["sim", "executor", "huge"], default="sim",
                     help="sim: the batched simulator (BASELINE configs[1], the headline); "
                          "executor: the GraphExecutor alone over synthetic commit streams")
     ap.add_argument("--gpus", type=int, default=1)
@@ -116,6 +116,9 @@ def main():
     if args.mode == "sim":
         from bench_sim import main_sim
         return main_sim(args)
+    if args.mode == "huge":
+        from bench_huge import main_huge
+        return main_huge(args)
     if args.cmds is None:
         args.cmds = 1000
     if args.cpu_baseline_seconds is None:

@@ -1,0 +1,140 @@
+"""bench.py --mode huge: BASELINE configs[4], one simulated instance whose five
+executors each see a 10^6-Add commit stream with cycles (synthetic Atlas
+commit streams, n = 5, 2 % conflicts, 30 % cross-coordinator cycles), executed
+by the quiescent-cut driver (fx_batch_run_cut, graph_cut.hip).
+
+One step = fx_batch_run_cut over the 5 x 10^6 Adds + fx_batch_metrics.  The
+instance does not shard: with --gpus N every rank runs its
+own replica and `value` counts the Adds of all replicas.  cpu_baseline: the
+C++ oracle (oracle/graph_oracle.cpp, one std::thread per stream) on the same
+five streams, whose outputs are also compared with the GPU's bit for bit."""
+import ctypes
+import json
+import os
+import time
+
+HBM_PEAK_GBPS = 8000.0
+
+
+def main_huge(args):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from fantoch_amd import _lib
+    from fantoch_amd import streams as fs
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    lib = _lib.load()
+    if lib.fx_device_count() <= 0:
+        raise SystemExit("no GPU visible to libfantoch_amd")
+    cmds = args.cmds if args.cmds is not None else 200_000  # n x cmds = 10^6 Adds per executor
+    p = fs.synth_params(seed=args.seed, instances=1, n=5, cmds=cmds, window=args.window,
+                        cycle_pct=args.cycle_pct, conflicts=(2,))
+    S, steps, dmax = fs.synth_shape(p)
+    pw = _lib.plane_words(S, steps)
+    stream = torch.cuda.current_stream(dev)
+    hs = ctypes.c_void_p(stream.cuda_stream)
+
+    def buf(words):
+        return torch.empty(words, dtype=torch.int32, device=dev)
+
+    dot, hdr, deps = buf(pw), buf(pw), buf(pw * dmax)
+    order, release = buf(pw), buf(pw)
+    nexec, err = buf(S), buf(S)
+    NBC, NBD = 64, 4096
+    chain = torch.zeros(NBC, dtype=torch.int64, device=dev)
+    delay = torch.zeros(NBD, dtype=torch.int64, device=dev)
+    _lib.check(lib.fx_synth_generate(ctypes.byref(p), dot.data_ptr(), hdr.data_ptr(), deps.data_ptr(), hs),
+               "fx_synth_generate")
+    torch.cuda.synchronize(dev)
+    inb = _lib.StreamBatch(dot.data_ptr(), hdr.data_ptr(), deps.data_ptr(), None, S, steps, dmax, 5)
+    outb = _lib.OrderBatch(order.data_ptr(), release.data_ptr(), nexec.data_ptr(), err.data_ptr())
+    hb = _lib.HistBatch(chain.data_ptr(), NBC, delay.data_ptr(), NBD)
+    nd_total = int(((hdr >> 24) & 31).sum(dtype=torch.int64).item())
+    n_adds = S * steps
+    stats = _lib.CutStats()
+
+    def step():
+        chain.zero_()
+        delay.zero_()
+        st = lib.fx_batch_run_cut(ctypes.byref(inb), ctypes.byref(outb), 0, hs, ctypes.byref(stats))
+        _lib.check(st, "fx_batch_run_cut")
+        _lib.check(lib.fx_batch_metrics(ctypes.byref(inb), ctypes.byref(outb), ctypes.byref(hb), hs),
+                   "fx_batch_metrics")
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.time()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.time() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    executed = int(nexec.sum(dtype=torch.int64).item())
+    assert executed == n_adds and int((err != 0).sum().item()) == 0, "configs[4] run incomplete"
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    value = executed * world * args.steps / elapsed
+    alg_bytes = (36.0 * n_adds + 8.0 * nd_total)
+    achieved = alg_bytes / (elapsed / args.steps) / 1e9
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        from oracle import oracle_lib
+        host = fs.Planes(S, steps, dmax, 5, dot=dot.cpu().numpy().view(np.uint32),
+                         hdr=hdr.cpu().numpy().view(np.uint32), deps=deps.cpu().numpy().view(np.uint32))
+        t1 = time.time()
+        o_order, o_rel, o_nexec, o_err = oracle_lib.batch_execute(host, threads=S)
+        cpu_s = time.time() - t1
+        g_order = order.cpu().numpy().view(np.uint32)
+        g_rel = release.cpu().numpy().view(np.uint32)
+        same = bool(np.array_equal(o_nexec, nexec.cpu().numpy().view(np.uint32)))
+        for s in range(S):
+            idx = _lib.index(np.arange(steps), s, steps)
+            same = same and np.array_equal(g_order[idx], o_order[idx]) and np.array_equal(g_rel[idx], o_rel[idx])
+        cpu = {"value": round(n_adds / cpu_s, 1), "unit": "cmds/s", "cores": S, "kind": "port",
+               "sample": "the whole configs[4] instance (5 x %d Adds) through the C++ oracle, one thread per "
+                         "executor stream (the reference's executors of one instance run on their own "
+                         "tasks), %.3f s; GPU output identical: %s" % (steps, cpu_s, same),
+               "sample_parity": same}
+    line = {
+        "metric": "executed cmds/sec (node) for batched Atlas/EPaxos sims; % of HBM roofline",
+        "value": round(value, 1), "unit": "cmds/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic Atlas commit streams (fx_synth: 2 %% conflicts, 30 %% cycles, window %d)" % args.window,
+        "config": {"workload": "single huge instance: 5 executors x %d Adds with cycles (BASELINE configs[4])"
+                               % steps,
+                   "parallelism": "quiescent-cut decomposition on one GPU; replicas only across GPUs"},
+        "segments": int(stats.segments), "max_segment": int(stats.max_segment),
+        "whole_streams": int(stats.whole_streams),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": None,
+                     "kernel": "fx_batch_run_cut (cut analysis + segment executor + scatter)",
+                     "alg_bytes_per_cmd": round(alg_bytes / n_adds, 3)},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()

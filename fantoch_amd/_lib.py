@@ -81,6 +81,13 @@ class OrderBatch(ctypes.Structure):
                 ("nexec", ctypes.c_void_p), ("err", ctypes.c_void_p)]
 
 
+class CutStats(ctypes.Structure):
+    """fx_cut_stats (fx_batch_run_cut)."""
+    _fields_ = [("segments", ctypes.c_uint64), ("max_segment", ctypes.c_uint32),
+                ("whole_streams", ctypes.c_uint32), ("failed_streams", ctypes.c_uint32),
+                ("tier_counts", ctypes.c_uint32 * 8)]
+
+
 class HistBatch(ctypes.Structure):
     _fields_ = [("chain_size", ctypes.c_void_p), ("nbins_chain", ctypes.c_uint32),
                 ("execution_delay", ctypes.c_void_p), ("nbins_delay", ctypes.c_uint32)]
@@ -182,6 +189,9 @@ SIGNATURES = [
     ("fx_batch_run_tiered", ctypes.c_int,
      [ctypes.POINTER(StreamBatch), ctypes.POINTER(OrderBatch), ctypes.c_uint32, ctypes.c_void_p,
       u32p]),
+    ("fx_batch_run_cut", ctypes.c_int,
+     [ctypes.POINTER(StreamBatch), ctypes.POINTER(OrderBatch), ctypes.c_uint32, ctypes.c_void_p,
+      ctypes.c_void_p]),
     ("fx_synth_shape", ctypes.c_int, [ctypes.POINTER(SynthParams), u32p, u32p, u32p]),
     ("fx_synth_generate", ctypes.c_int,
      [ctypes.POINTER(SynthParams), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

@@ -1,6 +1,9 @@
 // fx_internal.h — declarations shared by the kernel and host translation units.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <vector>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -85,4 +88,16 @@ int gather_release(const uint32_t* order, const uint32_t* release, uint32_t step
 // returns the count.
 uint32_t decode_pending(uint32_t tier, const uint32_t* block, uint32_t lane, uint32_t* dots,
                         uint32_t* waits, uint32_t cap);
+
+// Device scratch that persists across calls: slot `slot` grown to at least
+// `bytes` (never shrunk; hipMalloc of multi-GB buffers per call costs more
+// than the kernels of a configs[4] step).  NULL on allocation failure.
+// Callers hold scratch_mutex() while they use their slots.
+void* scratch(uint32_t slot, size_t bytes);
+std::recursive_mutex& scratch_mutex();
+enum : uint32_t { SCRATCH_TIERED_STATE = 0, SCRATCH_TIERED_MAP = 1, SCRATCH_CUT_FIRST = 2, SCRATCH_SLOTS = 40 };
+
+// fx_batch_run_tiered over all streams (only == NULL) or the listed ones.
+int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
+               const std::vector<uint32_t>* only, uint32_t* tier_counts);
 }  // namespace fx

@@ -974,6 +974,9 @@ const char* fx_status_string(int s) {
     case FX_ERR_TIME_RANGE: return "time out of range";
     case FX_ERR_NO_DEVICE: return "no GPU device";
     case FX_ERR_LOG_FORMAT: return "malformed execution log";
+    case FX_ERR_SIM_CAPACITY: return "simulated instance outgrew its launch geometry";
+    case FX_ERR_SIM_LATE: return "simulated message found no state for its dot";
+    case FX_ERR_SIM_EVENTS: return "simulated instance exceeded its event budget";
     default: return "unknown";
   }
 }
@@ -1192,6 +1195,31 @@ int fx_synth_generate_host(const fx_synth_params* p, uint32_t* dot, uint32_t* hd
   return FX_OK;
 }
 
+}  // extern "C"
+
+namespace fx {
+
+static void* g_scratch[SCRATCH_SLOTS] = {};
+static size_t g_scratch_cap[SCRATCH_SLOTS] = {};
+
+void* scratch(uint32_t slot, size_t bytes) {
+  if (slot >= SCRATCH_SLOTS) return nullptr;
+  bytes = std::max<size_t>(bytes, 256);
+  if (g_scratch_cap[slot] >= bytes) return g_scratch[slot];
+  if (g_scratch[slot]) (void)hipFree(g_scratch[slot]);
+  g_scratch[slot] = nullptr;
+  g_scratch_cap[slot] = 0;
+  const size_t grown = bytes + bytes / 4;
+  if (hipMalloc(&g_scratch[slot], grown) != hipSuccess) return nullptr;
+  g_scratch_cap[slot] = grown;
+  return g_scratch[slot];
+}
+
+std::recursive_mutex& scratch_mutex() {
+  static std::recursive_mutex m;
+  return m;
+}
+
 // Escalation chain of fx_batch_run_tiered (FX_NUM_TIERS = none).
 static uint32_t escalate(uint32_t tier) {
   switch (tier) {
@@ -1205,10 +1233,12 @@ static uint32_t escalate(uint32_t tier) {
   }
 }
 
-// Synchronous tiered driver: the first tier for all, then reruns of the
-// streams that ran out of capacity up the escalation chain.
-int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags,
-                        void* hip_stream, uint32_t* tier_counts) {
+// Synchronous tiered driver: the first tier for all (or for the streams in
+// `only`), then reruns of the streams that ran out of capacity up the
+// escalation chain.  The error plane comes back with one copy per tier.
+int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
+               const std::vector<uint32_t>* only, uint32_t* tier_counts) {
+  std::lock_guard<std::recursive_mutex> lock(scratch_mutex());
   int st = check_batch(in, out);
   if (st) return st;
   hipStream_t hs = (hipStream_t)hip_stream;
@@ -1219,54 +1249,61 @@ int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out, ui
   flags &= ~(7u << FX_FLAG_TIER_SHIFT);
   uint32_t first = ft ? ft - 1u : (uint32_t)FX_TIER_DEFAULT;
   if (first >= FX_NUM_TIERS) return FX_ERR_INVALID_ARG;
+  if (only && first == FX_TIER_SPLIT) first = FX_TIER_GROUP;  // the split tier takes whole batches
   // tiers that cannot hold the widest Add start one step up the chain
   if ((first == FX_TIER_WAVE && in->dmax > WAVE_MAX_DEPS) ||
       ((first == FX_TIER_GROUP || first == FX_TIER_SPLIT) && in->dmax > GROUP_LANES) ||
       (first == FX_TIER_LANE_REG && in->dmax > LANE_MAX_DEPS))
     first = FX_TIER_LDS_LARGE;
-  void* st1 = nullptr;
-  if ((first == FX_TIER_GLOBAL || first == FX_TIER_SPLIT) && hipMalloc(&st1, fx_batch_state_bytes(first, in->n, S)) != hipSuccess)
-    return FX_ERR_HIP;
-  st = fx_batch_execute(in, out, first, nullptr, S, st1, 0, in->steps, flags, nullptr, hip_stream);
-  if (st1) (void)hipFree(st1);
-  if (st) return st;
-  if (tier_counts) {
+  if (tier_counts)
     for (uint32_t t = 0; t < FX_NUM_TIERS; ++t) tier_counts[t] = 0;
-    tier_counts[first] = S;
+  std::vector<uint32_t> todo;
+  if (only) {
+    todo = *only;
+  } else {
+    todo.resize(S);
+    for (uint32_t s = 0; s < S; ++s) todo[s] = s;
   }
-  std::vector<uint32_t> err(S);
-  if (hipMemcpyAsync(err.data(), out->err, (size_t)S * 4, hipMemcpyDeviceToHost, hs) != hipSuccess)
-    return FX_ERR_HIP;
-  if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
-  for (uint32_t tier = escalate(first); tier < FX_NUM_TIERS; tier = escalate(tier)) {
-    std::vector<uint32_t> redo;
-    for (uint32_t s = 0; s < S; ++s)
-      if (err[s] == FX_ERR_CAPACITY) redo.push_back(s);
-    if (tier_counts) tier_counts[tier] = (uint32_t)redo.size();
-    if (redo.empty()) break;
+  if (todo.empty()) return FX_OK;
+  std::vector<uint32_t> err(S, 0);
+  for (uint32_t tier = first; tier < FX_NUM_TIERS && !todo.empty(); tier = escalate(tier)) {
+    const uint32_t L = (uint32_t)todo.size();
+    if (tier_counts) tier_counts[tier] = L;
+    const bool whole = !only && tier == first;
     uint32_t* dmap = nullptr;
     void* dstate = nullptr;
-    const uint32_t L = (uint32_t)redo.size();
-    if (hipMalloc(&dmap, (size_t)L * 4) != hipSuccess) return FX_ERR_HIP;
-    const size_t sb = fx_batch_state_bytes(tier, in->n, L);
-    if (tier == 2 && hipMalloc(&dstate, sb) != hipSuccess) {
-      (void)hipFree(dmap);
+    if (!whole && !(dmap = (uint32_t*)scratch(SCRATCH_TIERED_MAP, (size_t)L * 4))) return FX_ERR_HIP;
+    if ((tier == FX_TIER_GLOBAL || tier == FX_TIER_SPLIT) &&
+        !(dstate = scratch(SCRATCH_TIERED_STATE, fx_batch_state_bytes(tier, in->n, L))))
       return FX_ERR_HIP;
-    }
-    (void)hipMemcpyAsync(dmap, redo.data(), (size_t)L * 4, hipMemcpyHostToDevice, hs);
+    if (dmap) (void)hipMemcpyAsync(dmap, todo.data(), (size_t)L * 4, hipMemcpyHostToDevice, hs);
     st = fx_batch_execute(in, out, tier, dmap, L, dstate, 0, in->steps, flags, nullptr, hip_stream);
-    if (!st) {
-      for (uint32_t x = 0; x < L; ++x)
-        (void)hipMemcpyAsync(&err[redo[x]], out->err + redo[x], 4, hipMemcpyDeviceToHost, hs);
-      if (hipStreamSynchronize(hs) != hipSuccess) st = FX_ERR_HIP;
-    }
-    (void)hipFree(dmap);
-    if (dstate) (void)hipFree(dstate);
+    if (!st && hipMemcpyAsync(err.data(), out->err, (size_t)S * 4, hipMemcpyDeviceToHost, hs) != hipSuccess)
+      st = FX_ERR_HIP;
+    if (!st && hipStreamSynchronize(hs) != hipSuccess) st = FX_ERR_HIP;
     if (st) return st;
+    std::vector<uint32_t> redo;
+    for (uint32_t x : todo)
+      if (err[x] == FX_ERR_CAPACITY) redo.push_back(x);
+    todo.swap(redo);
   }
-  for (uint32_t s = 0; s < S; ++s)
-    if (err[s]) return (int)err[s];
+  if (only) {
+    for (uint32_t x : *only)
+      if (err[x]) return (int)err[x];
+  } else {
+    for (uint32_t s = 0; s < S; ++s)
+      if (err[s]) return (int)err[s];
+  }
   return FX_OK;
+}
+
+}  // namespace fx
+
+extern "C" {
+
+int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags,
+                        void* hip_stream, uint32_t* tier_counts) {
+  return fx::run_tiered(in, out, flags, hip_stream, nullptr, tier_counts);
 }
 
 }  // extern "C"

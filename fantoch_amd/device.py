@@ -33,6 +33,9 @@ class DeviceBuffer:
     def zero(self, stream=None):
         check(_lib.load().fx_dev_memset(self.ptr, 0, self.nbytes, stream), "fx_dev_memset")
 
+    def fill_bytes(self, value, stream=None):
+        check(_lib.load().fx_dev_memset(self.ptr, value, self.nbytes, stream), "fx_dev_memset")
+
     def free(self):
         if self.ptr:
             _lib.load().fx_dev_free(self.ptr)
@@ -50,7 +53,7 @@ def device_count():
 
 
 class BatchResult:
-    def __init__(self, order, release, nexec, err, chain, delay, tier_counts, status):
+    def __init__(self, order, release, nexec, err, chain, delay, tier_counts, status, cut_stats=None):
         self.order = order
         self.release = release
         self.nexec = nexec
@@ -59,12 +62,14 @@ class BatchResult:
         self.delay = delay
         self.tier_counts = tier_counts
         self.status = status
+        self.cut_stats = cut_stats
 
 
 def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096, tiered=True,
-              tier=None, init_frontier=None, metrics=True):
+              tier=None, init_frontier=None, metrics=True, cut=False):
     """Runs a host batch on the GPU; returns host outputs (BatchResult).
 
+    cut: fx_batch_run_cut (quiescent-cut decomposition, for huge streams);
     tiered: fx_batch_run_tiered starting at `tier` (None = FX_TIER_DEFAULT);
     otherwise one fx_batch_execute launch at `tier` (None = FX_TIER_DEFAULT)."""
     lib = _lib.load()
@@ -80,6 +85,7 @@ def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096,
         lengths.upload(np.asarray(planes.lengths, np.uint32))
     order = DeviceBuffer(pw * 4)
     release = DeviceBuffer(pw * 4)
+    release.fill_bytes(0xFF)  # rows a stream never reaches (an error) stay FX_RELEASE_NONE
     nexec = DeviceBuffer(S * 4)
     err = DeviceBuffer(S * 4)
     inb = _lib.StreamBatch(bufs["dot"].ptr, bufs["hdr"].ptr, bufs["deps"].ptr,
@@ -87,7 +93,12 @@ def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096,
     outb = _lib.OrderBatch(order.ptr, release.ptr, nexec.ptr, err.ptr)
     flags = _lib.FX_FLAG_EXECUTE_AT_COMMIT if execute_at_commit else 0
     tier_counts = (ctypes.c_uint32 * _lib.FX_NUM_TIERS)()
-    if tiered and init_frontier is None:
+    cut_stats = None
+    if cut:
+        cut_stats = _lib.CutStats()
+        status = lib.fx_batch_run_cut(ctypes.byref(inb), ctypes.byref(outb), flags, None,
+                                      ctypes.byref(cut_stats))
+    elif tiered and init_frontier is None:
         tflags = flags | (_lib.first_tier_flag(tier) if tier is not None else 0)
         status = lib.fx_batch_run_tiered(ctypes.byref(inb), ctypes.byref(outb), tflags, None, tier_counts)
     else:
@@ -118,5 +129,5 @@ def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096,
         delay = hd.download(np.uint64, nbins_delay)
     res = BatchResult(order.download(np.uint32, pw), release.download(np.uint32, pw),
                       nexec.download(np.uint32, S), err.download(np.uint32, S),
-                      chain, delay, list(tier_counts), status)
+                      chain, delay, list(tier_counts), status, cut_stats)
     return res

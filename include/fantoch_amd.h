@@ -206,6 +206,30 @@ int fx_batch_metrics(const fx_stream_batch* in, const fx_order_batch* out,
 int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out,
                         uint32_t flags, void* hip_stream, uint32_t* tier_counts);
 
+/* Quiescent-cut driver for huge streams (BASELINE configs[4]): every stream is
+ * split after each step t whose prefix is dependency-closed (every dep of an
+ * Add at a step <= t was added at a step <= t); there the reference's
+ * DependencyGraph (graph/mod.rs:213-642) has executed the whole prefix and
+ * holds nothing pending, so each segment runs from an empty graph with its
+ * prefix deps dropped and its dots renumbered per source (order-preserving).
+ * All segments run as one batch through fx_batch_run_tiered and map back.
+ * A stream without a usable decomposition (a dep that never arrives, a
+ * segment over 256 steps, a double index, an index-only record) or whose
+ * segments do not all execute completely runs whole through
+ * fx_batch_run_tiered.  Output planes are identical to fx_batch_run_tiered's.
+ * Synchronous; device pointers. */
+typedef struct fx_cut_stats {
+  uint64_t segments;                    /* segments executed as independent streams */
+  uint32_t max_segment;                 /* longest segment (steps)                  */
+  uint32_t whole_streams;               /* streams run whole (all reasons)          */
+  uint32_t failed_streams;              /* ... of which because a segment did not
+                                           execute completely (capacity, or the cut
+                                           argument failing: never seen so far)     */
+  uint32_t tier_counts[8];              /* segment-batch streams run per tier       */
+} fx_cut_stats;
+int fx_batch_run_cut(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
+                     fx_cut_stats* stats);
+
 /* --------------------------------------- synthetic Atlas/EPaxos streams */
 /* Commit streams of `instances` independent simulated instances; instance i
  * has n processes, each coordinating cmds_per_process commands; conflict rate

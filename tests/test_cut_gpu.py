@@ -1,0 +1,96 @@
+"""Quiescent-cut driver (fx_batch_run_cut) vs the CPU oracle, bit for bit:
+order plane, release plane, nexec, status and both histograms.  GPU only.
+
+The driver splits each stream at its dependency-closed prefixes and runs the
+segments as one batch (graph_cut.hip); a stream it cannot split runs whole.
+Either way the outputs must equal the oracle's on the unsplit stream."""
+import time
+
+import numpy as np
+import pytest
+
+from fantoch_amd import _lib
+from fantoch_amd import device as fd
+from fantoch_amd import streams as fs
+from oracle import oracle_lib
+from test_gpu_parity import assert_parity, oracle_hists
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", [
+    dict(n=5, instances=8, cmds=400, window=8, cycle_pct=30, conflicts=(2, 50, 100)),
+    dict(n=3, instances=16, cmds=300, window=6, cycle_pct=60, conflicts=(10, 100)),
+    # long SCC chains: segments over 256 steps send streams to the whole path
+    dict(n=7, instances=4, cmds=200, window=16, cycle_pct=60, conflicts=(100,), whole_ok=True),
+    dict(n=5, instances=8, cmds=200, window=0, cycle_pct=0, conflicts=(0, 100)),
+    dict(n=2, instances=33, cmds=77, window=5, cycle_pct=40, conflicts=(50,)),
+])
+def test_cut_matches_oracle(case):
+    case = dict(case)
+    whole_ok = case.pop("whole_ok", False)
+    p = fs.synth_params(seed=11, **case)
+    planes = fs.synth_host(p)
+    res = fd.run_batch(planes, cut=True, nbins_chain=64, nbins_delay=4096)
+    assert res.status == _lib.FX_OK
+    o_order, o_rel, o_nexec = assert_parity(planes, res)
+    chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 64, 4096)
+    assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
+    st = res.cut_stats
+    assert st.failed_streams == 0
+    assert whole_ok or (st.whole_streams == 0 and st.segments > planes.S)
+
+
+def test_cut_ragged_lengths():
+    """Ragged stream lengths (an empty stream among them): a truncated stream
+    whose last Adds wait on dots past its end has no final cut and runs whole."""
+    p = fs.synth_params(seed=5, instances=12, n=5, cmds=120, window=8, cycle_pct=30, conflicts=(2, 50, 100))
+    planes = fs.synth_host(p)
+    rng = np.random.default_rng(3)
+    lengths = rng.integers(0, planes.steps + 1, planes.S).astype(np.uint32)
+    lengths[0] = 0
+    lengths[1] = planes.steps
+    planes.lengths = lengths
+    res = fd.run_batch(planes, cut=True)
+    assert res.status == _lib.FX_OK
+    assert_parity(planes, res)
+
+
+def test_cut_unsplittable_and_errors():
+    """A dep that never arrives (no final cut: the stream runs whole) and a
+    double index (runs whole, FX_ERR_DOUBLE_INDEX as with the tiered driver)."""
+    n = 3
+    streams = [
+        [((1, 1), [], 1), ((2, 1), [(3, 9)], 2), ((1, 2), [(2, 1)], 3), ((3, 1), [], 4)],  # (3, 9) never arrives
+        [((1, 1), [(3, 5)], 1), ((2, 1), [(1, 1)], 2), ((1, 1), [], 3)],  # double index of a pending dot
+        [((1, 1), [(2, 1)], 1), ((2, 1), [(1, 1)], 2), ((3, 1), [(1, 1), (2, 1)], 3)],  # a 2-cycle, then a cut
+        [],
+    ]
+    planes = fs.pack_streams(streams, n)
+    res = fd.run_batch(planes, cut=True)
+    ref = fd.run_batch(planes)
+    assert np.array_equal(res.err, ref.err) and np.array_equal(res.nexec, ref.nexec)
+    assert res.err[1] == _lib.FX_ERR_DOUBLE_INDEX and res.err[0] == _lib.FX_OK
+    assert res.cut_stats.whole_streams == 2
+    assert_parity(planes, res)
+
+
+def test_config4_single_huge_instance_cut():
+    """BASELINE configs[4]: one instance, five executors each fed a
+    10^6-Add commit stream with cycles; bit-exact with the oracle and timed
+    against it."""
+    p = fs.synth_params(seed=2025, instances=1, n=5, cmds=200_000, window=8, cycle_pct=30, conflicts=(2,))
+    planes = fs.synth_host(p)
+    fd.run_batch(planes, cut=True, metrics=False)  # warm-up (module load, allocations)
+    t0 = time.time()
+    res = fd.run_batch(planes, cut=True, nbins_chain=64, nbins_delay=2048)
+    t_gpu = time.time() - t0
+    assert res.status == _lib.FX_OK and res.cut_stats.whole_streams == 0
+    t0 = time.time()
+    o_order, o_rel, o_nexec = assert_parity(planes, res)
+    t_cpu = time.time() - t0
+    assert np.all(res.nexec == planes.steps)
+    chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 64, 2048)
+    assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
+    print("configs[4]: GPU cut driver %.3f s (incl. host<->device copies), oracle+compare %.3f s, "
+          "%d segments, longest %d" % (t_gpu, t_cpu, res.cut_stats.segments, res.cut_stats.max_segment))
