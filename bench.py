@@ -44,7 +44,7 @@ LAYOUT = {0: "16 lanes per stream", 1: "one lane per stream", 2: "one lane per s
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["sim", "executor", "huge"], default="sim",
+    ap.add_argument("--mode", choices=["sim", "executor", "huge", "placements"], default="sim",
                     help="sim: the batched simulator (BASELINE configs[1], the headline); "
                          "executor: the GraphExecutor alone over synthetic commit streams")
     ap.add_argument("--gpus", type=int, default=1)
@@ -65,11 +65,17 @@ def parse(argv=None):
                     help="instances per conflict rate block (-1 = --seeds: conflict-major "
                          "enumeration, so a wavefront's streams share a rate; 0 = seed-major)")
     ap.add_argument("--tier", type=int, default=-1, help="executor tier (-1 = FX_TIER_DEFAULT)")
-    ap.add_argument("--ring-entries", type=int, default=16, help="sim: messages in flight per link")
-    ap.add_argument("--dot-slots", type=int, default=8, help="sim: live dots per coordinator")
+    ap.add_argument("--ring-entries", type=int, default=0,
+                    help="sim: messages in flight per instance (pool shared by the links; 0 = min(4096, 64 n))")
+    ap.add_argument("--dot-slots", type=int, default=0,
+                    help="sim: live dots per instance (pool shared by the coordinators; 0 = min(64, 8 n))")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=None,
                     help="CPU work budget of the cpu_baseline sample (sim default 15, executor 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--placement-conflict", type=int, default=2,
+                    help="placements mode (BASELINE configs[2]): conflict rate of every placement")
+    ap.add_argument("--placement-limit", type=int, default=None,
+                    help="placements mode: run only the first K placements of the enumeration")
     ap.add_argument("--traffic-json", type=str, default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args(argv)
 
@@ -119,6 +125,9 @@ def main():
     if args.mode == "huge":
         from bench_huge import main_huge
         return main_huge(args)
+    if args.mode == "placements":
+        from bench_placements import main_placements
+        return main_placements(args)
     if args.cmds is None:
         args.cmds = 1000
     if args.cpu_baseline_seconds is None:

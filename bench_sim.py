@@ -101,7 +101,7 @@ def main_sim(args):
         lat_hist.zero_()
         chain.zero_()
         delay.zero_()
-        _lib.check(lib.fx_sim_run(ctypes.byref(batch), ctypes.byref(out), hs), "fx_sim_run")
+        _lib.check(lib.fx_sim_run_tiered(ctypes.byref(batch), ctypes.byref(out), hs, None), "fx_sim_run_tiered")
 
     for _ in range(max(args.warmup, 1)):
         step()
@@ -121,7 +121,7 @@ def main_sim(args):
         chain.zero_()
         delay.zero_()
         ev0.record(stream)
-        _lib.check(lib.fx_sim_run(ctypes.byref(batch), ctypes.byref(out), hs), "fx_sim_run")
+        _lib.check(lib.fx_sim_run_tiered(ctypes.byref(batch), ctypes.byref(out), hs, None), "fx_sim_run_tiered")
         ev1.record(stream)
         ev1.synchronize()
         kernel_ms.append(ev0.elapsed_time(ev1))

@@ -36,6 +36,8 @@ FX_SIM_FLAG_EXEC_NOTIFICATIONS = 1
 FX_SIM_STAT_FAST, FX_SIM_STAT_SLOW, FX_SIM_STAT_STABLE = 0, 8, 16
 FX_SIM_STAT_EVENTS, FX_SIM_STAT_END_MS, FX_SIM_STAT_TRACE, FX_SIM_STAT_SEQ = 24, 25, 26, 27
 FX_SIM_STAT_DEPS = 28
+FX_SIM_STAT_LAT_SUM = 29
+FX_SIM_STAT_ERR_SITE = 30
 FX_SIM_STATS = 32
 
 FX_SEQ_BITS = 24
@@ -227,6 +229,8 @@ SIGNATURES = [
      [ctypes.POINTER(SimSpec), ctypes.c_uint32, ctypes.c_uint32, u32p]),
     ("fx_sim_run", ctypes.c_int,
      [ctypes.POINTER(SimBatch), ctypes.POINTER(SimOutput), ctypes.c_void_p]),
+    ("fx_sim_run_tiered", ctypes.c_int,
+     [ctypes.POINTER(SimBatch), ctypes.POINTER(SimOutput), ctypes.c_void_p, u32p]),
     ("fx_planet_load", ctypes.c_int,
      [ctypes.c_char_p, ctypes.c_uint32, u32p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p,
       ctypes.c_void_p]),

@@ -63,6 +63,7 @@ constexpr uint32_t FMAX = 12;            // frame stack depth
 constexpr uint32_t RDMAX = 16;           // ready results per frame
 constexpr uint32_t HMAX = 2;             // link heads per lane (links <= 128; a template parameter)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t LNIL = 0xFFFFu;  // end of a link's message list
 
 // FX_SIM_PROFILE builds (make prof): shader-clock cycles per event phase in
 // the stats rows (slots 0-15 cycles, 16-23 counts) instead of the counters
@@ -83,7 +84,8 @@ enum : uint32_t { PH_IDLE = 0, PH_DFS = 1, PH_TRY = 2, PH_CHECK = 3 };
 
 // dot-table slot (u32 words): fixed header, then (per-launch sizes, Geo)
 // collect deps [K] | value [vmax] | ack deps [n][amax]
-constexpr uint32_t SL_DOT = 0, SL_CLIENT = 1, SL_IDX = 2, SL_KEYS = 3, SL_PST = 4,  // 4,5: per-process state bytes
+constexpr uint32_t SL_CLIENT = 1,  // word 0 spare (the slot's dot lives in lane `slot`, sdv)
+    SL_IDX = 2, SL_KEYS = 3, SL_PST = 4,  // 4,5: per-process state bytes
     SL_MASKS = 6, SL_CNT = 7, SL_COLLECT = 8;
 // per-process state byte: status(2) | buffered commit(1) | accepted(1) | buffered-from(4)
 // SL_MASKS: participants(8) | proposer accepts(8) | committed count(8) | executed count(8)
@@ -93,7 +95,7 @@ constexpr uint32_t SL_DOT = 0, SL_CLIENT = 1, SL_IDX = 2, SL_KEYS = 3, SL_PST = 
 struct Geo {  // launch-uniform geometry
   uint32_t n, C, K, W, R, L, NP, ncli_keys, rt, rc;
   uint32_t amax, vmax, sl_value, sl_ack, slotw;  // dot-slot layout (MCollectAck deps <= 2K, value <= K(n+1))
-  uint32_t off_ring, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_frame, off_wl, words;
+  uint32_t off_pool, off_free, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_frame, off_wl, words;
 };
 
 struct SimArgs {
@@ -162,7 +164,7 @@ __device__ __forceinline__ uint32_t tep(uint32_t t) { return t >> 14; }
 __device__ __forceinline__ uint32_t tmk(uint32_t id, uint32_t low, uint32_t ep) { return id | (low << 7) | (ep << 14); }
 constexpr uint32_t EPOCH_MAX = 0xFFFFu;
 
-template <uint32_t HM>
+template <uint32_t HM, uint32_t DS>
 struct Sim {
   // ---------------------------------------------------------------- context
   uint32_t lid;
@@ -176,9 +178,14 @@ struct Sim {
   bool has_extra;
   uint32_t C;
   uint32_t err = 0;
+  uint32_t err_site = 0;  // source line of the first capacity failure (diagnostics)
+  __device__ __forceinline__ void fail_cap(uint32_t line) {
+    if (!err) err_site = line;
+    err = FX_ERR_SIM_CAPACITY;
+  }
   uint32_t now = 0;       // ms
   uint32_t seq = 0;       // insertion counter (C3)
-  uint64_t events = 0, trace = 0, deps_total = 0;
+  uint64_t events = 0, trace = 0, deps_total = 0, lat_sum = 0;
   uint32_t clients_done = 0;
   bool done = false, in_extra = false;
   uint32_t final_ms = 0;
@@ -202,7 +209,9 @@ struct Sim {
   // kind << 2 | targets << 8 | next target << 16 | ready results << 20; dot
   uint32_t frw = 0, frd = 0;
   // message ring of process link l (< n (n - 1) <= 56): head | tail << 16 in lane l
-  uint32_t rhv = 0;
+  uint32_t rhv = 0xFFFFFFFFu;
+  uint32_t nfree = 0;  // free message-pool entries (a stack of indices in LDS)
+  uint32_t sdv[DS];  // dot of dot-table slot 64 k + lane in sdv[k] (0 = free)
   // executed clocks of the executors: lane 8 p + s = source s + 1 at process p
   uint32_t ecf = 0, ecw = 0;
 
@@ -219,16 +228,42 @@ struct Sim {
 
   // ------------------------------------------------------------ LDS views
   __device__ __forceinline__ uint32_t& W(uint32_t i) { return lds[i]; }
-  __device__ __forceinline__ uint32_t& ring(uint32_t link, uint32_t e, uint32_t w) {
-    return lds[g.off_ring + (link * g.R + e) * 3 + w];
+  // message pool entry e: time | kind << 28, insertion seq, dot, next entry of its link
+  __device__ __forceinline__ uint32_t& msg(uint32_t e, uint32_t w) {
+    return lds[g.off_pool + e * 4 + w];
   }
   // GC logs of (process p, source s): tick log entry i = (tick count, frontier
   // before the change), change log entry i = (time, frontier after)
   __device__ __forceinline__ uint32_t* gct(uint32_t p, uint32_t s) { return &lds[g.off_gct + (p * g.n + s) * g.rt * 2]; }
   __device__ __forceinline__ uint32_t* gcc(uint32_t p, uint32_t s) { return &lds[g.off_gcc + (p * g.n + s) * g.rc * 2]; }
   __device__ __forceinline__ uint32_t* gcr(uint32_t p, uint32_t s) { return &lds[g.off_gcr + (p * g.n + s) * 4]; }
-  __device__ __forceinline__ uint32_t slot_of(uint32_t d) const {
-    return ((d >> FX_SEQ_BITS) - 1u) * g.W + (d & (g.W - 1u));
+  // dot table: a pool of g.W <= 64 DS slots shared by every coordinator of
+  // the instance (a coordinator far ahead of a lagging replica holds many live
+  // dots); slot 64 k + l is lane l of sdv[k]; look-up = DS ballots
+  __device__ __forceinline__ uint32_t slot_find(uint32_t d) const {
+    uint32_t r = NONE;
+#pragma unroll
+    for (uint32_t k = 0; k < DS; ++k) {
+      const uint64_t m = bal(sdv[k] == d && d != 0u);
+      if (m && r == NONE) r = k * 64u + ctz64(m);
+    }
+    return r;
+  }
+  __device__ __forceinline__ void slot_set(uint32_t sl, uint32_t d) {
+#pragma unroll
+    for (uint32_t k = 0; k < DS; ++k)
+      if ((sl >> 6) == k && lid == (sl & 63u)) sdv[k] = d;
+  }
+  __device__ __forceinline__ uint32_t slot_alloc() const {
+#pragma unroll
+    for (uint32_t k = 0; k < DS; ++k) {
+      const uint32_t lo = k * 64u;
+      if (lo >= g.W) break;
+      const uint64_t pool = g.W - lo >= 64u ? ~0ull : ((1ull << (g.W - lo)) - 1ull);
+      const uint64_t fre = ~bal(sdv[k] != 0u) & pool;
+      if (fre) return lo + ctz64(fre);
+    }
+    return NONE;
   }
   __device__ __forceinline__ uint32_t& S(uint32_t sl, uint32_t w) { return lds[g.off_slot + sl * g.slotw + w]; }
   // GC deliveries p -> q: base insertion seq of p's tick k (the tick's sends
@@ -289,22 +324,28 @@ struct Sim {
   __device__ __forceinline__ void send_p_(uint32_t from, uint32_t to, uint32_t kind, uint32_t w2) {  // 0-based processes
     const uint32_t link = link_p(from, to);
     const uint32_t t = now + rl(dpq, from * 8u + to);
-    const uint32_t ht_ = rl(rhv, link);
-    const uint32_t head = ht_ & 0xFFFFu, tail = ht_ >> 16;
-    if (((tail - head) & 0xFFFFu) >= g.R) {
-      err = FX_ERR_SIM_CAPACITY;
+    if (nfree == 0) {
+      fail_cap(__LINE__);
       return;
     }
-    const uint32_t e = tail & (g.R - 1u);
     if (t >= (1u << 28)) {
       err = FX_ERR_TIME_RANGE;
       return;
     }
-    put(ring(link, e, 0), t | (kind << 28));
-    put(ring(link, e, 1), seq);
-    put(ring(link, e, 2), w2);
-    lset(rhv, link, head | (((tail + 1u) & 0xFFFFu) << 16));
-    if (head == tail) head_set(link, t, seq);
+    const uint32_t e = uni(lds[g.off_free + --nfree]);
+    put(msg(e, 0), t | (kind << 28));
+    put(msg(e, 1), seq);
+    put(msg(e, 2), w2);
+    put(msg(e, 3), LNIL);
+    const uint32_t ht_ = rl(rhv, link);
+    const uint32_t head = ht_ & 0xFFFFu, tail = ht_ >> 16;
+    if (head == LNIL) {
+      lset(rhv, link, e | (e << 16));
+      head_set(link, t, seq);
+    } else {
+      put(msg(tail, 3), e);
+      lset(rhv, link, head | (e << 16));
+    }
     ++seq;
   }
 
@@ -336,7 +377,7 @@ struct Sim {
       if (nk == 0) { k0 = key; nk = 1; }
       else if (key != k0) { k1 = key; nk = 2; }
     }
-    if (nk != g.K) err = FX_ERR_SIM_CAPACITY;
+    if (nk != g.K) fail_cap(__LINE__);
     if (nk == 2 && k1 < k0) { const uint32_t t = k0; k0 = k1; k1 = t; }  // C11
     return k0 | (k1 << 16);
   }
@@ -396,14 +437,14 @@ struct Sim {
     lset(pseq, p, s);
     if (s > FX_SEQ_MASK) { err = FX_ERR_DOT_RANGE; return; }
     const uint32_t dot = FX_PACK_DOT(p + 1, s);
-    const uint32_t sl = slot_of(dot);
-    if (uni(S(sl, SL_DOT)) != 0) { err = FX_ERR_SIM_CAPACITY; return; }
+    const uint32_t sl = slot_alloc();
+    if (sl == NONE) { fail_cap(__LINE__); return; }
     const uint32_t idx = rl(ciss, c) - 1u;
     uint32_t nk = 0;
     const uint32_t keys = gen_keys(c + 1, idx, nk);
     // fresh slot
     if (lid < g.slotw) S(sl, lid) = 0;
-    put(S(sl, SL_DOT), dot);
+    slot_set(sl, dot);
     put(S(sl, SL_CLIENT), c);
     put(S(sl, SL_IDX), idx);
     put(S(sl, SL_KEYS), keys);
@@ -416,8 +457,8 @@ struct Sim {
 
   // atlas.rs:251-325 / epaxos.rs:223-301
   __device__ __forceinline__ void h_mcollect(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
-    if (uni(S(sl, SL_DOT)) != dot) { err = FX_ERR_SIM_LATE; return; }
+    const uint32_t sl = slot_find(dot);
+    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
     const uint32_t ps = pst(sl, p);
     if ((ps & 3u) != ST_START) return;
     const uint32_t src = (dot >> FX_SEQ_BITS) - 1u;
@@ -441,7 +482,7 @@ struct Sim {
     } else {
       nd = add_cmd(p, dot, uni(S(sl, SL_KEYS)), nk, colv, ncol, depv);
     }
-    if (nd > g.amax) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (nd > g.amax) { fail_cap(__LINE__); return; }
     set_pst(sl, p, (ps & ~3u) | ST_COLLECT);
     // the ack's deps travel in the slot: ack deps of p
     if (lid < g.amax) S(sl, g.sl_ack + p * g.amax + lid) = lid < nd ? depv : 0u;
@@ -451,8 +492,8 @@ struct Sim {
 
   // atlas.rs:327-402 / epaxos.rs:303-368
   __device__ __forceinline__ void h_mcollectack(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
-    if (uni(S(sl, SL_DOT)) != dot) { err = FX_ERR_SIM_LATE; return; }
+    const uint32_t sl = slot_find(dot);
+    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
     if ((pst(sl, p) & 3u) != ST_COLLECT) return;
     const uint32_t masks = uni(S(sl, SL_MASKS));
     const uint32_t part = (masks & 0xFFu) | (1u << from);
@@ -480,7 +521,7 @@ struct Sim {
     }
     const uint64_t um = bal(first);  // one lane per distinct dep
     const uint32_t nu = pop64(um);
-    if (nu > g.vmax) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (nu > g.vmax) { fail_cap(__LINE__); return; }
     bool fast;
     if (protocol == FX_PROTOCOL_ATLAS) {
       // threshold = |quorum| - minority (atlas.rs:361-368)
@@ -510,8 +551,8 @@ struct Sim {
 
   // atlas.rs:404-475 / epaxos.rs:370-428
   __device__ __forceinline__ void h_mcommit(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
-    if (uni(S(sl, SL_DOT)) != dot) { err = FX_ERR_SIM_LATE; return; }
+    const uint32_t sl = slot_find(dot);
+    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
     const uint32_t ps = pst(sl, p);
     if ((ps & 3u) == ST_START) {  // buffered_commits.insert
       set_pst(sl, p, (ps & 0x0Bu) | 4u | (from << 4));
@@ -530,8 +571,8 @@ struct Sim {
 
   // atlas.rs:477-524 / epaxos.rs:430-477
   __device__ __forceinline__ void h_mconsensus(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
-    if (uni(S(sl, SL_DOT)) != dot) { err = FX_ERR_SIM_LATE; return; }
+    const uint32_t sl = slot_find(dot);
+    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
     const uint32_t ps = pst(sl, p);
     if ((ps & 3u) == ST_COMMIT) {  // chosen: reply with the chosen value
       act_send(M_COMMIT, dot, 1u << from);
@@ -543,8 +584,8 @@ struct Sim {
 
   // atlas.rs:526-558 / epaxos.rs:479-517
   __device__ __forceinline__ void h_mconsensusack(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
-    if (uni(S(sl, SL_DOT)) != dot) { err = FX_ERR_SIM_LATE; return; }
+    const uint32_t sl = slot_find(dot);
+    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
     if (!((uni(S(sl, SL_CNT)) >> 16) & 1u)) return;  // proposer ballot != b
     const uint32_t masks = uni(S(sl, SL_MASKS));
     const uint32_t acc = ((masks >> 8) & 0xFFu) | (1u << from);
@@ -612,7 +653,7 @@ struct Sim {
         }
       }
     }
-    if (bal(bad)) err = FX_ERR_SIM_CAPACITY;
+    if (bal(bad)) fail_cap(__LINE__);
   }
 
   // frontier of source s at p reported by tick k; false if the log lost it
@@ -707,7 +748,7 @@ struct Sim {
             cur = min(cur, v);
           }
         }
-        if (bal(lid < n && !ok)) err = FX_ERR_SIM_CAPACITY;
+        if (bal(lid < n && !ok)) fail_cap(__LINE__);
         for (uint32_t s2 = 0; s2 < n; ++s2) stable += rl(cur, s2);
       }
       if (st && lid == 0) st[FX_SIM_STAT_STABLE + q] = stable;
@@ -716,8 +757,8 @@ struct Sim {
 
   // ===================================================== GraphExecutor
   __device__ __forceinline__ bool mine(uint64_t m) const { return (m & lbit) != 0; }
-  __device__ __forceinline__ uint32_t vcount_of(uint32_t d) { return uni(S(slot_of(d), SL_CNT)) & 0xFFu; }
-  __device__ __forceinline__ uint32_t value_at(uint32_t d, uint32_t j) { return uni(S(slot_of(d), g.sl_value + j)); }
+  __device__ __forceinline__ uint32_t vcount_of(uint32_t d) { return uni(S(slot_find(d), SL_CNT)) & 0xFFu; }
+  __device__ __forceinline__ uint32_t value_at(uint32_t d, uint32_t j) { return uni(S(slot_find(d), g.sl_value + j)); }
 
   __device__ __forceinline__ void x_load(uint32_t p) {
     xp = p;
@@ -768,7 +809,7 @@ struct Sim {
     const uint32_t sq = d & FX_SEQ_MASK;
     if (sq <= fr) return;
     const uint32_t off = sq - fr - 1u;
-    if (off >= 32u) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (off >= 32u) { fail_cap(__LINE__); return; }
     if (off != 0) {
       w |= 1u << off;
     } else {
@@ -803,8 +844,8 @@ struct Sim {
     ++xk;
     const uint32_t delay = now - start;  // ExecutionDelay (graph/mod.rs:514-518)
     if (lid == 0 && A.delay_hist) atomicAdd(&A.delay_hist[min(delay, A.delay_bins - 1u)], 1ull);
-    const uint32_t sl = slot_of(d);
-    if (uni(S(sl, SL_DOT)) != d) { err = FX_ERR_SIM_LATE; return; }
+    const uint32_t sl = slot_find(d);
+    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
     const uint32_t c = uni(S(sl, SL_CLIENT));
     const uint32_t nk = (uni(S(sl, SL_CNT)) >> 20) & 3u;
     if ((rl(cpr, c) & 0xFFu) == p) {  // pending.wait_for registered this rifl at p
@@ -815,14 +856,14 @@ struct Sim {
         const uint32_t fi = nfrm - 1;
         const uint32_t w = rl(frw, fi);
         const uint32_t nr = (w >> 20) & 31u;
-        if (nr >= RDMAX) { err = FX_ERR_SIM_CAPACITY; return; }
+        if (nr >= RDMAX) { fail_cap(__LINE__); return; }
         put(FRR(fi, nr), c);
         lset(frw, fi, w + (1u << 20));
       }
     }
     const uint32_t masks = uni(S(sl, SL_MASKS));
     if (((masks >> 24) & 0xFFu) + 1u == n) {
-      put(S(sl, SL_DOT), 0u);  // executed everywhere: free the slot
+      slot_set(sl, 0u);  // executed everywhere: free the slot
     } else {
       put(S(sl, SL_MASKS), masks + (1u << 24));
     }
@@ -836,7 +877,7 @@ struct Sim {
 
   __device__ __forceinline__ int insert_vertex(uint32_t d) {
     const uint64_t fre = ~occ;
-    if (!fre) { err = FX_ERR_SIM_CAPACITY; return -1; }
+    if (!fre) { fail_cap(__LINE__); return -1; }
     const uint32_t sl = ctz64(fre);
     if (lid == sl) {
       sdot = d;
@@ -870,7 +911,7 @@ struct Sim {
     const bool mem = mine(occ) && tid(stl) >= idv;
     const uint64_t mm = bal(mem);
     const uint32_t cnt = pop64(mm);
-    if (nwl + cnt > 65u) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (nwl + cnt > 65u) { fail_cap(__LINE__); return; }
     if (lid == 0 && A.chain_hist) atomicAdd(&A.chain_hist[min(cnt, A.chain_bins - 1u)], 1ull);
     uint32_t rank = 0;
     for (uint64_t m = mm; m; m &= m - 1) rank += rl(sdot, ctz64(m)) < sdot ? 1u : 0u;
@@ -923,7 +964,7 @@ struct Sim {
       const uint32_t tx = rl(stl, (uint32_t)x);
       if (tid(tx) == 0) {  // recurse (tarjan.rs:172-214)
         ++idc;
-        if (idc > 127u) { err = FX_ERR_SIM_CAPACITY; return; }
+        if (idc > 127u) { fail_cap(__LINE__); return; }
         if (lid == (uint32_t)x) stl = tmk(idc, idc, tep(tx));
         if (lid == nfr) sfr = fv | (fdi << 8);
         ++nfr;
@@ -995,7 +1036,8 @@ struct Sim {
     if (find(d) >= 0) { err = FX_ERR_DOUBLE_INDEX; x_store(); return; }
     const uint32_t vc = vcount_of(d);
     deps_total += vc;
-    const uint32_t depj = lid < vc ? S(slot_of(d), g.sl_value + lid) : 0u;
+    const uint32_t dsl = slot_find(d);
+    const uint32_t depj = lid < vc ? S(dsl, g.sl_value + lid) : 0u;
     const bool keep = lid < vc && depj != d && !contains_v(depj);
     if (!bal(keep)) {  // fast path: a singleton SCC
       emit_one(d, now);
@@ -1013,14 +1055,14 @@ struct Sim {
       if (phase == PH_DFS) dfs_iter();
       else if (phase == PH_TRY) try_iter();
       else check_iter();
-      if (++guard > (1u << 22)) err = FX_ERR_SIM_CAPACITY;
+      if (++guard > (1u << 22)) fail_cap(__LINE__);
     }
     x_store();
   }
 
   // =========================================== send_to_processes_and_executors
   __device__ __forceinline__ void frame_push() {
-    if (nfrm >= FMAX) { err = FX_ERR_SIM_CAPACITY; return; }
+    if (nfrm >= FMAX) { fail_cap(__LINE__); return; }
     const uint32_t fi = nfrm++;
     lset(frw, fi, 0);
     xinfo = 0;
@@ -1042,7 +1084,7 @@ struct Sim {
     bool pend = true;
     uint32_t guard = 0;
     while (!err) {
-      if (++guard > 4096u) { err = FX_ERR_SIM_CAPACITY; return; }
+      if (++guard > 4096u) { fail_cap(__LINE__); return; }
       if (pend) {
         pend = false;
         frame_push();
@@ -1120,16 +1162,15 @@ struct Sim {
       const uint32_t p = link / (g.n - 1u), qi = link % (g.n - 1u);
       const uint32_t q = qi < p ? qi : qi + 1u;
       const uint32_t ht_ = rl(rhv, link);
-      const uint32_t head = ht_ & 0xFFFFu, tail = ht_ >> 16;
-      const uint32_t e = head & (g.R - 1u);
-      const uint32_t w0 = uni(ring(link, e, 0)), w2 = uni(ring(link, e, 2));
+      const uint32_t e = ht_ & 0xFFFFu, tail = ht_ >> 16;
+      const uint32_t w0 = uni(msg(e, 0)), w2 = uni(msg(e, 2)), nx = uni(msg(e, 3));
       const uint32_t kind = w0 >> 28;
-      const uint32_t nh = (head + 1u) & 0xFFFFu;
-      lset(rhv, link, nh | (tail << 16));
-      if (nh != tail) {
-        const uint32_t e2 = nh & (g.R - 1u);
-        head_set(link, uni(ring(link, e2, 0)) & 0x0FFFFFFFu, uni(ring(link, e2, 1)));
+      put(lds[g.off_free + nfree++], e);
+      if (nx != LNIL) {
+        lset(rhv, link, nx | (tail << 16));
+        head_set(link, uni(msg(nx, 0)) & 0x0FFFFFFFu, uni(msg(nx, 1)));
       } else {
+        lset(rhv, link, 0xFFFFFFFFu);
         head_set(link, NONE, NONE);
       }
       note(3, q + 1, p + 1, ((uint64_t)kind << 32) | w2);
@@ -1159,6 +1200,7 @@ struct Sim {
       const uint32_t issued = rl(ciss, c);
       note(4, c + 1, 0, issued);
       const uint32_t lat = now - rl(cst, c);  // latency.as_millis()
+      lat_sum += lat;
       const uint32_t region = rl(cpr, c) >> 8;
       if (lid == 0) {
         if (A.latency_log && issued - 1u < A.lat_cap)
@@ -1215,12 +1257,14 @@ struct Sim {
   }
 };
 
-template <uint32_t HM>
-__global__ __launch_bounds__(64, 3) void k_sim(SimArgs a) {
+template <uint32_t HM, uint32_t DS>
+__global__ __launch_bounds__(64, DS == 1 ? 3 : 2) void k_sim(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
-  Sim<HM> s;
+  Sim<HM, DS> s;
+#pragma unroll
+  for (uint32_t k = 0; k < DS; ++k) s.sdv[k] = 0;
   s.lid = threadIdx.x;
   s.lbit = 1ull << s.lid;
   s.A = a;
@@ -1254,6 +1298,8 @@ __global__ __launch_bounds__(64, 3) void k_sim(SimArgs a) {
   }
   // ---------------------------------------------------------------- init
   for (uint32_t i = s.lid; i < a.g.words; i += 64) smem[i] = 0;
+  for (uint32_t i = s.lid; i < a.g.R; i += 64) smem[a.g.off_free + i] = a.g.R - 1u - i;  // free stack
+  s.nfree = a.g.R;
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (uint32_t k = 0; k < HM; ++k) s.ht[k] = s.hs[k] = NONE;
@@ -1377,6 +1423,8 @@ __global__ __launch_bounds__(64, 3) void k_sim(SimArgs a) {
       st[FX_SIM_STAT_TRACE] = s.trace;
       st[FX_SIM_STAT_SEQ] = s.seq;
       st[FX_SIM_STAT_DEPS] = s.deps_total;
+      st[FX_SIM_STAT_LAT_SUM] = s.lat_sum;
+      st[FX_SIM_STAT_ERR_SITE] = s.err_site;
     }
   }
   if (s.lid == 0) a.err[inst] = s.err;
@@ -1394,8 +1442,10 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   g.n = n;
   g.C = C;
   g.K = sp.keys_per_command;
-  g.W = wslots;
-  g.R = ring;
+  g.W = wslots ? wslots : 64u;  // live dots per instance
+  if (g.W > 256u) return false;
+  g.R = ring ? ring : std::min<uint32_t>(4096u, 64u * n);  // messages in flight per instance
+  if (g.R > 65534u) return false;
   g.NP = n * (n - 1);
   g.L = g.NP + n + 2 * C;
   if (g.L > 64 * HMAX) return false;
@@ -1410,7 +1460,9 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   g.slotw = g.sl_ack + n * g.amax;
   if (n * g.amax > 64 || g.slotw > 64) return false;
   uint32_t o = 0;
-  g.off_ring = o; o += g.NP * g.R * 3;
+  // messages in flight: one pool per instance, a FIFO list per process link
+  g.off_pool = o; o += g.R * 4;
+  g.off_free = o; o += g.R;
   // GC logs: 8 / 4 entries per client per region (commits of one source
   // arrive about once per client round trip)
   const uint32_t cpr = (C + n - 1) / n;
@@ -1420,7 +1472,7 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   g.off_gct = o; o += n * n * g.rt * 2;
   g.off_gcc = o; o += n * n * g.rc * 2;
   g.off_gcr = o; o += n * n * 4;
-  g.off_slot = o; o += n * g.W * g.slotw;
+  g.off_slot = o; o += g.W * g.slotw;
   g.off_kd = o; o += n * g.ncli_keys;
   g.off_frame = o; o += FMAX * RDMAX;
   g.off_wl = o; o += 72;
@@ -1447,9 +1499,9 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   if (b->instances == 0) return FX_OK;
   int dc = 0;
   if (hipGetDeviceCount(&dc) != hipSuccess || dc <= 0) return FX_ERR_NO_DEVICE;
-  const uint32_t ring = b->ring_entries ? b->ring_entries : 16u;
-  const uint32_t W = b->dot_slots ? b->dot_slots : 8u;
-  if ((ring & (ring - 1)) || ring > 4096 || (W & (W - 1)) || W > 256) return FX_ERR_INVALID_ARG;
+  const uint32_t ring = b->ring_entries;  // 0 = min(4096, 64 n)
+  const uint32_t W = b->dot_slots;  // 0 = min(64, 8 n)
+  if (ring > 65534 || W > 256) return FX_ERR_INVALID_ARG;
   const fx_sim_spec& s0 = b->host_specs[0];
   // every instance of a launch shares the geometry (protocol, n, clients, keys)
   for (uint32_t i = 0; i < b->instances; ++i) {
@@ -1498,16 +1550,170 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   a.err = o->err;
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     configured = true;
   }
   // link heads per lane: one when every link fits a lane
-  if (a.g.L <= 64)
-    hipLaunchKernelGGL(sim::k_sim<1>, dim3(b->instances), dim3(64), lds, (hipStream_t)hip_stream, a);
-  else
-    hipLaunchKernelGGL(sim::k_sim<2>, dim3(b->instances), dim3(64), lds, (hipStream_t)hip_stream, a);
+  // and one dot-table VGPR when the pool fits a lane each
+  const dim3 grid(b->instances), block(64);
+  hipStream_t hs = (hipStream_t)hip_stream;
+  if (a.g.W <= 64) {
+    if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 1>), grid, block, lds, hs, a);
+    else hipLaunchKernelGGL((sim::k_sim<2, 1>), grid, block, lds, hs, a);
+  } else {
+    if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 4>), grid, block, lds, hs, a);
+    else hipLaunchKernelGGL((sim::k_sim<2, 4>), grid, block, lds, hs, a);
+  }
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 
+// ------------------------------------------------------ escalation driver
+// Instances that outgrow the launch's message pool or dot table
+// (FX_ERR_SIM_CAPACITY) are rerun with larger tables.  Their histogram
+// contributions before the failure are removed exactly: the kernel is
+// deterministic per instance, so a rerun of just those instances at the
+// first geometry reproduces the same partial samples, which are subtracted.
+
 }  // extern "C"
+
+namespace fx {
+namespace sim {
+
+__global__ void k_hist_sub(unsigned long long* dst, const unsigned long long* src, uint32_t n) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] -= src[i];
+}
+template <typename T>
+__global__ void k_rows_scatter(T* dst, const T* src, const uint32_t* map, uint32_t rows, uint32_t width) {
+  const uint64_t total = (uint64_t)rows * width;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = t / width, c = t % width;
+    dst[(uint64_t)map[r] * width + c] = src[t];
+  }
+}
+
+struct Tmp {
+  std::vector<void*> ptrs;
+  ~Tmp() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  template <typename T>
+  T* alloc(size_t count, hipStream_t hs, bool zero) {
+    void* p = nullptr;
+    const size_t bytes = std::max<size_t>(count * sizeof(T), 8);
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    ptrs.push_back(p);
+    if (zero) (void)hipMemsetAsync(p, 0, bytes, hs);
+    return (T*)p;
+  }
+};
+
+}  // namespace sim
+}  // namespace fx
+
+extern "C" int fx_sim_run_tiered(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream,
+                                 uint32_t* reruns) {
+  if (reruns) *reruns = 0;
+  int st = fx_sim_run(b, o, hip_stream);
+  if (st || b->instances == 0) return st;
+  hipStream_t hs = (hipStream_t)hip_stream;
+  const uint32_t N = b->instances;
+  std::vector<uint32_t> err(N);
+  if (hipMemcpyAsync(err.data(), o->err, (size_t)N * 4, hipMemcpyDeviceToHost, hs) != hipSuccess ||
+      hipStreamSynchronize(hs) != hipSuccess)
+    return FX_ERR_HIP;
+  std::vector<uint32_t> fail;  // indices into the original batch
+  for (uint32_t i = 0; i < N; ++i)
+    if (err[i] == FX_ERR_SIM_CAPACITY) fail.push_back(i);
+  if (fail.empty()) return FX_OK;
+  Geo g0;
+  if (!sim_geometry(b->host_specs[0], b->ring_entries, b->dot_slots, g0)) return FX_ERR_UNSUPPORTED;
+  // geometries: the caller's, then a 4x (at least 256 n) message pool and 256 dot slots
+  const uint32_t geo_ring[2] = {b->ring_entries,
+                                std::min<uint32_t>(65534u, std::max<uint32_t>(4u * g0.R, 256u * g0.n))};
+  const uint32_t geo_dots[2] = {b->dot_slots, 256u};
+  const uint32_t C = b->host_specs[0].clients_per_region * b->host_specs[0].num_client_regions;
+  const uint32_t n = b->host_specs[0].n;
+  const size_t nh_lat = o->latency_hist ? (size_t)b->planet_regions * o->lat_bins : 0;
+  const size_t nh_chain = o->chain_hist ? o->chain_bins : 0, nh_delay = o->delay_hist ? o->delay_bins : 0;
+  for (uint32_t tier = 1; tier <= 2 && !fail.empty(); ++tier) {
+    Tmp tmp;
+    const uint32_t F = (uint32_t)fail.size();
+    std::vector<fx_sim_spec> sub(F);
+    for (uint32_t j = 0; j < F; ++j) sub[j] = b->host_specs[fail[j]];
+    fx_sim_spec* dspec = tmp.alloc<fx_sim_spec>(F, hs, false);
+    uint32_t* dmap = tmp.alloc<uint32_t>(F, hs, false);
+    uint32_t* terr = tmp.alloc<uint32_t>(F, hs, true);
+    uint64_t* nlat = tmp.alloc<uint64_t>(nh_lat, hs, true);
+    uint64_t* nchain = tmp.alloc<uint64_t>(nh_chain, hs, true);
+    uint64_t* ndelay = tmp.alloc<uint64_t>(nh_delay, hs, true);
+    if (!dspec || !dmap || !terr || !nlat || !nchain || !ndelay) return FX_ERR_HIP;
+    (void)hipMemcpyAsync(dspec, sub.data(), (size_t)F * sizeof(fx_sim_spec), hipMemcpyHostToDevice, hs);
+    (void)hipMemcpyAsync(dmap, fail.data(), (size_t)F * 4, hipMemcpyHostToDevice, hs);
+    // 1. replay the failed runs at the geometry they failed with: their partial
+    //    histogram samples, to subtract
+    fx_sim_batch nb = *b;
+    nb.specs = dspec;
+    nb.host_specs = sub.data();
+    nb.instances = F;
+    nb.ring_entries = geo_ring[tier - 1];
+    nb.dot_slots = geo_dots[tier - 1];
+    fx_sim_output no{};
+    no.latency_hist = o->latency_hist ? nlat : nullptr;
+    no.chain_hist = o->chain_hist ? nchain : nullptr;
+    no.delay_hist = o->delay_hist ? ndelay : nullptr;
+    no.err = terr;
+    no.lat_bins = o->lat_bins;
+    no.chain_bins = o->chain_bins;
+    no.delay_bins = o->delay_bins;
+    if ((st = fx_sim_run(&nb, &no, hip_stream))) return st;
+    const dim3 hg(64), hb(256);
+    if (nh_lat) hipLaunchKernelGGL(k_hist_sub, hg, hb, 0, hs, (unsigned long long*)o->latency_hist,
+                                   (const unsigned long long*)nlat, (uint32_t)nh_lat);
+    if (nh_chain) hipLaunchKernelGGL(k_hist_sub, hg, hb, 0, hs, (unsigned long long*)o->chain_hist,
+                                     (const unsigned long long*)nchain, (uint32_t)nh_chain);
+    if (nh_delay) hipLaunchKernelGGL(k_hist_sub, hg, hb, 0, hs, (unsigned long long*)o->delay_hist,
+                                     (const unsigned long long*)ndelay, (uint32_t)nh_delay);
+    if (tier == 2) {  // no larger geometry: these stay failed, without histogram samples
+      if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
+      break;
+    }
+    // 2. rerun them with larger tables into temporaries, histograms straight into the caller's
+    fx_sim_batch pb = nb;
+    pb.ring_entries = geo_ring[tier];
+    pb.dot_slots = geo_dots[tier];
+    fx_sim_output po = *o;
+    po.executed = o->executed ? tmp.alloc<uint32_t>((size_t)F * n * b->exec_cap, hs, false) : nullptr;
+    po.executed_len = o->executed_len ? tmp.alloc<uint32_t>((size_t)F * n, hs, true) : nullptr;
+    po.latency_log = o->latency_log && b->lat_cap ? tmp.alloc<uint32_t>((size_t)F * C * b->lat_cap, hs, false)
+                                                  : nullptr;
+    po.stats = o->stats ? tmp.alloc<uint64_t>((size_t)F * FX_SIM_STATS, hs, true) : nullptr;
+    po.err = tmp.alloc<uint32_t>(F, hs, true);
+    if (!po.err || (o->executed && !po.executed) || (o->executed_len && !po.executed_len) ||
+        (o->stats && !po.stats))
+      return FX_ERR_HIP;
+    if ((st = fx_sim_run(&pb, &po, hip_stream))) return st;
+    const dim3 sg(256), sb(256);
+    if (po.executed) hipLaunchKernelGGL(k_rows_scatter<uint32_t>, sg, sb, 0, hs, o->executed, po.executed, dmap, F,
+                                        n * b->exec_cap);
+    if (po.executed_len) hipLaunchKernelGGL(k_rows_scatter<uint32_t>, sg, sb, 0, hs, o->executed_len,
+                                            po.executed_len, dmap, F, n);
+    if (po.latency_log) hipLaunchKernelGGL(k_rows_scatter<uint32_t>, sg, sb, 0, hs, o->latency_log, po.latency_log,
+                                           dmap, F, C * b->lat_cap);
+    if (po.stats) hipLaunchKernelGGL(k_rows_scatter<uint64_t>, sg, sb, 0, hs, o->stats, po.stats, dmap, F,
+                                     FX_SIM_STATS);
+    hipLaunchKernelGGL(k_rows_scatter<uint32_t>, sg, sb, 0, hs, o->err, po.err, dmap, F, 1u);
+    std::vector<uint32_t> e2(F);
+    if (hipMemcpyAsync(e2.data(), po.err, (size_t)F * 4, hipMemcpyDeviceToHost, hs) != hipSuccess ||
+        hipStreamSynchronize(hs) != hipSuccess)
+      return FX_ERR_HIP;
+    if (reruns) *reruns += F;
+    std::vector<uint32_t> next;
+    for (uint32_t j = 0; j < F; ++j)
+      if (e2[j] == FX_ERR_SIM_CAPACITY) next.push_back(fail[j]);
+    fail.swap(next);
+  }
+  return FX_OK;
+}

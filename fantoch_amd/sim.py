@@ -121,7 +121,7 @@ class Result:
 
 
 def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bins=256,
-        delay_bins=8192, ring_entries=16, dot_slots=8, max_events=0, flags=0, stream=None):
+        delay_bins=8192, ring_entries=0, dot_slots=0, max_events=0, flags=0, stream=None):
     """Simulates every instance of `specs` on the GPU; returns a Result."""
     lib = _lib.load()
     planet = planet or Planet()
@@ -153,7 +153,9 @@ def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bi
                        out["latency_log"].ptr if lat_cap else None, out["latency_hist"].ptr,
                        out["chain"].ptr, out["delay"].ptr, out["stats"].ptr, out["err"].ptr,
                        lat_bins, chain_bins, delay_bins, 0)
-    check(lib.fx_sim_run(ctypes.byref(b), ctypes.byref(o), stream), "fx_sim_run")
+    reruns = ctypes.c_uint32()
+    check(lib.fx_sim_run_tiered(ctypes.byref(b), ctypes.byref(o), stream, ctypes.byref(reruns)),
+          "fx_sim_run_tiered")
     check(lib.fx_dev_synchronize(stream), "fx_sim_run sync")
     d = lambda k, dt, cnt: out[k].download(dt, cnt, stream)
     res = Result(specs, d("executed", np.uint32, N * s0.n * exec_cap),
@@ -163,4 +165,5 @@ def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bi
                  d("chain", np.uint64, chain_bins), d("delay", np.uint64, delay_bins),
                  d("stats", np.uint64, N * _lib.FX_SIM_STATS), d("err", np.uint32, N),
                  exec_cap, lat_cap)
+    res.reruns = int(reruns.value)  # instances rerun with larger tables (fx_sim_run_tiered)
     return res

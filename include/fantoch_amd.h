@@ -384,8 +384,10 @@ typedef struct fx_sim_batch {
   uint32_t exec_cap;               /* executed dots kept per process (the rest counted) */
   uint32_t lat_cap;                /* latencies kept per client (0 = no latency log)    */
   uint32_t max_events;             /* per-instance event budget (0 = 2^32 - 1)          */
-  uint32_t ring_entries;           /* messages in flight per process link (power of 2; 0 = 32) */
-  uint32_t dot_slots;              /* live dots per coordinator (power of 2; 0 = 8)     */
+  uint32_t ring_entries;           /* messages in flight per instance, a pool shared by the
+                                      process links (<= 65534; 0 = min(4096, 64 n))     */
+  uint32_t dot_slots;              /* live dots per instance, a pool shared by the
+                                      coordinators (<= 64; 0 = min(64, 8 n))            */
   uint32_t pad;
 } fx_sim_batch;
 
@@ -399,6 +401,8 @@ typedef struct fx_sim_batch {
 #define FX_SIM_STAT_TRACE 26u   /* hash of the processed action sequence, GC traffic excluded (debug) */
 #define FX_SIM_STAT_SEQ 27u     /* schedule insertions                             */
 #define FX_SIM_STAT_DEPS 28u    /* deps of every executor Add (sum over processes) */
+#define FX_SIM_STAT_LAT_SUM 29u /* sum of every client command's latency (ms)       */
+#define FX_SIM_STAT_ERR_SITE 30u /* where FX_ERR_SIM_CAPACITY was raised (sim_wave.hip line) */
 #define FX_SIM_STATS 32u
 
 typedef struct fx_sim_output {  /* device buffers; NULL where not wanted */
@@ -418,6 +422,15 @@ typedef struct fx_sim_output {  /* device buffers; NULL where not wanted */
 int fx_sim_plan(const fx_sim_spec* spec, uint32_t ring_entries, uint32_t dot_slots, uint32_t* lds_bytes);
 /* Runs every instance to completion (Runner::run, runner.rs:202-231); asynchronous. */
 int fx_sim_run(const fx_sim_batch* batch, const fx_sim_output* out, void* hip_stream);
+/* fx_sim_run, then (synchronously) reruns the instances that stopped with
+ * FX_ERR_SIM_CAPACITY with a 4x (at least 256 n) message pool and 256 dot slots, writing their
+ * rows of every output in place.  Histograms stay exact: the samples the
+ * failed runs added before failing are removed by replaying just those runs
+ * at the first geometry (the kernel is deterministic per instance) and
+ * subtracting.  An instance that fails at the larger geometry too keeps its
+ * error and contributes no histogram samples.  *reruns (optional) = instances
+ * rerun. */
+int fx_sim_run_tiered(const fx_sim_batch* batch, const fx_sim_output* out, void* hip_stream, uint32_t* reruns);
 
 /* Planet::from(dir) (fantoch/src/planet/mod.rs:38-54, dat.rs:20-94): regions
  * in name order; ping[a][b] (ms, `as u64` of the average) and rank[a][b] = the

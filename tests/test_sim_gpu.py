@@ -59,6 +59,9 @@ def assert_instance_parity(res, i, s, o):
     for c, r in enumerate(regs):
         np.add.at(hist[r], np.minimum(lat[c, :s.commands_per_client], hist.shape[1] - 1), 1)
     assert np.array_equal(hist, o["latency"])
+    # per-instance latency sum (FX_SIM_STAT_LAT_SUM, the per-placement mean of configs[2])
+    lat_sum = int(sum(ms * int(c) for h in o["latency"] for ms, c in enumerate(h) if c))
+    assert int(res.stats[i, _lib.FX_SIM_STAT_LAT_SUM]) == lat_sum
 
 
 def run_and_compare(specs, **kw):
@@ -113,7 +116,7 @@ def test_two_clients_per_region_two_keys():
     specs = [S.spec(S.EPAXOS, 5, 2, regs, regs, clients_per_region=2, commands_per_client=60,
                     keys_per_command=2, conflict_rate=c, seed=3, instance=i)
              for i, c in enumerate([10, 50, 90])]
-    run_and_compare(specs, dot_slots=16)
+    run_and_compare(specs)
 
 
 def test_extra_time_and_client_regions_apart():
@@ -135,3 +138,20 @@ def test_no_gc():
     specs = [S.spec(S.EPAXOS, 5, 2, regs, regs, commands_per_client=80, conflict_rate=50,
                     gc_interval_ms=0, seed=4, instance=i) for i in range(4)]
     run_and_compare(specs)
+
+
+def test_capacity_escalation_is_exact():
+    """configs[2]-style placements where a far replica lags: with small tables
+    the first launch stops some instances with FX_ERR_SIM_CAPACITY;
+    fx_sim_run_tiered reruns them with larger tables and removes their partial
+    histogram samples, so every output still equals the oracle's."""
+    pl = planet()
+    subs = [["asia-east1", "europe-west1", "europe-west2", "europe-west4", "us-east4"],
+            ["asia-east2", "europe-west1", "europe-west3", "europe-west6", "us-west1"],
+            ["asia-northeast2", "europe-north1", "europe-west2", "europe-west3", "europe-west4"],
+            ["asia-south1", "europe-north1", "southamerica-east1", "australia-southeast1", "europe-west1"]]
+    specs = [S.spec(S.ATLAS, 5, 1, pl.ids(sorted(r)), pl.ids(sorted(r)), commands_per_client=80, conflict_rate=c,
+                    seed=9, instance=i) for i, (r, c) in enumerate((r, c) for r in subs for c in (2, 50))]
+    # 24 messages / 16 dots in flight: the lagging placements outgrow them
+    res, _ = run_and_compare(specs, ring_entries=24, dot_slots=16)
+    assert res.reruns > 0
