@@ -207,6 +207,6 @@ def test_sim_plan_sizes():
     # default pools (0 = 64 n messages, 8 n dots) need more LDS than 32 / 8
     assert lib.fx_sim_plan(ctypes.byref(s), 0, 0, ctypes.byref(b)) == 0
     assert small < b.value < 64 * 1024
-    assert lib.fx_sim_plan(ctypes.byref(s), 0, 65, ctypes.byref(b)) == _lib.FX_ERR_UNSUPPORTED
+    assert lib.fx_sim_plan(ctypes.byref(s), 0, 257, ctypes.byref(b)) == _lib.FX_ERR_UNSUPPORTED
     s9 = S.spec(S.EPAXOS, 5, 2, regs, regs, clients_per_region=40)  # 200 clients: too many links
     assert lib.fx_sim_plan(ctypes.byref(s9), 32, 8, ctypes.byref(b)) == _lib.FX_ERR_UNSUPPORTED
