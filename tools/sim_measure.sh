@@ -28,4 +28,11 @@ for pass in "fetch FETCH_SIZE" "write WRITE_SIZE" \
     > $M/$name.log 2>&1 || { echo "$name rc=$?"; tail -20 $M/$name.log; exit 1; }
   echo "pmc $name done"
 done
+timeout -k 10 300 python3 bench.py --mode huge > $M/huge.log 2>&1 || { echo "huge rc=$?"; tail -20 $M/huge.log; exit 1; }
+tail -1 $M/huge.log | cut -c1-300
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $M/huge_trace -o run --output-format csv -- \
+  python3 bench.py --mode huge --no-cpu-baseline > $M/huge_trace.log 2>&1 || { echo "huge trace rc=$?"; exit 1; }
+timeout -k 10 600 python3 bench.py --mode placements --cmds 100 --steps 1 --warmup 0 > $M/placements.log 2>&1 \
+  || { echo "placements rc=$?"; tail -20 $M/placements.log; exit 1; }
+tail -1 $M/placements.log | cut -c1-300
 find $M -name "*.csv" | sort
