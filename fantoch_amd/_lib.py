@@ -49,7 +49,8 @@ FX_RELEASE_NONE = 0xFFFFFFFF
 FX_FLAG_INIT = 1
 FX_FLAG_EXECUTE_AT_COMMIT = 2
 FX_FLAG_SAVE_STATE = 4
-FX_NUM_TIERS = 7
+FX_TIER_WIDE, FX_TIER_WIDE_HBM = 7, 8
+FX_NUM_TIERS = 9
 FX_TIER_GROUP = 0
 FX_TIER_WAVE = 4
 FX_TIER_LANE_REG = 5
@@ -87,7 +88,7 @@ class CutStats(ctypes.Structure):
     """fx_cut_stats (fx_batch_run_cut)."""
     _fields_ = [("segments", ctypes.c_uint64), ("max_segment", ctypes.c_uint32),
                 ("whole_streams", ctypes.c_uint32), ("failed_streams", ctypes.c_uint32),
-                ("tier_counts", ctypes.c_uint32 * 8)]
+                ("tier_counts", ctypes.c_uint32 * 16)]
 
 
 class HistBatch(ctypes.Structure):
@@ -106,7 +107,7 @@ class SynthParams(ctypes.Structure):
                 ("cmds_per_process", ctypes.c_uint32), ("window", ctypes.c_uint32),
                 ("cycle_pct", ctypes.c_uint32), ("horizon", ctypes.c_uint32),
                 ("num_conflicts", ctypes.c_uint32), ("conflict_pct", ctypes.c_uint32 * 8),
-                ("conflict_block", ctypes.c_uint32)]
+                ("conflict_block", ctypes.c_uint32), ("clients", ctypes.c_uint32)]
 
 
 class Config(ctypes.Structure):

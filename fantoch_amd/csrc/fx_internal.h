@@ -97,6 +97,10 @@ void* scratch(uint32_t slot, size_t bytes);
 std::recursive_mutex& scratch_mutex();
 enum : uint32_t { SCRATCH_TIERED_STATE = 0, SCRATCH_TIERED_MAP = 1, SCRATCH_CUT_FIRST = 2, SCRATCH_SLOTS = 40 };
 
+// The wide tiers (graph_wide.hip): whole streams, tables in LDS or HBM.
+int launch_wide(const KArgs& a, bool hbm, hipStream_t stream);
+size_t wide_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes);
+
 // fx_batch_run_tiered over all streams (only == NULL) or the listed ones.
 int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
                const std::vector<uint32_t>* only, uint32_t* tier_counts);

@@ -51,7 +51,7 @@ FX_HD uint64_t synth_rand(uint64_t seed, uint64_t inst, uint64_t a, uint64_t b) 
 struct SynthInstance {
   uint64_t seed;
   uint32_t inst;  // global instance index
-  uint32_t n, cmds, window, cycle_pct, horizon, conflict;
+  uint32_t n, cmds, window, cycle_pct, horizon, conflict, clients;
 };
 
 FX_HD SynthInstance synth_instance(const fx_synth_params& p, uint32_t local) {
@@ -63,6 +63,7 @@ FX_HD SynthInstance synth_instance(const fx_synth_params& p, uint32_t local) {
   si.window = p.window;
   si.cycle_pct = p.cycle_pct;
   si.horizon = p.horizon;
+  si.clients = p.clients;
   const uint32_t nc = p.num_conflicts ? p.num_conflicts : 1;
   const uint32_t ci = p.conflict_block ? (si.inst / p.conflict_block) % nc : si.inst % nc;
   si.conflict = p.conflict_pct[ci];
@@ -81,8 +82,45 @@ FX_HD uint32_t synth_key(const SynthInstance& si, uint32_t g) {
   return synth_conflicts(si, g) ? 0u : (g % si.n) + 1u;
 }
 
+// C closed-loop clients per process (C >= 2): command g = (seq - 1) n + (s - 1)
+// as with one client, seqs of a source grouped in rounds of C concurrent
+// commands.  A command sees, per source, the latest same-key command of an
+// earlier round (its own source: the previous seq), or with probability
+// cycle_pct a random concurrent command of the same round of another source
+// (the dense, cyclic graph of BASELINE configs[3]).
+FX_HD uint32_t synth_deps_clients(const SynthInstance& si, uint32_t g, uint32_t* out) {
+  const uint32_t n = si.n, C = si.clients;
+  const uint32_t s = g % n + 1;
+  const uint32_t seq = g / n + 1;
+  const uint32_t round0 = (seq - 1) / C * C;  // seqs of earlier rounds are <= round0
+  const bool shared = synth_conflicts(si, g);
+  uint32_t nd = 0;
+  for (uint32_t s2 = 1; s2 <= n; ++s2) {
+    if (!shared && s2 != s) continue;
+    uint32_t dep = 0;
+    if (shared && s2 != s && si.cycle_pct > 0 &&
+        (uint32_t)(synth_rand(si.seed, si.inst, ((uint64_t)g << 4) | s2, PURPOSE_CYCLE) % 100u) < si.cycle_pct) {
+      const uint32_t k2 = (uint32_t)(synth_rand(si.seed, si.inst, ((uint64_t)g << 4) | s2, PURPOSE_JITTER + 1) % C);
+      const uint32_t q = round0 + k2 + 1;
+      if (synth_conflicts(si, (q - 1) * n + (s2 - 1))) dep = q;
+    }
+    if (dep == 0) {
+      const uint32_t top = s2 == s ? seq - 1 : round0;
+      const uint32_t lo = top > si.horizon ? top - si.horizon : 0u;
+      for (uint32_t q = top; q > lo; --q)
+        if (synth_conflicts(si, (q - 1) * n + (s2 - 1)) == shared) {
+          dep = q;
+          break;
+        }
+    }
+    if (dep) out[nd++] = FX_PACK_DOT(s2, dep);
+  }
+  return nd;
+}
+
 // Deps of command g, ascending by packed dot (one per source at most).
 FX_HD uint32_t synth_deps(const SynthInstance& si, uint32_t g, uint32_t* out) {
+  if (si.clients > 1) return synth_deps_clients(si, g, out);
   const uint32_t n = si.n;
   const uint32_t s = g % n + 1;
   const uint32_t j = g / n + 1;

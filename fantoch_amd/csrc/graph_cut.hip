@@ -48,7 +48,7 @@ namespace fx {
 namespace cut {
 
 constexpr uint32_t INF = 0xFFFFFFFFu;
-constexpr uint32_t MAX_SEG = 256;   // longer segments: the stream runs whole
+constexpr uint32_t MAX_SEG = 4096;  // longer segments: the stream runs whole
 constexpr uint32_t CHUNK = 1024;    // steps per scan block (256 threads x 4)
 constexpr uint32_t BT = 256;
 

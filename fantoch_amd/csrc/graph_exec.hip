@@ -991,13 +991,14 @@ int fx_tier_query(uint32_t tier, uint32_t n, fx_tier_info* out) {
     case 4: *out = {8, WAVE_SLOTS, WAVE_WINDOW_BITS, wave_state_words_per_stream()}; break;
     case 5: *out = {8, LANE_SLOTS, LANE_WINDOW_BITS, lane_state_words_per_stream()}; break;
     case 6: *out = {8, std::min(LANE_SLOTS, GROUP_SLOTS), std::min(LANE_WINDOW_BITS, GROUP_WINDOW_BITS), 0}; break;
+    case FX_TIER_WIDE: *out = {8, 1024, 2048, 0}; break;
+    case FX_TIER_WIDE_HBM: *out = {8, 16384, 32768, (uint32_t)(wide_state_bytes(FX_TIER_WIDE_HBM, n, 1) / 4)}; break;
     default: return FX_ERR_INVALID_ARG;
   }
   return n >= 1 && n <= out->max_sources ? FX_OK : FX_ERR_INVALID_ARG;
 }
 
 size_t fx_batch_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes) {
-  (void)n;
   switch (tier) {
     case 0: return group_state_bytes(lanes);
     case 1: return state_bytes<Tier1>(lanes);
@@ -1006,6 +1007,8 @@ size_t fx_batch_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes) {
     case 4: return wave_state_bytes(lanes);
     case 5: return lane_state_bytes(lanes);
     case 6: return split_scratch_bytes(lanes);  // scheduling scratch, not resumable state
+    case FX_TIER_WIDE:
+    case FX_TIER_WIDE_HBM: return wide_state_bytes(tier, n, lanes);  // working tables (HBM tier)
     default: return 0;
   }
 }
@@ -1073,6 +1076,8 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
     case 4: st = launch_wave(a, hs); break;
     case 5: st = launch_lane(a, hs); break;
     case 6: st = launch_split(a, state, hs); break;
+    case FX_TIER_WIDE: st = launch_wide(a, false, hs); break;
+    case FX_TIER_WIDE_HBM: st = launch_wide(a, true, hs); break;
     default: return FX_ERR_INVALID_ARG;
   }
   if (g_profile) {
@@ -1150,6 +1155,7 @@ static int check_synth(const fx_synth_params* p) {
       N >= (1u << 26))
     return FX_ERR_INVALID_ARG;
   if ((uint64_t)p->instances * p->n >= (1ull << 32)) return FX_ERR_INVALID_ARG;
+  if (p->clients > 1 && p->cmds_per_process % p->clients) return FX_ERR_INVALID_ARG;
   return FX_OK;
 }
 
@@ -1226,6 +1232,8 @@ static uint32_t escalate(uint32_t tier) {
     case FX_TIER_GROUP: return FX_TIER_LDS_LARGE;
     case FX_TIER_LANE: return FX_TIER_LDS_LARGE;
     case FX_TIER_LDS_LARGE: return FX_TIER_GLOBAL;
+    case FX_TIER_GLOBAL: return FX_TIER_WIDE;
+    case FX_TIER_WIDE: return FX_TIER_WIDE_HBM;
     case FX_TIER_WAVE: return FX_TIER_GLOBAL;
     case FX_TIER_LANE_REG: return FX_TIER_LDS_LARGE;
     case FX_TIER_SPLIT: return FX_TIER_LDS_LARGE;
@@ -1273,7 +1281,7 @@ int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t fl
     uint32_t* dmap = nullptr;
     void* dstate = nullptr;
     if (!whole && !(dmap = (uint32_t*)scratch(SCRATCH_TIERED_MAP, (size_t)L * 4))) return FX_ERR_HIP;
-    if ((tier == FX_TIER_GLOBAL || tier == FX_TIER_SPLIT) &&
+    if ((tier == FX_TIER_GLOBAL || tier == FX_TIER_SPLIT || tier == FX_TIER_WIDE_HBM) &&
         !(dstate = scratch(SCRATCH_TIERED_STATE, fx_batch_state_bytes(tier, in->n, L))))
       return FX_ERR_HIP;
     if (dmap) (void)hipMemcpyAsync(dmap, todo.data(), (size_t)L * 4, hipMemcpyHostToDevice, hs);

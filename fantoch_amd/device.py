@@ -108,7 +108,7 @@ def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096,
             front = DeviceBuffer(S * 8 * 4)
             front.upload(np.asarray(init_frontier, np.uint32).reshape(S, 8))
         state = None
-        if tier in (2, _lib.FX_TIER_SPLIT):  # HBM-resident tier's working memory / split scratch
+        if tier in (2, _lib.FX_TIER_SPLIT, _lib.FX_TIER_WIDE_HBM):  # HBM-resident tier's working memory / split scratch
             state = DeviceBuffer(lib.fx_batch_state_bytes(tier, planes.n, S))
         status = lib.fx_batch_execute(ctypes.byref(inb), ctypes.byref(outb), tier, None, S,
                                       state.ptr if state else None, 0, steps,

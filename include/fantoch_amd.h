@@ -143,7 +143,7 @@ typedef struct fx_hist_batch {
  * executed-clock window above each source's frontier.  A stream that exceeds
  * its tier stops with FX_ERR_CAPACITY and is rerun at the next tier
  * (fx_batch_run_tiered escalates 0 -> 1 -> 2, 3 -> 1 -> 2, 4 -> 2, 5 -> 1 -> 2,
- * 6 -> 1 -> 2). */
+ * 6 -> 1 -> 2, and then 2 -> 7 -> 8). */
 #define FX_TIER_GROUP 0      /* 16 lanes per stream: 16 pending, 8 cached deps, n <= 16 */
 #define FX_TIER_LDS_LARGE 1  /* lane per stream, LDS-resident: 32 pending, one wave per CU */
 #define FX_TIER_GLOBAL 2     /* lane per stream, HBM-resident: 64 pending, 1024-bit windows */
@@ -155,7 +155,11 @@ typedef struct fx_hist_batch {
                                 tier 0 for dense ones, both launched concurrently; whole
                                 batches only (FX_FLAG_INIT, no stream_map, no saved state);
                                 `state` = fx_batch_state_bytes(6, n, S) bytes of scratch */
-#define FX_NUM_TIERS 7
+#define FX_TIER_WIDE 7       /* one wavefront per stream, the graph as tables in LDS: 1024
+                                pending, 2048-bit windows (rerun tier after tier 2) */
+#define FX_TIER_WIDE_HBM 8   /* the same over HBM tables: 16384 pending, 32768-bit windows;
+                                `state` = fx_batch_state_bytes(8, n, lanes) bytes */
+#define FX_NUM_TIERS 9
 #define FX_TIER_DEFAULT FX_TIER_SPLIT
 
 typedef struct fx_tier_info {
@@ -214,7 +218,7 @@ int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out,
  * prefix deps dropped and its dots renumbered per source (order-preserving).
  * All segments run as one batch through fx_batch_run_tiered and map back.
  * A stream without a usable decomposition (a dep that never arrives, a
- * segment over 256 steps, a double index, an index-only record) or whose
+ * segment over 4096 steps, a double index, an index-only record) or whose
  * segments do not all execute completely runs whole through
  * fx_batch_run_tiered.  Output planes are identical to fx_batch_run_tiered's.
  * Synchronous; device pointers. */
@@ -225,7 +229,7 @@ typedef struct fx_cut_stats {
   uint32_t failed_streams;              /* ... of which because a segment did not
                                            execute completely (capacity, or the cut
                                            argument failing: never seen so far)     */
-  uint32_t tier_counts[8];              /* segment-batch streams run per tier       */
+  uint32_t tier_counts[16];             /* segment-batch streams run per tier       */
 } fx_cut_stats;
 int fx_batch_run_cut(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
                      fx_cut_stats* stats);
@@ -251,6 +255,12 @@ typedef struct fx_synth_params {
   uint32_t conflict_block;   /* 0: rate = conflict_pct[i % num_conflicts] (seed-major);
                                 B: rate = conflict_pct[(i / B) % num_conflicts]
                                 (conflict-major: B consecutive instances share a rate) */
+  uint32_t clients;          /* closed-loop clients per process (0/1: one; C >= 2:
+                                seqs form rounds of C concurrent commands per source,
+                                a command sees other sources' earlier rounds only, and
+                                with probability cycle_pct a random concurrent command
+                                of any other source: large SCCs, BASELINE configs[3];
+                                cmds_per_process must be a multiple of C)            */
 } fx_synth_params;
 
 /* Planes of the synthetic batch: S = instances * n, steps = n * cmds, dmax = n. */
