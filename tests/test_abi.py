@@ -42,13 +42,14 @@ def test_tier_query(lib):
     assert lib.fx_tier_query(0, 5, ctypes.byref(ti)) == 0
     assert ti.pending_cap >= 8 and ti.window_bits >= 32 and ti.max_sources >= 5
     caps = []
-    for t in range(3):  # the escalation order of fx_batch_run_tiered: 0 -> 1 -> 2
+    # the escalation order of fx_batch_run_tiered: 0 -> 1 -> 2 -> 7 (wide, LDS) -> 8 (wide, HBM)
+    for t in (0, 1, 2, _lib.FX_TIER_WIDE, _lib.FX_TIER_WIDE_HBM):
         assert lib.fx_tier_query(t, 7, ctypes.byref(ti)) == 0
         caps.append((ti.pending_cap, ti.window_bits))
     assert caps == sorted(caps)
     assert lib.fx_tier_query(3, 7, ctypes.byref(ti)) == 0
     assert lib.fx_tier_query(1, 9, ctypes.byref(ti)) != 0
-    assert lib.fx_tier_query(7, 5, ctypes.byref(ti)) != 0
+    assert lib.fx_tier_query(_lib.FX_NUM_TIERS, 5, ctypes.byref(ti)) != 0
 
 
 def test_no_device_fails_loudly(lib):
