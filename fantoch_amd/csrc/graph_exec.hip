@@ -1253,8 +1253,8 @@ int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t fl
   const uint32_t S = in->num_streams;
   flags |= FX_FLAG_INIT;
   flags &= ~FX_FLAG_SAVE_STATE;
-  const uint32_t ft = (flags >> FX_FLAG_TIER_SHIFT) & 7u;
-  flags &= ~(7u << FX_FLAG_TIER_SHIFT);
+  const uint32_t ft = (flags >> FX_FLAG_TIER_SHIFT) & 15u;
+  flags &= ~(15u << FX_FLAG_TIER_SHIFT);
   uint32_t first = ft ? ft - 1u : (uint32_t)FX_TIER_DEFAULT;
   if (first >= FX_NUM_TIERS) return FX_ERR_INVALID_ARG;
   if (only && first == FX_TIER_SPLIT) first = FX_TIER_GROUP;  // the split tier takes whole batches

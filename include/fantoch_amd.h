@@ -79,7 +79,7 @@ extern "C" {
 #define FX_FLAG_INIT 1u              /* start from an empty executor (else resume from state) */
 #define FX_FLAG_EXECUTE_AT_COMMIT 2u /* Config::execute_at_commit (executor.rs:72-73)    */
 #define FX_FLAG_SAVE_STATE 4u        /* write the executor state back for a later resume */
-/* fx_batch_run_tiered only: first tier = (flags >> FX_FLAG_TIER_SHIFT) & 7
+/* fx_batch_run_tiered only: first tier = ((flags >> FX_FLAG_TIER_SHIFT) & 15) - 1
  * (0 = the default tier, FX_TIER_DEFAULT). */
 #define FX_FLAG_TIER_SHIFT 8u
 #define FX_FLAG_FIRST_TIER(t) ((((uint32_t)(t)) + 1u) << FX_FLAG_TIER_SHIFT)
