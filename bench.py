@@ -66,9 +66,9 @@ def parse(argv=None):
                          "enumeration, so a wavefront's streams share a rate; 0 = seed-major)")
     ap.add_argument("--tier", type=int, default=-1, help="executor tier (-1 = FX_TIER_DEFAULT)")
     ap.add_argument("--ring-entries", type=int, default=0,
-                    help="sim: messages in flight per instance (pool shared by the links; 0 = min(4096, 64 n))")
+                    help="sim: messages in flight per instance (pool shared by the links; 0 = 16 n x clients per region)")
     ap.add_argument("--dot-slots", type=int, default=0,
-                    help="sim: live dots per instance (pool shared by the coordinators; 0 = min(64, 8 n))")
+                    help="sim: live dots per instance (pool shared by the coordinators; 0 = min(64, 8 clients))")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=None,
                     help="CPU work budget of the cpu_baseline sample (sim default 15, executor 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -1258,7 +1258,10 @@ struct Sim {
 };
 
 template <uint32_t HM, uint32_t DS>
-__global__ __launch_bounds__(64, DS == 1 ? 3 : 2) void k_sim(SimArgs a) {
+#ifndef FX_SIM_WAVES
+#define FX_SIM_WAVES 3  // waves per SIMD the register budget of k_sim<., 1> targets
+#endif
+__global__ __launch_bounds__(64, DS == 1 ? FX_SIM_WAVES : 2) void k_sim(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
@@ -1442,9 +1445,12 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   g.n = n;
   g.C = C;
   g.K = sp.keys_per_command;
-  g.W = wslots ? wslots : 64u;  // live dots per instance
+  // table sizes: small by default (LDS decides how many instances share a CU);
+  // fx_sim_run_tiered reruns the instances that outgrow them with 256 dots
+  const uint32_t cpr = (C + n - 1) / n;  // clients per process region
+  g.W = wslots ? wslots : std::min<uint32_t>(64u, 8u * C);  // live dots per instance
   if (g.W > 256u) return false;
-  g.R = ring ? ring : std::min<uint32_t>(4096u, 64u * n);  // messages in flight per instance
+  g.R = ring ? ring : std::min<uint32_t>(4096u, 16u * n * cpr);  // messages in flight per instance
   if (g.R > 65534u) return false;
   g.NP = n * (n - 1);
   g.L = g.NP + n + 2 * C;
@@ -1463,11 +1469,11 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   // messages in flight: one pool per instance, a FIFO list per process link
   g.off_pool = o; o += g.R * 4;
   g.off_free = o; o += g.R;
-  // GC logs: 8 / 4 entries per client per region (commits of one source
-  // arrive about once per client round trip)
-  const uint32_t cpr = (C + n - 1) / n;
-  g.rt = 8;
-  while (g.rt < 8 * cpr && g.rt < 64) g.rt <<= 1;
+  // GC logs: 4 / 2 entries per client per region (commits of one source
+  // arrive about once per client round trip), 32 / 16 in the rerun geometry
+  g.rt = 4;
+  while (g.rt < 4 * cpr && g.rt < 64) g.rt <<= 1;
+  if (g.W > 64u) g.rt = std::max<uint32_t>(g.rt, 32u);
   g.rc = g.rt / 2;
   g.off_gct = o; o += n * n * g.rt * 2;
   g.off_gcc = o; o += n * n * g.rc * 2;

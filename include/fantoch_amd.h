@@ -395,9 +395,10 @@ typedef struct fx_sim_batch {
   uint32_t lat_cap;                /* latencies kept per client (0 = no latency log)    */
   uint32_t max_events;             /* per-instance event budget (0 = 2^32 - 1)          */
   uint32_t ring_entries;           /* messages in flight per instance, a pool shared by the
-                                      process links (<= 65534; 0 = min(4096, 64 n))     */
+                                      process links (<= 65534; 0 = 16 n x clients per
+                                      process region)                                   */
   uint32_t dot_slots;              /* live dots per instance, a pool shared by the
-                                      coordinators (<= 64; 0 = min(64, 8 n))            */
+                                      coordinators (<= 256; 0 = min(64, 8 clients))     */
   uint32_t pad;
 } fx_sim_batch;
 
