@@ -100,6 +100,7 @@ enum : uint32_t { SCRATCH_TIERED_STATE = 0, SCRATCH_TIERED_MAP = 1, SCRATCH_CUT_
 // The wide tiers (graph_wide.hip): whole streams, tables in LDS or HBM.
 int launch_wide(const KArgs& a, bool hbm, hipStream_t stream);
 size_t wide_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes);
+bool wide_lds_fits(uint32_t n, uint32_t dmax);  // the LDS wide tier's tables fit a workgroup
 
 // fx_batch_run_tiered over all streams (only == NULL) or the listed ones.
 int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,

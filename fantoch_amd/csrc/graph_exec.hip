@@ -1275,6 +1275,7 @@ int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t fl
   if (todo.empty()) return FX_OK;
   std::vector<uint32_t> err(S, 0);
   for (uint32_t tier = first; tier < FX_NUM_TIERS && !todo.empty(); tier = escalate(tier)) {
+    if (tier == FX_TIER_WIDE && !wide_lds_fits(in->n, in->dmax)) continue;  // straight to the HBM tables
     const uint32_t L = (uint32_t)todo.size();
     if (tier_counts) tier_counts[tier] = L;
     const bool whole = !only && tier == first;

@@ -34,16 +34,19 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 enum : uint32_t { FOUND = 0, MISSING = 1, NOT_PENDING = 2 };
 
 struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-bit clock windows
-  uint32_t P, Q, WB, n;
-  uint32_t vdot, vrec, vwait, vid, vlow, vmark, vfree, tstk, fv, fi, wl, tl, tmp, hidx, front, bits, words;
-  __host__ __device__ void make(uint32_t P_, uint32_t Q_, uint32_t WB_, uint32_t n_) {
+  uint32_t P, Q, WB, n, D;
+  uint32_t vdot, vrec, vnd, vdeps, vwait, vid, vlow, vmark, vfree, tstk, fv, fi, wl, tl, tmp, hidx, front, bits, words;
+  __host__ __device__ void make(uint32_t P_, uint32_t Q_, uint32_t WB_, uint32_t n_, uint32_t D_) {
     P = P_;
     Q = Q_;
     WB = WB_;
     n = n_;
+    D = D_;
     uint32_t o = 0;
     vdot = o; o += P;
     vrec = o; o += P;
+    vnd = o; o += P;      // deps of the vertex (copied from the planes at index time:
+    vdeps = o; o += P * D;  // the DFS then never waits on HBM)
     vwait = o; o += P;
     vid = o; o += P;
     vlow = o; o += P;
@@ -179,10 +182,9 @@ struct W {
     uint32_t result = FOUND;
     while (fsp && !err) {
       const uint32_t v = rd(L.fv, fsp - 1), i = rd(L.fi, fsp - 1);
-      const uint32_t rec = rd(L.vrec, v);
-      if (i < ndeps(rec)) {
+      if (i < rd(L.vnd, v)) {
         put(L.fi, fsp - 1, i + 1);
-        const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)dep(rec, i));
+        const uint32_t d = rd(L.vdeps, v * L.D + i);
         if (d == rd(L.vdot, v) || contains(d)) continue;  // self or executed (tarjan.rs:128-145)
         const uint32_t w = find(d);
         if (w == NONE) {  // missing (tarjan.rs:148-157, shard_count == 1)
@@ -306,6 +308,9 @@ struct W {
     const uint32_t v = rd(L.vfree, --nfree);
     put(L.vdot, v, d);
     put(L.vrec, v, r);
+    const uint32_t nd = ndeps(r);
+    put(L.vnd, v, nd);
+    if (lid < nd) m[L.vdeps + v * L.D + lid] = dep(r, lid);
     put(L.vwait, v, 0);
     put(L.vid, v, 0);
     put(L.vmark, v, 0);
@@ -369,22 +374,25 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
 
 // LDS tables: 1024 vertices, 2048 index slots per source, 2048-bit windows;
 // HBM tables: 16384 vertices, 32768 index slots, 32768-bit windows
-static wide::Lay wide_layout(bool hbm, uint32_t n) {
+static wide::Lay wide_layout(bool hbm, uint32_t n, uint32_t dmax) {
   wide::Lay L;
-  if (hbm) L.make(16384, 32768, 1024, n);
-  else L.make(1024, 2048, 64, n);
+  if (hbm) L.make(16384, 32768, 1024, n, std::max(dmax, 1u));
+  else L.make(1024, 2048, 64, n, std::max(dmax, 1u));
   return L;
 }
 
+bool wide_lds_fits(uint32_t n, uint32_t dmax) { return (size_t)wide_layout(false, n, dmax).words * 4 <= 160 * 1024; }
+
 size_t wide_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes) {
-  return tier == FX_TIER_WIDE_HBM ? (size_t)wide_layout(true, n).words * 4 * lanes : 0;
+  return tier == FX_TIER_WIDE_HBM ? (size_t)wide_layout(true, n, 31).words * 4 * lanes : 0;
 }
 
 int launch_wide(const KArgs& a, bool hbm, hipStream_t hs) {
   if (a.step_begin != 0 || a.step_end != a.steps || !(a.flags & FX_FLAG_INIT) || (a.flags & FX_FLAG_SAVE_STATE))
     return FX_ERR_INVALID_ARG;  // whole streams only (a rerun tier)
   if (a.num_lanes == 0) return FX_OK;
-  const wide::Lay L = wide_layout(hbm, a.n);
+  const wide::Lay L = wide_layout(hbm, a.n, a.dmax);
+  if (!hbm && (size_t)L.words * 4 > 160 * 1024) return FX_ERR_UNSUPPORTED;
   if (hbm) {
     if (!a.state) return FX_ERR_INVALID_ARG;
     hipLaunchKernelGGL(wide::k_graph_wide<true>, dim3(a.num_lanes), dim3(64), 0, hs, a, L);
