@@ -84,6 +84,12 @@ class OrderBatch(ctypes.Structure):
                 ("nexec", ctypes.c_void_p), ("err", ctypes.c_void_p)]
 
 
+class PredBatch(ctypes.Structure):
+    """fx_pred_batch (predecessors executor input)."""
+    _fields_ = [("base", StreamBatch), ("clock_lo", ctypes.c_void_p), ("clock_hi", ctypes.c_void_p),
+                ("ndeps", ctypes.c_void_p)]
+
+
 class CutStats(ctypes.Structure):
     """fx_cut_stats (fx_batch_run_cut)."""
     _fields_ = [("segments", ctypes.c_uint64), ("max_segment", ctypes.c_uint32),
@@ -192,6 +198,12 @@ SIGNATURES = [
     ("fx_batch_run_tiered", ctypes.c_int,
      [ctypes.POINTER(StreamBatch), ctypes.POINTER(OrderBatch), ctypes.c_uint32, ctypes.c_void_p,
       u32p]),
+    ("fx_pred_execute", ctypes.c_int,
+     [ctypes.POINTER(PredBatch), ctypes.POINTER(OrderBatch), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+      ctypes.c_uint32, ctypes.c_void_p]),
+    ("fx_pred_state_bytes", ctypes.c_size_t, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    ("fx_pred_run", ctypes.c_int,
+     [ctypes.POINTER(PredBatch), ctypes.POINTER(OrderBatch), ctypes.c_uint32, ctypes.c_void_p, u32p]),
     ("fx_batch_run_cut", ctypes.c_int,
      [ctypes.POINTER(StreamBatch), ctypes.POINTER(OrderBatch), ctypes.c_uint32, ctypes.c_void_p,
       ctypes.c_void_p]),

@@ -131,3 +131,47 @@ def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096,
                       nexec.download(np.uint32, S), err.download(np.uint32, S),
                       chain, delay, list(tier_counts), status, cut_stats)
     return res
+
+
+def run_pred(planes, clock_lo, clock_hi, ndeps=None, execute_at_commit=False, hbm=False, nbins_delay=4096):
+    """PredecessorsExecutor (fx_pred_run, or one fx_pred_execute over HBM
+    tables with hbm=True) over a host batch with packed Caesar clock planes;
+    returns a BatchResult (delay histogram from fx_batch_metrics)."""
+    lib = _lib.load()
+    S, steps, pw = planes.S, planes.steps, planes.plane
+    bufs = {}
+    for name, arr in (("dot", planes.dot), ("hdr", planes.hdr), ("deps", planes.deps),
+                      ("clo", np.asarray(clock_lo, np.uint32)), ("chi", np.asarray(clock_hi, np.uint32)),
+                      ("nd", np.asarray(ndeps if ndeps is not None else [0], np.uint32))):
+        b = DeviceBuffer(arr.nbytes)
+        b.upload(arr)
+        bufs[name] = b
+    lengths = None
+    if planes.lengths is not None:
+        lengths = DeviceBuffer(S * 4)
+        lengths.upload(np.asarray(planes.lengths, np.uint32))
+    order, release = DeviceBuffer(pw * 4), DeviceBuffer(pw * 4)
+    release.fill_bytes(0xFF)
+    nexec, err = DeviceBuffer(S * 4), DeviceBuffer(S * 4)
+    base = _lib.StreamBatch(bufs["dot"].ptr, bufs["hdr"].ptr, bufs["deps"].ptr, lengths.ptr if lengths else None,
+                            S, steps, planes.dmax, planes.n)
+    inb = _lib.PredBatch(base, bufs["clo"].ptr, bufs["chi"].ptr, bufs["nd"].ptr if ndeps is not None else None)
+    outb = _lib.OrderBatch(order.ptr, release.ptr, nexec.ptr, err.ptr)
+    flags = _lib.FX_FLAG_EXECUTE_AT_COMMIT if execute_at_commit else 0
+    reruns = ctypes.c_uint32()
+    if hbm:
+        state = DeviceBuffer(lib.fx_pred_state_bytes(planes.n, planes.dmax, S))
+        status = lib.fx_pred_execute(ctypes.byref(inb), ctypes.byref(outb), None, S, state.ptr, flags, None)
+        check(lib.fx_dev_synchronize(None), "sync")
+    else:
+        status = lib.fx_pred_run(ctypes.byref(inb), ctypes.byref(outb), flags, None, ctypes.byref(reruns))
+    hc, hd = DeviceBuffer(64 * 8), DeviceBuffer(nbins_delay * 8)
+    hc.zero()
+    hd.zero()
+    hb = _lib.HistBatch(hc.ptr, 64, hd.ptr, nbins_delay)
+    check(lib.fx_batch_metrics(ctypes.byref(base), ctypes.byref(outb), ctypes.byref(hb), None), "fx_batch_metrics")
+    res = BatchResult(order.download(np.uint32, pw), release.download(np.uint32, pw), nexec.download(np.uint32, S),
+                      err.download(np.uint32, S), hc.download(np.uint64, 64), hd.download(np.uint64, nbins_delay),
+                      [], status)
+    res.reruns = int(reruns.value)
+    return res

@@ -234,6 +234,37 @@ typedef struct fx_cut_stats {
 int fx_batch_run_cut(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
                      fx_cut_stats* stats);
 
+/* ---------------------------------------- predecessors executor (Caesar) */
+/* PredecessorsExecutor (fantoch_ps/src/executor/pred/{mod,index,executor}.rs):
+ * commit streams as fx_stream_batch plus each Add's Caesar clock
+ * (common/pred/clocks/mod.rs:15-30: (seq, process id), lexicographic) packed
+ * as (seq << 8) | id in two planes (low / high 32 bits).  Phase one waits for
+ * every dep to commit, phase two for every dep with a lower clock to execute;
+ * the waiters of a removed PendingIndex entry are visited ascending by dot.
+ * Outputs as the batched GraphExecutor: order row k = arrival index of the
+ * k-th executed command (| FX_ORDER_SCC_START: every command its own group),
+ * release[arrival] = executing step; fx_batch_metrics gives ExecutionDelay. */
+#define FX_PRED_MAX_DEPS 256u
+typedef struct fx_pred_batch {
+  fx_stream_batch base;       /* dot / hdr / deps / lengths planes, S, steps, dmax, n */
+  const uint32_t* clock_lo;   /* plane: low 32 bits of (clock seq << 8 | process id) */
+  const uint32_t* clock_hi;   /* plane: high 32 bits                                */
+  const uint32_t* ndeps;      /* plane: deps per Add (Caesar commits carry every
+                                 conflicting command: up to FX_PRED_MAX_DEPS), or
+                                 NULL = FX_HDR_ND (dmax <= 31) */
+} fx_pred_batch;
+/* One launch over num_lanes streams (stream_map NULL = all): tables in LDS
+ * (512 pending) when state == NULL, else in `state` (HBM, 8192 pending;
+ * fx_pred_state_bytes).  Streams that run out report FX_ERR_CAPACITY.
+ * Whole streams, from an empty executor; flags: FX_FLAG_EXECUTE_AT_COMMIT. */
+int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* out, const uint32_t* stream_map,
+                    uint32_t num_lanes, void* state, uint32_t flags, void* hip_stream);
+size_t fx_pred_state_bytes(uint32_t n, uint32_t dmax, uint32_t lanes);
+/* Synchronous driver: LDS tables for all, HBM tables for the streams that ran
+ * out of capacity; *reruns (optional) = streams rerun. */
+int fx_pred_run(const fx_pred_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
+                uint32_t* reruns);
+
 /* --------------------------------------- synthetic Atlas/EPaxos streams */
 /* Commit streams of `instances` independent simulated instances; instance i
  * has n processes, each coordinating cmds_per_process commands; conflict rate

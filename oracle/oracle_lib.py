@@ -12,7 +12,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liboracle.so")
-SRCS = [os.path.join(HERE, f) for f in ("graph_oracle.cpp", "sim_oracle.cpp")]
+SRCS = [os.path.join(HERE, f) for f in ("graph_oracle.cpp", "sim_oracle.cpp", "pred_oracle.cpp")]
 DEPS = SRCS + [os.path.join(HERE, "graph_oracle.hpp"),
                os.path.join(os.path.dirname(HERE), "include", "fantoch_amd.h")]
 
@@ -39,6 +39,8 @@ def load():
         lib.oracle_batch_execute.restype = ctypes.c_int
         lib.oracle_batch_execute.argtypes = [vp, vp, vp, u32, u32, u32, vp, u32, u32, vp, vp, vp,
                                              vp, vp, ctypes.c_int, vp, vp]
+        lib.oracle_pred_batch.restype = ctypes.c_int
+        lib.oracle_pred_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, u32, u32, u32, u32, vp, vp, vp, vp, u32]
         lib.oracle_graph_new.restype = vp
         lib.oracle_graph_new.argtypes = [u32, u32]
         lib.oracle_graph_free.argtypes = [vp]
@@ -86,6 +88,29 @@ def batch_execute(planes, execute_at_commit=False, init_frontier=None, threads=1
         mp.ctypes.data if stats else None, mw.ctypes.data if stats else None)
     if stats:
         return order, release, nexec, err, mp, mw
+    return order, release, nexec, err
+
+
+def pred_batch_execute(planes, clock_lo, clock_hi, execute_at_commit=False, threads=1, ndeps=None):
+    """PredecessorsGraph (pred/mod.rs) over every stream of a host batch with
+    packed Caesar clock planes ((seq << 8 | process id) split in two u32
+    planes).  Returns (order, release, nexec, err) in the GPU plane layout."""
+    lib = load()
+    pw = planes.plane
+    order = np.zeros(pw, np.uint32)
+    release = np.zeros(pw, np.uint32)
+    nexec = np.zeros(planes.S, np.uint32)
+    err = np.zeros(planes.S, np.uint32)
+    lengths = None
+    if planes.lengths is not None:
+        lengths = np.ascontiguousarray(planes.lengths, np.uint32)
+    clo = np.ascontiguousarray(clock_lo, np.uint32)
+    chi = np.ascontiguousarray(clock_hi, np.uint32)
+    nd = None if ndeps is None else np.ascontiguousarray(ndeps, np.uint32)
+    lib.oracle_pred_batch(planes.dot.ctypes.data, planes.hdr.ctypes.data, planes.deps.ctypes.data, clo.ctypes.data,
+                          chi.ctypes.data, nd.ctypes.data if nd is not None else None,
+                          lengths.ctypes.data if lengths is not None else None, planes.S, planes.steps, planes.dmax, planes.n, 2 if execute_at_commit else 0, order.ctypes.data,
+                          release.ctypes.data, nexec.ctypes.data, err.ctypes.data, int(threads))
     return order, release, nexec, err
 
 

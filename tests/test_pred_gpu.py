@@ -1,0 +1,68 @@
+"""GPU predecessors executor (fx_pred_run / fx_pred_execute) vs the oracle
+(oracle/pred_oracle.cpp), bit for bit: order plane, release plane, nexec,
+status and the ExecutionDelay histogram.  GPU only."""
+import itertools
+
+import numpy as np
+import pytest
+
+import pred_shapes as P
+from fantoch_amd import _lib
+from fantoch_amd import device as fd
+from oracle import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+def check(streams, n, **kw):
+    planes, clo, chi, nd = P.pack_pred_streams(streams, n)
+    res = fd.run_pred(planes, clo, chi, ndeps=nd, **kw)
+    o_order, o_rel, o_nexec, o_err = O.pred_batch_execute(
+        planes, clo, chi, threads=8, ndeps=nd, execute_at_commit=kw.get("execute_at_commit", False))
+    assert res.status == (int(o_err[o_err != 0][0]) if np.any(o_err) else 0)
+    assert np.array_equal(res.err, o_err)
+    assert np.array_equal(res.nexec, o_nexec)
+    for s in range(planes.S):
+        rows = _lib.index(np.arange(int(o_nexec[s])), s, planes.steps)
+        assert np.array_equal(res.order[rows], o_order[rows]), "order differs on stream %d" % s
+        L = planes.steps if planes.lengths is None else int(planes.lengths[s])
+        rr = _lib.index(np.arange(L), s, planes.steps)
+        assert np.array_equal(res.release[rr], o_rel[rr]), "release differs on stream %d" % s
+    return planes, res
+
+
+def test_simple_kat():
+    planes, res = check([P.SIMPLE], 2)
+    order = [int(x) & 0x7FFFFFFF for x in res.order[_lib.index(np.arange(2), 0, planes.steps)]]
+    assert order == P.SIMPLE_ORDER
+
+
+def test_random_kat_permutations():
+    streams = []
+    for args in P.random_cases():
+        for perm in itertools.permutations(range(len(args))):
+            streams.append([(args[i][0], args[i][1], t, (args[i][2], 1)) for t, i in enumerate(perm)])
+    planes, res = check(streams, 2)
+    assert np.all(res.nexec == planes.lengths)
+
+
+@pytest.mark.parametrize("hbm", [False, True])
+@pytest.mark.parametrize("n,events,keys,window", [(3, 40, 8, 0), (5, 30, 16, 12), (2, 80, 4, 0), (4, 16, 32, 4)])
+def test_random_streams(hbm, n, events, keys, window):
+    streams = P.random_streams(7, 24, n, events, keys=keys, window=window)
+    check(streams, n, hbm=hbm)
+
+
+def test_execute_at_commit_and_errors():
+    check([P.SIMPLE], 2, execute_at_commit=True)
+    dup = [((1, 1), [(2, 1)], 0, (2, 1)), ((1, 1), [], 1, (3, 1))]
+    planes, res = check([dup, P.SIMPLE], 2)
+    assert res.err[0] == _lib.FX_ERR_DOUBLE_INDEX
+
+
+def test_very_wide_deps():
+    """~220 deps per commit: the LDS tables shrink to 128 vertices, the
+    streams outgrow them and rerun on the HBM tables."""
+    streams = P.random_streams(3, 8, 2, 110, keys=3, reverse_pct=80)
+    planes, res = check(streams, 2)
+    assert planes.dmax > 200 and res.reruns == 8 and np.all(res.nexec == planes.lengths)
