@@ -68,8 +68,12 @@ struct fx_graph_executor {
   std::vector<Cmd> cmds;
   bool have_base = false;
   uint64_t t_base = 0;
-  uint32_t init_frontier[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  bool use_frontier = false;
+  // per-source sequence base: the device sees seq - base[source - 1] (24-bit),
+  // the boundary takes any u32 sequence.  base = the executed frontier the
+  // handle starts from (fx_graph_executor_set_executed_frontier), else 0; deps
+  // at or below it are executed, which handle_add skips (mod.rs find_scc), so
+  // they are dropped on the way in.
+  uint32_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   // device mirror
   uint32_t cap = 0;      // plane rows
@@ -187,16 +191,8 @@ int flush(fx_graph_executor* ex) {
     uint32_t flags = FX_FLAG_SAVE_STATE;
     if (ex->processed == 0) flags |= FX_FLAG_INIT;
     if (ex->cfg.execute_at_commit) flags |= FX_FLAG_EXECUTE_AT_COMMIT;
-    DevBuf d_front;
-    const uint32_t* front = nullptr;
-    if (ex->processed == 0 && ex->use_frontier) {
-      if (!d_front.ensure(32) ||
-          hipMemcpyAsync(d_front.p, ex->init_frontier, 32, hipMemcpyHostToDevice, ex->stream))
-        return ex->sticky = FX_ERR_HIP;
-      front = d_front.u32();
-    }
     int st = fx_batch_execute(&in, &out, ex->tier, nullptr, 1, ex->d_state.p, ex->processed, N, flags,
-                              front, ex->stream);
+                              nullptr, ex->stream);
     if (st) return ex->sticky = st;
     if (hipMemcpyAsync(&nexec, ex->d_nexec.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipMemcpyAsync(&err, ex->d_err.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
@@ -254,7 +250,7 @@ int flush(fx_graph_executor* ex) {
       const uint64_t delay = (uint64_t)FX_HDR_T(ex->hdrs[rs]) - FX_HDR_T(ex->hdrs[rec]);
       ex->execution_delay[delay] += 1;  // ExecutionDelay (mod.rs:514-518)
     }
-    ex->executed.emplace_back(ex->dots[rec], start);
+    ex->executed.emplace_back(ex->dots[rec], start);  // device-local sequence
     const Cmd& c = ex->cmds[rec];
     for (uint32_t key : c.keys) {
       ex->to_clients.push_back(fx_executor_result{c.rifl, key, c.read_only});
@@ -270,7 +266,9 @@ int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys
   if (!ex) return FX_ERR_INVALID_ARG;
   if (ex->sticky) return ex->sticky;
   if (ex->executor_index != 0) return FX_ERR_INVALID_ARG;  // mod.rs:220 assert_eq!(executor_index, 0)
-  if (dot.source < 1 || dot.source > ex->cfg.n || dot.seq < 1 || dot.seq > FX_SEQ_MASK) return FX_ERR_DOT_RANGE;
+  if (dot.source < 1 || dot.source > ex->cfg.n || dot.seq <= ex->base[dot.source - 1] ||
+      dot.seq - ex->base[dot.source - 1] > FX_SEQ_MASK)
+    return FX_ERR_DOT_RANGE;
   if (ndeps && !deps) return FX_ERR_INVALID_ARG;
   if (nkeys && !keys) return FX_ERR_INVALID_ARG;
   if (!ex->have_base) {
@@ -281,9 +279,11 @@ int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys
   std::vector<uint32_t> dv;
   dv.reserve(ndeps);
   for (uint32_t j = 0; j < ndeps; ++j) {
-    if (deps[j].source < 1 || deps[j].source > 255 || deps[j].seq < 1 || deps[j].seq > FX_SEQ_MASK)
-      return FX_ERR_DOT_RANGE;
-    dv.push_back(FX_PACK_DOT(deps[j].source, deps[j].seq));
+    if (deps[j].source < 1 || deps[j].source > 255 || deps[j].seq < 1) return FX_ERR_DOT_RANGE;
+    const uint32_t b = deps[j].source <= ex->cfg.n ? ex->base[deps[j].source - 1] : 0;
+    if (deps[j].seq <= b) continue;  // executed before the handle started
+    if (deps[j].seq - b > FX_SEQ_MASK) return FX_ERR_DOT_RANGE;
+    dv.push_back(FX_PACK_DOT(deps[j].source, deps[j].seq - b));
   }
   std::sort(dv.begin(), dv.end());  // canonical C1 (executor.rs:76 iterates a HashSet)
   dv.erase(std::unique(dv.begin(), dv.end()), dv.end());
@@ -295,7 +295,7 @@ int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys
   std::sort(c.keys.begin(), c.keys.end());
   c.keys.erase(std::unique(c.keys.begin(), c.keys.end()), c.keys.end());
   c.read_only = read_only;
-  ex->dots.push_back(FX_PACK_DOT(dot.source, dot.seq));
+  ex->dots.push_back(FX_PACK_DOT(dot.source, dot.seq - ex->base[dot.source - 1]));
   ex->hdrs.push_back(FX_MAKE_HDR((uint32_t)(now_ms - ex->t_base), (uint32_t)dv.size(), kind));
   ex->deps.push_back(std::move(dv));
   ex->cmds.push_back(std::move(c));
@@ -346,12 +346,10 @@ int fx_graph_executor_index_only(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl
 
 int fx_graph_executor_set_executed_frontier(fx_graph_executor* ex, const uint64_t* frontier, uint32_t n) {
   if (!ex || !frontier || n > 8 || n > ex->cfg.n) return FX_ERR_INVALID_ARG;
-  if (ex->processed > 0) return FX_ERR_INVALID_ARG;
-  for (uint32_t p = 0; p < n; ++p) {
-    if (frontier[p] > FX_SEQ_MASK) return FX_ERR_DOT_RANGE;
-    ex->init_frontier[p] = (uint32_t)frontier[p];
-  }
-  ex->use_frontier = true;
+  if (!ex->dots.empty()) return FX_ERR_INVALID_ARG;
+  for (uint32_t p = 0; p < n; ++p)
+    if (frontier[p] > 0xFFFFFFFFull) return FX_ERR_DOT_RANGE;
+  for (uint32_t p = 0; p < n; ++p) ex->base[p] = (uint32_t)frontier[p];
   return FX_OK;
 }
 
@@ -377,7 +375,8 @@ int fx_graph_executor_drain_dots(fx_graph_executor* ex, fx_dot* out, uint8_t* sc
   while (c < cap && !ex->executed.empty()) {
     const auto e = ex->executed.front();
     ex->executed.pop_front();
-    out[c] = fx_dot{FX_DOT_SRC(e.first), FX_DOT_SEQ(e.first)};
+    const uint32_t src = FX_DOT_SRC(e.first);
+    out[c] = fx_dot{src, FX_DOT_SEQ(e.first) + ex->base[src - 1]};
     if (scc_start) scc_start[c] = e.second ? 1 : 0;
     ++c;
   }
@@ -439,8 +438,9 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
   uint32_t m = 0;
   for (const auto& e : pw) {
     if (m < cap) {
-      dots[m] = fx_dot{FX_DOT_SRC(e.first), FX_DOT_SEQ(e.first)};
-      waiting_on[m] = fx_dot{FX_DOT_SRC(e.second), FX_DOT_SEQ(e.second)};
+      const uint32_t s0 = FX_DOT_SRC(e.first), s1 = FX_DOT_SRC(e.second);
+      dots[m] = fx_dot{s0, FX_DOT_SEQ(e.first) + ex->base[s0 - 1]};
+      waiting_on[m] = fx_dot{s1, FX_DOT_SEQ(e.second) + (s1 >= 1 && s1 <= ex->cfg.n ? ex->base[s1 - 1] : 0)};
     }
     ++m;
   }

@@ -176,14 +176,33 @@ def replay(data, n, f=1, now_ms=None, monitor=True):
     return ex
 
 
-def log_stream(log, now_ms=None):
-    """A decoded log as one commit stream for the batched executor: [(dot, deps, t_ms)]."""
-    out = []
-    for i, (dot, _rifl, _keys, deps, _ro) in enumerate(log):
-        if dot[1] > _lib.FX_SEQ_MASK or any(q > _lib.FX_SEQ_MASK for _, q in deps):
-            raise _lib.FxError(_lib.FX_ERR_DOT_RANGE, "log_stream: sequence >= 2^24")
-        out.append((dot, deps, now_ms(i) if now_ms else 0))
+def renumbering(log):
+    """Per-source rank of every sequence the log names (Add dots and deps):
+    {source: sorted sequences}.  A whole log is known up front, so its dots can
+    be renumbered by rank, which keeps every per-source comparison the executor
+    makes (AEClock frontier / membership, dot order) and fits any u32 sequence
+    into the stream format's 24 bits."""
+    seqs = {}
+    for dot, _rifl, _keys, deps, _ro in log:
+        seqs.setdefault(dot[0], set()).add(dot[1])
+        for s, q in deps:
+            seqs.setdefault(s, set()).add(q)
+    out = {s: sorted(v) for s, v in seqs.items()}
+    if any(len(v) > _lib.FX_SEQ_MASK for v in out.values()):
+        raise _lib.FxError(_lib.FX_ERR_DOT_RANGE, "log_stream: more than 2^24 - 1 sequences of one source")
     return out
+
+
+def log_stream(log, now_ms=None, ranks=None):
+    """A decoded log as one commit stream for the batched executor: [(dot, deps,
+    t_ms)], dots renumbered per source by rank (`renumbering`)."""
+    import bisect
+    ranks = ranks if ranks is not None else renumbering(log)
+
+    def local(d):
+        return (d[0], bisect.bisect_left(ranks[d[0]], d[1]) + 1)
+    return [(local(dot), [local(d) for d in deps], now_ms(i) if now_ms else 0)
+            for i, (dot, _rifl, _keys, deps, _ro) in enumerate(log)]
 
 
 def replay_batch(logs, n, execute_at_commit=False):

@@ -341,7 +341,10 @@ int fx_graph_executor_index_only(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl
                                  const uint32_t* keys, uint32_t nkeys,
                                  const fx_dot* deps, uint32_t ndeps, uint64_t now_ms);
 /* Test hook mirroring `queue.executed_clock = AEClock::from(..)` (mod.rs:1309-1315):
- * frontier[i] = highest contiguous executed seq of source i+1. Only before the first Add. */
+ * frontier[i] = highest contiguous executed seq of source i+1 (any u32). Only
+ * before the first Add.  Sequences: fx_dot.seq is any u32; the device holds
+ * seq - frontier (24 bits), so one handle spans 2^24 - 1 sequence numbers per
+ * source above the frontier it starts from (FX_ERR_DOT_RANGE beyond). */
 int fx_graph_executor_set_executed_frontier(fx_graph_executor* ex, const uint64_t* frontier, uint32_t n);
 /* Executor::to_clients (executor.rs:95-97): pops up to cap results in execution order. */
 int fx_graph_executor_to_clients(fx_graph_executor* ex, fx_executor_result* out, uint32_t cap, uint32_t* n_out);

@@ -146,3 +146,40 @@ def test_replay_batch_matches_single_replay_and_oracle(gpu):
     assert (res.err == 0).all()
     assert got == exp
     assert got[0] == [d for d, _ in L.replay(logs[0], 3).drain_dots()]
+
+
+def stretched_log(seed, n, cmds):
+    """synth_log with every sequence s mapped to 2^31 + 7919 s (gaps, and far
+    beyond the stream format's 24 bits)."""
+    stream, _ = synth_log(seed=seed, n=n, cmds=cmds)
+    big = lambda d: (d[0], 2**31 + 7919 * d[1])
+    payloads = [L.encode_add(big(dot), (dot[0], dot[1]), {0: {"k": [L.GET]}}, [(big(d), None) for d in deps])
+                for dot, deps, _, _ in stream]
+    return stream, big, b"".join(L.frame(x) for x in payloads)
+
+
+def test_log_renumbering_preserves_the_execution_order():
+    """Rank renumbering per source (log_stream) executes exactly like the
+    original sequences: the oracle over both, mapped back."""
+    stream, big, data = stretched_log(8, 3, 150)
+    log = L.read_log(data)
+    ranks = L.renumbering(log)
+    local = L.log_stream(log, ranks=ranks)
+    assert max(q for (_, q), _, _ in local) < 2**24
+    g1, g2 = oracle_lib.Graph(1, 3), oracle_lib.Graph(1, 3)
+    for (dot, deps, _, _), (ldot, ldeps, _) in zip(stream, local):
+        g1.handle_add(dot, deps)
+        g2.handle_add(ldot, sorted(ldeps))
+    back = lambda d: (d[0], (ranks[d[0]][d[1] - 1] - 2**31) // 7919)
+    assert [back(d) for d, _, _ in g2.drain()] == [d for d, _, _ in g1.drain()]
+
+
+@pytest.mark.gpu
+def test_replay_batch_of_u32_sequences(gpu):
+    stream, big, data = stretched_log(9, 3, 150)
+    g = oracle_lib.Graph(1, 3)
+    for dot, deps, _, _ in stream:
+        g.handle_add(dot, deps)
+    got, res = L.replay_batch([data], 3)
+    assert (res.err == 0).all()
+    assert got[0] == [big(d) for d, _, _ in g.drain()]

@@ -401,6 +401,30 @@ def test_executor_drain_after_every_add_is_linear(gpu):
     assert per_add_large < 2.0 * per_add_small + 64, (per_add_small, per_add_large)
 
 
+def test_executor_u32_sequences_above_the_frontier(gpu):
+    """Sequences near 2^32 - 1: the handle starts from an executed frontier F
+    and holds seq - F on the device; the run equals the same stream at F = 0."""
+    p = fs.synth_params(seed=12, n=3, instances=1, cmds=300, window=8, cycle_pct=30)
+    stream = fs.synth_host(p).stream(0)
+    F = 2**32 - 1 - 2000
+    runs = []
+    for base in (0, F):
+        ex = GraphExecutor(1, 0, 3, monitor=False)
+        if base:
+            ex.set_executed_frontier([base] * 3)
+        shift = lambda d: (d[0], d[1] + base)
+        for i, (dot, deps, t, _kind) in enumerate(stream):
+            ex.handle_add(shift(dot), dot, [0], [shift(d) for d in deps] + ([(1, base)] if base else []), t)
+            if i % 50 == 0:
+                ex.to_clients_iter()
+        runs.append([((d[0], d[1] - base), s) for d, s in ex.drain_dots()])
+    assert runs[0] == runs[1] and len(runs[0]) > 0
+    ex = GraphExecutor(1, 0, 3, monitor=False)
+    ex.set_executed_frontier([F] * 3)
+    with pytest.raises(_lib.FxError):
+        ex.handle_add((1, F), (1, 1), [0], [], 0)  # at or below the frontier: executed
+
+
 def test_cpp_executor_tests(gpu):
     exe = os.path.join(ROOT, "tests", "cpp", "build", "test_graph_executor")
     assert os.path.exists(exe), "build with `make`"
