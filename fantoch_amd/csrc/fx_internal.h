@@ -28,6 +28,7 @@ struct KArgs {
   const uint32_t* init_frontier;
   uint32_t* dbg;  // per-lane diagnostic counters (FX_LANE_DEBUG), normally null
   const uint32_t* lanes_dev;  // device lane count (FX_TIER_SPLIT sub-launches), normally null
+  uint32_t drift;             // lane tier: max blocks (4 steps) a lane runs ahead of the slowest, 0 = unbounded
 };
 
 // Lane-per-stream executor tiers (graph_exec.hip) and the 16-lanes-per-stream

@@ -628,45 +628,68 @@ void k_graph_lane(KArgs a) {
     return make_uint4(v[0], v[1], v[2], v[3]);
   };
 
-  // 2-block pipeline: c = block blk (readable); block blk + 1 is in x when this
-  // lane loaded it at the last refill (xl), else in xo (kept from before)
+  // Pipeline: c = block blk (readable); x = block blk + 1 (dot / hdr, and the
+  // dep planes its headers need); y = dot / hdr of block blk + 2.  A lane that
+  // moves to the next block issues the dep loads of its new x, skipping the
+  // planes no Add of that block uses (the headers came one block earlier, in
+  // y), and the dot / hdr loads of its new y, into t; the next refill merges t
+  // (tl: t holds this lane's loads).  Sparse streams so read ~3 of the 2 + DC
+  // planes.
   uint32_t i = a.step_begin;
   uint32_t blk = i >> 2;
-  uint4 c[NP], x[NP], xo[NP];
+  uint4 c[NP], x[NP], y[2], t[NP];
 #pragma unroll
   for (uint32_t p = 0; p < NP; ++p) c[p] = ld(boff(blk), p);
 #pragma unroll
   for (uint32_t p = 0; p < NP; ++p) x[p] = ld(boff(blk + 1), p);
 #pragma unroll
-  for (uint32_t p = 0; p < NP; ++p) xo[p] = make_uint4(0, 0, 0, 0);
-  uint32_t xl = ~0u;  // all-ones: x holds block blk + 1
+  for (uint32_t p = 0; p < 2; ++p) y[p] = ld(boff(blk + 2), p);
+#pragma unroll
+  for (uint32_t p = 0; p < NP; ++p) t[p] = make_uint4(0, 0, 0, 0);
+  uint32_t tl = 0;  // all-ones: t holds the loads of the last refill
+  // Drift bound: a lane moves to block blk + 1 only while that block is fewer
+  // than `drift` blocks past the slowest live lane's, so the lanes of a
+  // wavefront read (and write) each 1 KiB tile row within a short window and
+  // the row's cache lines are fetched once instead of once per straggler.
+  const uint32_t drift = a.drift ? a.drift : 0xFFFFFFFFu;
+  auto mset = [](uint4& d, const uint4& v, uint32_t m) {
+    d.x = (v.x & m) | (d.x & ~m);
+    d.y = (v.y & m) | (d.y & ~m);
+    d.z = (v.z & m) | (d.z & ~m);
+    d.w = (v.w & m) | (d.w & ~m);
+  };
 
   for (uint32_t it = 0;; ++it) {
     if ((it & 3u) == 0) {
       const bool live = e.phase != PH_IDLE || (i < lim && !e.err);
       if (!__any(live)) break;
-      // lanes that have consumed their c block take block blk + 1; every lane
-      // then issues the same NP loads, in range only for the lanes that moved
-      const bool sh = (i >> 2) > blk;
-      blk += sh ? 1u : 0u;
-      const uint32_t m = 0u - (uint32_t)sh;  // masks, not selects (a select of the two
-#pragma unroll                               // arrays becomes a select of their addresses)
-      for (uint32_t p = 0; p < NP; ++p) {
-        uint4 e4;
-        e4.x = (x[p].x & xl) | (xo[p].x & ~xl);
-        e4.y = (x[p].y & xl) | (xo[p].y & ~xl);
-        e4.z = (x[p].z & xl) | (xo[p].z & ~xl);
-        e4.w = (x[p].w & xl) | (xo[p].w & ~xl);
-        c[p].x = (e4.x & m) | (c[p].x & ~m);
-        c[p].y = (e4.y & m) | (c[p].y & ~m);
-        c[p].z = (e4.z & m) | (c[p].z & ~m);
-        c[p].w = (e4.w & m) | (c[p].w & ~m);
-        xo[p] = e4;
-      }
-      xl = m;
-      const uint32_t off = sh ? boff(blk + 1) : OOB;
+      uint32_t lo = (i < lim && !e.err) ? (i >> 2) : 0xFFFFFFFFu;
+      if (drift != 0xFFFFFFFFu) {
 #pragma unroll
-      for (uint32_t p = 0; p < NP; ++p) x[p] = ld(off, p);
+        for (uint32_t o = 1; o < 64; o <<= 1) lo = min(lo, (uint32_t)__shfl_xor((int)lo, (int)o));
+      }
+      // merge the last refill's loads (masks, not selects: a select of two
+      // arrays becomes a select of their addresses)
+#pragma unroll
+      for (uint32_t p = 2; p < NP; ++p) mset(x[p], t[p], tl);
+      mset(y[0], t[0], tl);
+      mset(y[1], t[1], tl);
+      const bool sh = (i >> 2) > blk && (drift == 0xFFFFFFFFu || lo == 0xFFFFFFFFu || blk + 1 < lo + drift);
+      blk += sh ? 1u : 0u;
+      const uint32_t m = 0u - (uint32_t)sh;
+#pragma unroll
+      for (uint32_t p = 0; p < NP; ++p) mset(c[p], x[p], m);
+      mset(x[0], y[0], m);
+      mset(x[1], y[1], m);
+      tl = m;
+      // deps the new x block's Adds carry (its headers are in x[1] now)
+      const uint4 h = x[1];
+      const uint32_t nd = max(max(FX_HDR_ND(h.x), FX_HDR_ND(h.y)), max(FX_HDR_ND(h.z), FX_HDR_ND(h.w)));
+      const uint32_t offx = sh ? boff(blk + 1) : OOB, offy = sh ? boff(blk + 2) : OOB;
+#pragma unroll
+      for (uint32_t p = 0; p < 2; ++p) t[p] = ld(offy, p);
+#pragma unroll
+      for (uint32_t j = 0; j < DC; ++j) t[2 + j] = ld(j < nd ? offx : OOB, 2 + j);
     }
     // a lane consumes at most one step per iteration, so between two refills
     // it never runs past the end of x; it only waits (at most 3 iterations)
@@ -727,6 +750,9 @@ static uint32_t decode(const uint32_t* block, uint32_t lane, uint32_t* dots, uin
   return c;
 }
 
+// drift bound of k_graph_lane in blocks (FX_LANE_DRIFT overrides; 0 = unbounded)
+constexpr uint32_t DEFAULT_DRIFT = 4;
+
 // instantiation for a batch: sources rounded to 5 / 8, deps to 3 / 5 / 8
 #define FX_LANE_DISPATCH(F, ...)                                         \
   do {                                                                   \
@@ -742,7 +768,13 @@ static uint32_t decode(const uint32_t* block, uint32_t lane, uint32_t* dots, uin
 
 }  // namespace lane
 
-static int launch_lane_d(const KArgs& a, hipStream_t stream) {
+static int launch_lane_d(const KArgs& a0, hipStream_t stream) {
+  static const uint32_t drift = [] {
+    const char* e = getenv("FX_LANE_DRIFT");
+    return e ? (uint32_t)atoi(e) : lane::DEFAULT_DRIFT;
+  }();
+  KArgs a = a0;
+  a.drift = drift;
   const uint32_t n = a.n, dmax = a.dmax;
   FX_LANE_DISPATCH(lane::launch_t, a, stream);
 }

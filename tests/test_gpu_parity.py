@@ -114,19 +114,19 @@ def test_tier_reruns_happen_and_match(gpu):
     assert_parity(planes, res)
 
 
-def test_capacity_is_reported_exactly(gpu):
-    """Streams that need more than 64 pending vertices (every tier's ceiling)
-    stop with FX_ERR_CAPACITY after the reruns; all others match the oracle."""
+def test_capacity_escalates_past_64_pending(gpu):
+    """Streams that need more than 64 pending vertices (the ceiling of tiers
+    0-6) escalate to the wide tiers (1024 / 16384 pending) and execute exactly
+    like the oracle; nothing stops on FX_ERR_CAPACITY."""
     p = fs.synth_params(seed=5, n=5, instances=10, cmds=300, window=120, cycle_pct=70,
                         conflicts=(100, 50))
     planes = fs.synth_host(p)
     res = fd.run_batch(planes, metrics=False)
     o_order, o_rel, o_nexec, o_err, mp, _ = oracle_lib.batch_execute(planes, threads=8, stats=True)
-    over, fits = mp > 64, mp < 64
-    assert over.any() and fits.any()
-    assert np.all(res.err[over] == _lib.FX_ERR_CAPACITY)
-    assert np.all(res.err[fits] == 0) and np.all(o_err == 0)
-    for s in np.flatnonzero(fits):
+    assert (mp > 64).any() and (mp < 64).any()
+    assert np.all(res.err == 0) and np.all(o_err == 0)
+    assert res.tier_counts[_lib.FX_TIER_WIDE] + res.tier_counts[_lib.FX_TIER_WIDE_HBM] >= int((mp > 64).sum())
+    for s in range(planes.S):
         idx = _lib.index(np.arange(int(o_nexec[s])), s, planes.steps)
         assert res.nexec[s] == o_nexec[s]
         assert np.array_equal(res.order[idx], o_order[idx])
