@@ -44,7 +44,7 @@ LAYOUT = {0: "16 lanes per stream", 1: "one lane per stream", 2: "one lane per s
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["sim", "executor", "huge", "dense", "placements"], default="sim",
+    ap.add_argument("--mode", choices=["sim", "executor", "huge", "dense", "placements", "pred"], default="sim",
                     help="sim: the batched simulator (BASELINE configs[1], the headline); "
                          "executor: the GraphExecutor alone over synthetic commit streams")
     ap.add_argument("--gpus", type=int, default=1)
@@ -128,6 +128,9 @@ def main():
     if args.mode == "dense":
         from bench_huge import main_dense
         return main_dense(args)
+    if args.mode == "pred":
+        from bench_pred import main_pred
+        return main_pred(args)
     if args.mode == "placements":
         from bench_placements import main_placements
         return main_placements(args)

@@ -51,6 +51,7 @@ FX_FLAG_EXECUTE_AT_COMMIT = 2
 FX_FLAG_SAVE_STATE = 4
 FX_TIER_WIDE, FX_TIER_WIDE_HBM = 7, 8
 FX_NUM_TIERS = 9
+FX_PRED_TIER_SMALL, FX_PRED_TIER_LDS, FX_PRED_TIER_HBM = 0, 1, 2
 FX_TIER_GROUP = 0
 FX_TIER_WAVE = 4
 FX_TIER_LANE_REG = 5
@@ -199,8 +200,8 @@ SIGNATURES = [
      [ctypes.POINTER(StreamBatch), ctypes.POINTER(OrderBatch), ctypes.c_uint32, ctypes.c_void_p,
       u32p]),
     ("fx_pred_execute", ctypes.c_int,
-     [ctypes.POINTER(PredBatch), ctypes.POINTER(OrderBatch), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
-      ctypes.c_uint32, ctypes.c_void_p]),
+     [ctypes.POINTER(PredBatch), ctypes.POINTER(OrderBatch), ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     ("fx_pred_state_bytes", ctypes.c_size_t, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     ("fx_pred_run", ctypes.c_int,
      [ctypes.POINTER(PredBatch), ctypes.POINTER(OrderBatch), ctypes.c_uint32, ctypes.c_void_p, u32p]),

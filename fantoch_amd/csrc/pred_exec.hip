@@ -347,15 +347,21 @@ __global__ __launch_bounds__(64) void k_pred(PArgs a, Lay L) {
 
 }  // namespace pred
 
-// LDS tables: the most vertices of 512 / 256 / 128 whose tables fit 160 KiB
-// (2 index slots per vertex and source, 2048-bit windows, waiter lists 4 per
-// vertex); words == 0 when none fits.  HBM tables: 8192 vertices (16384 index
-// slots, 32768-bit windows, lists 8 per vertex).
-static pred::Lay pred_layout(bool hbm, uint32_t n, uint32_t dmax) {
+// SMALL: 64 vertices (128 index slots per source, 1024-bit windows, lists 4
+// per vertex).  LDS: the most vertices of 512 / 256 / 128 whose tables fit
+// 160 KiB (2 index slots per vertex and source, 2048-bit windows, lists 4 per
+// vertex).  words == 0 when a tier does not fit.  HBM: 8192 vertices (16384
+// index slots, 32768-bit windows, lists 8 per vertex).
+static pred::Lay pred_layout(uint32_t tier, uint32_t n, uint32_t dmax) {
   pred::Lay L;
   const uint32_t D = std::max(dmax, 1u);
-  if (hbm) {
+  if (tier == FX_PRED_TIER_HBM) {
     L.make(8192, 16384, 1024, n, D, 8 * 8192);
+    return L;
+  }
+  if (tier == FX_PRED_TIER_SMALL) {
+    L.make(64, 128, 32, n, D, 4 * 64);
+    if ((size_t)L.words * 4 > 160 * 1024) L.words = 0;
     return L;
   }
   for (uint32_t P = 512; P >= 128; P /= 2) {
@@ -371,11 +377,12 @@ static pred::Lay pred_layout(bool hbm, uint32_t n, uint32_t dmax) {
 using namespace fx;
 
 extern "C" size_t fx_pred_state_bytes(uint32_t n, uint32_t dmax, uint32_t lanes) {
-  return (size_t)pred_layout(true, n, dmax).words * 4 * lanes;
+  return (size_t)pred_layout(FX_PRED_TIER_HBM, std::max(n, 1u), dmax).words * 4 * lanes;
 }
 
 extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* out, const uint32_t* stream_map,
-                               uint32_t num_lanes, void* state, uint32_t flags, void* hip_stream) {
+                               uint32_t num_lanes, uint32_t tier, void* state, uint32_t flags,
+                               void* hip_stream) {
   if (!in || !out || !in->base.dot || !in->base.hdr || (in->base.dmax && !in->base.deps) || !in->clock_lo ||
       !in->clock_hi || !out->order || !out->release || !out->nexec || !out->err)
     return FX_ERR_INVALID_ARG;
@@ -384,8 +391,9 @@ extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* ou
     return FX_ERR_INVALID_ARG;
   if (fx_device_count() <= 0) return FX_ERR_NO_DEVICE;
   if (!stream_map && num_lanes > in->base.num_streams) return FX_ERR_INVALID_ARG;
+  if (tier > FX_PRED_TIER_HBM || (tier == FX_PRED_TIER_HBM) != (state != nullptr)) return FX_ERR_INVALID_ARG;
   if (num_lanes == 0) return FX_OK;
-  const bool hbm = state != nullptr;
+  const bool hbm = tier == FX_PRED_TIER_HBM;
   pred::PArgs a{};
   a.k.dot = in->base.dot;
   a.k.hdr = in->base.hdr;
@@ -407,7 +415,7 @@ extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* ou
   a.clo = in->clock_lo;
   a.chi = in->clock_hi;
   a.ndeps = in->ndeps;
-  const pred::Lay L = pred_layout(hbm, in->base.n, in->base.dmax);
+  const pred::Lay L = pred_layout(tier, in->base.n, in->base.dmax);
   hipStream_t hs = (hipStream_t)hip_stream;
   if (hbm) {
     hipLaunchKernelGGL(pred::k_pred<true>, dim3(num_lanes), dim3(64), 0, hs, a, L);
@@ -424,40 +432,49 @@ extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* ou
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 
-// All streams on the LDS tables, then the ones that ran out of capacity on
-// the HBM tables.  Synchronous.
+// Every stream at SMALL, then the ones that ran out of capacity at LDS, then
+// HBM (tiers whose tables do not fit are skipped).  Synchronous.
 extern "C" int fx_pred_run(const fx_pred_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
                            uint32_t* reruns) {
   if (reruns) *reruns = 0;
   if (!in) return FX_ERR_INVALID_ARG;
-  const uint32_t S = in->base.num_streams;
+  const uint32_t S = in->base.num_streams, n = std::max(in->base.n, 1u);
   hipStream_t hs = (hipStream_t)hip_stream;
-  std::vector<uint32_t> err(S, FX_ERR_CAPACITY);
-  const bool lds = pred_layout(false, std::max(in->base.n, 1u), in->base.dmax).words != 0;
-  if (lds) {  // else every stream goes to the HBM tables
-    int st = fx_pred_execute(in, out, nullptr, S, nullptr, flags, hip_stream);
+  std::vector<uint32_t> err(S), todo;
+  bool first = true;
+  uint32_t rr = 0;
+  for (uint32_t tier = FX_PRED_TIER_SMALL; tier <= FX_PRED_TIER_HBM; ++tier) {
+    if (pred_layout(tier, n, in->base.dmax).words == 0) continue;
+    int st;
+    if (first) {
+      st = fx_pred_execute(in, out, nullptr, S, tier, nullptr, flags, hip_stream);
+    } else {
+      if (todo.empty()) break;
+      std::lock_guard<std::recursive_mutex> lock(scratch_mutex());
+      const uint32_t R = (uint32_t)todo.size();
+      uint32_t* dmap = (uint32_t*)scratch(SCRATCH_TIERED_MAP, (size_t)R * 4);
+      void* dstate = tier == FX_PRED_TIER_HBM ? scratch(SCRATCH_TIERED_STATE, fx_pred_state_bytes(n, in->base.dmax, R))
+                                              : nullptr;
+      if (!dmap || (tier == FX_PRED_TIER_HBM && !dstate)) return FX_ERR_HIP;
+      if (hipMemcpyAsync(dmap, todo.data(), (size_t)R * 4, hipMemcpyHostToDevice, hs) != hipSuccess) return FX_ERR_HIP;
+      st = fx_pred_execute(in, out, dmap, R, tier, dstate, flags, hip_stream);
+      rr += R;
+      if (!st && (hipMemcpyAsync(err.data(), out->err, (size_t)S * 4, hipMemcpyDeviceToHost, hs) != hipSuccess ||
+                  hipStreamSynchronize(hs) != hipSuccess))
+        return FX_ERR_HIP;
+    }
     if (st) return st;
-    if (hipMemcpyAsync(err.data(), out->err, (size_t)S * 4, hipMemcpyDeviceToHost, hs) != hipSuccess ||
-        hipStreamSynchronize(hs) != hipSuccess)
-      return FX_ERR_HIP;
+    if (first) {
+      if (hipMemcpyAsync(err.data(), out->err, (size_t)S * 4, hipMemcpyDeviceToHost, hs) != hipSuccess ||
+          hipStreamSynchronize(hs) != hipSuccess)
+        return FX_ERR_HIP;
+      first = false;
+    }
+    todo.clear();
+    for (uint32_t s = 0; s < S; ++s)
+      if (err[s] == FX_ERR_CAPACITY) todo.push_back(s);
   }
-  int st = 0;
-  std::vector<uint32_t> redo;
-  for (uint32_t s = 0; s < S; ++s)
-    if (err[s] == FX_ERR_CAPACITY) redo.push_back(s);
-  if (!redo.empty()) {
-    std::lock_guard<std::recursive_mutex> lock(scratch_mutex());
-    const uint32_t R = (uint32_t)redo.size();
-    uint32_t* dmap = (uint32_t*)scratch(SCRATCH_TIERED_MAP, (size_t)R * 4);
-    void* dstate = scratch(SCRATCH_TIERED_STATE, fx_pred_state_bytes(in->base.n, in->base.dmax, R));
-    if (!dmap || !dstate) return FX_ERR_HIP;
-    (void)hipMemcpyAsync(dmap, redo.data(), (size_t)R * 4, hipMemcpyHostToDevice, hs);
-    if ((st = fx_pred_execute(in, out, dmap, R, dstate, flags, hip_stream))) return st;
-    if (hipMemcpyAsync(err.data(), out->err, (size_t)S * 4, hipMemcpyDeviceToHost, hs) != hipSuccess ||
-        hipStreamSynchronize(hs) != hipSuccess)
-      return FX_ERR_HIP;
-    if (reruns) *reruns = lds ? R : 0;
-  }
+  if (reruns) *reruns = rr;
   for (uint32_t s = 0; s < S; ++s)
     if (err[s]) return (int)err[s];
   return FX_OK;

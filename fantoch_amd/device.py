@@ -133,10 +133,11 @@ def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096,
     return res
 
 
-def run_pred(planes, clock_lo, clock_hi, ndeps=None, execute_at_commit=False, hbm=False, nbins_delay=4096):
-    """PredecessorsExecutor (fx_pred_run, or one fx_pred_execute over HBM
-    tables with hbm=True) over a host batch with packed Caesar clock planes;
-    returns a BatchResult (delay histogram from fx_batch_metrics)."""
+def run_pred(planes, clock_lo, clock_hi, ndeps=None, execute_at_commit=False, tier=None, nbins_delay=4096):
+    """PredecessorsExecutor over a host batch with packed Caesar clock planes:
+    fx_pred_run (tier None: the escalation chain) or one fx_pred_execute at
+    `tier` (FX_PRED_TIER_*); returns a BatchResult (delay histogram from
+    fx_batch_metrics)."""
     lib = _lib.load()
     S, steps, pw = planes.S, planes.steps, planes.plane
     bufs = {}
@@ -159,9 +160,11 @@ def run_pred(planes, clock_lo, clock_hi, ndeps=None, execute_at_commit=False, hb
     outb = _lib.OrderBatch(order.ptr, release.ptr, nexec.ptr, err.ptr)
     flags = _lib.FX_FLAG_EXECUTE_AT_COMMIT if execute_at_commit else 0
     reruns = ctypes.c_uint32()
-    if hbm:
-        state = DeviceBuffer(lib.fx_pred_state_bytes(planes.n, planes.dmax, S))
-        status = lib.fx_pred_execute(ctypes.byref(inb), ctypes.byref(outb), None, S, state.ptr, flags, None)
+    if tier is not None:
+        state = DeviceBuffer(lib.fx_pred_state_bytes(planes.n, planes.dmax, S)) if tier == _lib.FX_PRED_TIER_HBM \
+            else None
+        status = lib.fx_pred_execute(ctypes.byref(inb), ctypes.byref(outb), None, S, tier,
+                                     state.ptr if state else None, flags, None)
         check(lib.fx_dev_synchronize(None), "sync")
     else:
         status = lib.fx_pred_run(ctypes.byref(inb), ctypes.byref(outb), flags, None, ctypes.byref(reruns))

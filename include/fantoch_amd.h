@@ -253,15 +253,20 @@ typedef struct fx_pred_batch {
                                  conflicting command: up to FX_PRED_MAX_DEPS), or
                                  NULL = FX_HDR_ND (dmax <= 31) */
 } fx_pred_batch;
-/* One launch over num_lanes streams (stream_map NULL = all): tables in LDS
- * (512 pending) when state == NULL, else in `state` (HBM, 8192 pending;
- * fx_pred_state_bytes).  Streams that run out report FX_ERR_CAPACITY.
- * Whole streams, from an empty executor; flags: FX_FLAG_EXECUTE_AT_COMMIT. */
+/* Table tiers: SMALL = LDS, 64 pending (many wavefronts per CU); LDS = LDS,
+ * the most of 512 / 256 / 128 pending that fit (FX_ERR_UNSUPPORTED if none
+ * does); HBM = tables in `state` (fx_pred_state_bytes), 8192 pending. */
+#define FX_PRED_TIER_SMALL 0u
+#define FX_PRED_TIER_LDS 1u
+#define FX_PRED_TIER_HBM 2u
+/* One launch over num_lanes streams (stream_map NULL = all) at one table
+ * tier.  Streams that run out report FX_ERR_CAPACITY.  Whole streams, from an
+ * empty executor; flags: FX_FLAG_EXECUTE_AT_COMMIT. */
 int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* out, const uint32_t* stream_map,
-                    uint32_t num_lanes, void* state, uint32_t flags, void* hip_stream);
+                    uint32_t num_lanes, uint32_t tier, void* state, uint32_t flags, void* hip_stream);
 size_t fx_pred_state_bytes(uint32_t n, uint32_t dmax, uint32_t lanes);
-/* Synchronous driver: LDS tables for all, HBM tables for the streams that ran
- * out of capacity; *reruns (optional) = streams rerun. */
+/* Synchronous driver: every stream at SMALL, then the streams that ran out of
+ * capacity at LDS, then HBM; *reruns (optional) = stream reruns in total. */
 int fx_pred_run(const fx_pred_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
                 uint32_t* reruns);
 

@@ -46,11 +46,24 @@ def test_random_kat_permutations():
     assert np.all(res.nexec == planes.lengths)
 
 
-@pytest.mark.parametrize("hbm", [False, True])
+@pytest.mark.parametrize("tier", [None, 0, 1, 2])
 @pytest.mark.parametrize("n,events,keys,window", [(3, 40, 8, 0), (5, 30, 16, 12), (2, 80, 4, 0), (4, 16, 32, 4)])
-def test_random_streams(hbm, n, events, keys, window):
+def test_random_streams(tier, n, events, keys, window):
+    """tier None: the escalation chain; a fixed tier: streams that outgrow it
+    report FX_ERR_CAPACITY (the oracle's err then differs: compared only where
+    both finished)."""
     streams = P.random_streams(7, 24, n, events, keys=keys, window=window)
-    check(streams, n, hbm=hbm)
+    if tier is None or tier == _lib.FX_PRED_TIER_HBM:
+        check(streams, n, tier=tier)
+        return
+    planes, clo, chi, nd = P.pack_pred_streams(streams, n)
+    res = fd.run_pred(planes, clo, chi, ndeps=nd, tier=tier)
+    o_order, o_rel, o_nexec, o_err = O.pred_batch_execute(planes, clo, chi, threads=8, ndeps=nd)
+    ok = res.err == 0
+    assert np.all((res.err == 0) | (res.err == _lib.FX_ERR_CAPACITY))
+    for s in np.flatnonzero(ok):
+        rows = _lib.index(np.arange(int(o_nexec[s])), s, planes.steps)
+        assert res.nexec[s] == o_nexec[s] and np.array_equal(res.order[rows], o_order[rows])
 
 
 def test_execute_at_commit_and_errors():
@@ -65,4 +78,4 @@ def test_very_wide_deps():
     streams outgrow them and rerun on the HBM tables."""
     streams = P.random_streams(3, 8, 2, 110, keys=3, reverse_pct=80)
     planes, res = check(streams, 2)
-    assert planes.dmax > 200 and res.reruns == 8 and np.all(res.nexec == planes.lengths)
+    assert planes.dmax > 200 and res.reruns >= 8 and np.all(res.nexec == planes.lengths)
