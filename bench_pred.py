@@ -154,7 +154,12 @@ def _cpu_baseline(args, S, steps, dmax, pw, dot, hdr, deps, clo, chi, order, rel
     g_nexec = nexec[:Ss].cpu().numpy().view(np.uint32)
     g_order, g_rel = pre(order), pre(release)
     same = bool(np.array_equal(o_nexec, g_nexec) and not o_err.any())
-    for s in range(Ss):
+    if same and Ss % 64 == 0 and np.all(o_nexec == steps):  # every row of every plane is defined
+        same = bool(np.array_equal(g_order, o_order) and np.array_equal(g_rel, o_rel))
+        Ss_loop = 0
+    else:
+        Ss_loop = Ss
+    for s in range(Ss_loop):
         rows = _lib.index(np.arange(int(o_nexec[s])), s, steps)
         allr = _lib.index(np.arange(steps), s, steps)
         same = same and np.array_equal(g_order[rows], o_order[rows]) and np.array_equal(g_rel[allr], o_rel[allr])
