@@ -61,6 +61,9 @@ constexpr uint32_t VMAX = 16;            // deps of a committed value (per-launc
 // last max-distance + interval, the change log the moves of the last interval
 constexpr uint32_t FMAX = 12;            // frame stack depth
 constexpr uint32_t RDMAX = 16;           // ready results per frame
+constexpr uint32_t HC_BINS = 64;         // ChainSize bins counted per instance in LDS
+constexpr uint32_t HD_BINS = 256;        // ExecutionDelay bins counted per instance in LDS
+constexpr uint32_t HL_LOG = 7, HL_SLOTS = 1u << HL_LOG;  // client-latency cache entries per instance
 constexpr uint32_t HMAX = 2;             // link heads per lane (links <= 128; a template parameter)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t LNIL = 0xFFFFu;  // end of a link's message list
@@ -95,7 +98,8 @@ constexpr uint32_t SL_CLIENT = 1,  // word 0 spare (the slot's dot lives in lane
 struct Geo {  // launch-uniform geometry
   uint32_t n, C, K, W, R, L, NP, ncli_keys, rt, rc;
   uint32_t amax, vmax, sl_value, sl_ack, slotw;  // dot-slot layout (MCollectAck deps <= 2K, value <= K(n+1))
-  uint32_t off_pool, off_free, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_frame, off_wl, words;
+  uint32_t off_pool, off_free, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_frame, off_wl, off_hist, off_lat,
+      words;
 };
 
 struct SimArgs {
@@ -272,6 +276,45 @@ struct Sim {
   __device__ __forceinline__ uint32_t& kd(uint32_t p, uint32_t key) { return lds[g.off_kd + p * g.ncli_keys + key]; }
   __device__ __forceinline__ uint32_t& FRR(uint32_t fi, uint32_t r) { return lds[g.off_frame + fi * RDMAX + r]; }
   __device__ __forceinline__ uint32_t& wl(uint32_t i) { return lds[g.off_wl + i]; }
+  // Histogram samples are counted per instance in LDS (ChainSize bins
+  // [0, HC_BINS), ExecutionDelay bins [0, HD_BINS)) and added to the global
+  // histograms once at the end: one global atomic per sample made every
+  // executed command a device-scope atomic on the same few bins.
+  __device__ __forceinline__ void hist_chain(uint32_t v) {
+    if (!A.chain_hist) return;
+    const uint32_t b = min(v, A.chain_bins - 1u);
+    if (lid == 0) {
+      if (b < HC_BINS) atomicAdd(&lds[g.off_hist + b], 1u);
+      else atomicAdd(&A.chain_hist[b], 1ull);
+    }
+  }
+  // client latency samples: a direct-mapped per-instance cache of (region,
+  // bin) -> count (a region's latencies take few distinct values); a sample
+  // whose entry is taken by another bin goes to the global bin directly
+  __device__ __forceinline__ void hist_lat(uint32_t region, uint32_t lat) {
+    if (!A.lat_hist) return;
+    const uint32_t key = region * A.lat_bins + min(lat, A.lat_bins - 1u);
+    const uint32_t h = (key * 2654435761u) >> (32 - HL_LOG);
+    const uint32_t k = uni(lds[g.off_lat + h]);
+    if (lid == 0) {
+      if (k == key + 1u) {
+        atomicAdd(&lds[g.off_lat + HL_SLOTS + h], 1u);
+      } else if (k == 0) {
+        lds[g.off_lat + h] = key + 1u;
+        lds[g.off_lat + HL_SLOTS + h] = 1u;
+      } else {
+        atomicAdd(&A.lat_hist[key], 1ull);
+      }
+    }
+  }
+  __device__ __forceinline__ void hist_delay(uint32_t v) {
+    if (!A.delay_hist) return;
+    const uint32_t b = min(v, A.delay_bins - 1u);
+    if (lid == 0) {
+      if (b < HD_BINS) atomicAdd(&lds[g.off_hist + HC_BINS + b], 1u);
+      else atomicAdd(&A.delay_hist[b], 1ull);
+    }
+  }
 
   __device__ __forceinline__ uint32_t pst(uint32_t sl, uint32_t p) {
     return (uni(S(sl, SL_PST + (p >> 2))) >> ((p & 3u) * 8u)) & 0xFFu;
@@ -843,7 +886,7 @@ struct Sim {
       A.executed[((size_t)inst * n + p) * A.exec_cap + xk] = d;
     ++xk;
     const uint32_t delay = now - start;  // ExecutionDelay (graph/mod.rs:514-518)
-    if (lid == 0 && A.delay_hist) atomicAdd(&A.delay_hist[min(delay, A.delay_bins - 1u)], 1ull);
+    hist_delay(delay);
     const uint32_t sl = slot_find(d);
     if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
     const uint32_t c = uni(S(sl, SL_CLIENT));
@@ -870,7 +913,7 @@ struct Sim {
   }
 
   __device__ __forceinline__ void emit_one(uint32_t d, uint32_t start) {
-    if (lid == 0 && A.chain_hist) atomicAdd(&A.chain_hist[min(1u, A.chain_bins - 1u)], 1ull);
+    hist_chain(1u);
     clk_add(d);
     on_execute(d, start);
   }
@@ -912,7 +955,7 @@ struct Sim {
     const uint64_t mm = bal(mem);
     const uint32_t cnt = pop64(mm);
     if (nwl + cnt > 65u) { fail_cap(__LINE__); return; }
-    if (lid == 0 && A.chain_hist) atomicAdd(&A.chain_hist[min(cnt, A.chain_bins - 1u)], 1ull);
+    hist_chain(cnt);
     uint32_t rank = 0;
     for (uint64_t m = mm; m; m &= m - 1) rank += rl(sdot, ctz64(m)) < sdot ? 1u : 0u;
     for (uint32_t r = 0; r < cnt; ++r) {
@@ -1205,10 +1248,8 @@ struct Sim {
       if (lid == 0) {
         if (A.latency_log && issued - 1u < A.lat_cap)
           A.latency_log[((size_t)inst * g.C + c) * A.lat_cap + issued - 1u] = lat;
-        if (A.lat_hist) {
-          atomicAdd(&A.lat_hist[(size_t)region * A.lat_bins + min(lat, A.lat_bins - 1u)], 1ull);
-        }
       }
+      hist_lat(region, lat);
       if (!client_send(c)) {
         ++clients_done;
         if (clients_done == g.C) {
@@ -1430,6 +1471,21 @@ __global__ __launch_bounds__(64, DS == 1 ? FX_SIM_WAVES : 2) void k_sim(SimArgs 
       st[FX_SIM_STAT_ERR_SITE] = s.err_site;
     }
   }
+  // the instance's cached histogram bins (exact: a sample either went here or
+  // straight to the global bin)
+  for (uint32_t i = s.lid; i < HC_BINS + HD_BINS; i += 64) {
+    const uint32_t c = smem[a.g.off_hist + i];
+    if (!c) continue;
+    if (i < HC_BINS) {
+      if (a.chain_hist) atomicAdd(&a.chain_hist[i], (unsigned long long)c);
+    } else if (a.delay_hist) {
+      atomicAdd(&a.delay_hist[i - HC_BINS], (unsigned long long)c);
+    }
+  }
+  for (uint32_t i = s.lid; i < HL_SLOTS; i += 64) {
+    const uint32_t k = smem[a.g.off_lat + i];
+    if (k && a.lat_hist) atomicAdd(&a.lat_hist[k - 1u], (unsigned long long)smem[a.g.off_lat + HL_SLOTS + i]);
+  }
   if (s.lid == 0) a.err[inst] = s.err;
 }
 
@@ -1482,6 +1538,8 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   g.off_kd = o; o += n * g.ncli_keys;
   g.off_frame = o; o += FMAX * RDMAX;
   g.off_wl = o; o += 72;
+  g.off_hist = o; o += HC_BINS + HD_BINS;
+  g.off_lat = o; o += 2 * HL_SLOTS;
   g.words = (o + 3) & ~3u;
   return true;
 }
