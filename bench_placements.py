@@ -207,9 +207,12 @@ def _cpu_baseline(args, launches, cmds):
     host = host_cpus()
     threads = host["usable"]
     picks = []
+    # ~cpu_baseline_seconds (default 10) of oracle work at ~0.15 M executed
+    # commands per second per thread, split over the launches
+    budget = (args.cpu_baseline_seconds or 10) * 0.15e6 * threads / max(1, len(launches))
     for L in launches:
-        N = len(L["ids"])
-        k = max(1, min(N, int(args.cpu_baseline_seconds or 10) * threads // 4))
+        N, n = len(L["ids"]), L["n"]
+        k = max(1, min(N, int(budget / (n * n * cmds))))
         for i in np.unique(np.linspace(0, N - 1, k).round().astype(np.int64)):
             picks.append((L, int(i)))
     t0 = time.perf_counter()
