@@ -96,7 +96,14 @@ uint32_t decode_pending(uint32_t tier, const uint32_t* block, uint32_t lane, uin
 // Callers hold scratch_mutex() while they use their slots.
 void* scratch(uint32_t slot, size_t bytes);
 std::recursive_mutex& scratch_mutex();
-enum : uint32_t { SCRATCH_TIERED_STATE = 0, SCRATCH_TIERED_MAP = 1, SCRATCH_CUT_FIRST = 2, SCRATCH_SLOTS = 40 };
+enum : uint32_t {
+  SCRATCH_TIERED_STATE = 0,
+  SCRATCH_TIERED_MAP = 1,
+  SCRATCH_TIERED_MAP2 = 2,
+  SCRATCH_TIERED_CNT = 3,
+  SCRATCH_CUT_FIRST = 4,
+  SCRATCH_SLOTS = 40
+};
 
 // The wide tiers (graph_wide.hip): whole streams, tables in LDS or HBM.
 int launch_wide(const KArgs& a, bool hbm, hipStream_t stream);

@@ -1244,6 +1244,43 @@ static uint32_t escalate(uint32_t tier) {
 // Synchronous tiered driver: the first tier for all (or for the streams in
 // `only`), then reruns of the streams that ran out of capacity up the
 // escalation chain.  The error plane comes back with one copy per tier.
+// Streams of a launch (list, or 0..L-1 when list is null) that stopped with
+// FX_ERR_CAPACITY, appended to out_list (order arbitrary: the next tier's
+// stream map; results do not depend on it); cnt[0] = how many.
+__global__ __launch_bounds__(256) void k_collect_capacity(const uint32_t* __restrict__ err,
+                                                          const uint32_t* __restrict__ list, uint32_t L,
+                                                          uint32_t* __restrict__ out_list, uint32_t* cnt) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t s = i < L ? (list ? list[i] : i) : 0u;
+  const bool cap = i < L && err[s] == FX_ERR_CAPACITY;
+  const uint64_t b = __ballot(cap);
+  if (!b) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t base = 0;
+  if (lane == (uint32_t)__builtin_ctzll(b)) base = atomicAdd(cnt, (uint32_t)__builtin_popcountll(b));
+  base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(b), 64);
+  if (cap) out_list[base + (uint32_t)__builtin_popcountll(b & ((1ull << lane) - 1ull))] = s;
+}
+
+// cnt[1] = lowest stream index (of list, or 0..L-1) with a nonzero status
+__global__ __launch_bounds__(256) void k_first_error(const uint32_t* __restrict__ err,
+                                                     const uint32_t* __restrict__ list, uint32_t L, uint32_t* cnt) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t s = i < L ? (list ? list[i] : i) : 0u;
+  const bool bad = i < L && err[s] != 0;
+  const uint64_t b = __ballot(bad);
+  if (!b) return;
+  uint32_t m = bad ? s : 0xFFFFFFFFu;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) m = min(m, (uint32_t)__shfl_xor((int)m, (int)o, 64));
+  if ((threadIdx.x & 63u) == 0) atomicMin(&cnt[1], m);
+}
+
+// The escalation driver.  Every decision stays on the device except one
+// 8-byte read per tier: the streams that ran out of capacity are compacted
+// into the next tier's stream map by k_collect_capacity, and the status to
+// return is the lowest failing stream's (k_first_error) -- no per-stream host
+// work, which at 4.4 M segments (configs[4]) had cost ~10 ms per call.
 int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
                const std::vector<uint32_t>* only, uint32_t* tier_counts) {
   std::lock_guard<std::recursive_mutex> lock(scratch_mutex());
@@ -1265,45 +1302,54 @@ int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t fl
     first = FX_TIER_LDS_LARGE;
   if (tier_counts)
     for (uint32_t t = 0; t < FX_NUM_TIERS; ++t) tier_counts[t] = 0;
-  std::vector<uint32_t> todo;
-  if (only) {
-    todo = *only;
-  } else {
-    todo.resize(S);
-    for (uint32_t s = 0; s < S; ++s) todo[s] = s;
-  }
-  if (todo.empty()) return FX_OK;
-  std::vector<uint32_t> err(S, 0);
-  for (uint32_t tier = first; tier < FX_NUM_TIERS && !todo.empty(); tier = escalate(tier)) {
+  const uint32_t L0 = only ? (uint32_t)only->size() : S;
+  if (L0 == 0) return FX_OK;
+  uint32_t* maps[2] = {(uint32_t*)scratch(SCRATCH_TIERED_MAP, (size_t)L0 * 4),
+                       (uint32_t*)scratch(SCRATCH_TIERED_MAP2, (size_t)L0 * 4)};
+  uint32_t* cnt = (uint32_t*)scratch(SCRATCH_TIERED_CNT, 8);
+  if (!maps[0] || !maps[1] || !cnt) return FX_ERR_HIP;
+  const uint32_t* list0 = nullptr;  // the launch's streams: null = all S
+  if (only && hipMemcpyAsync(maps[0], only->data(), (size_t)L0 * 4, hipMemcpyHostToDevice, hs) != hipSuccess)
+    return FX_ERR_HIP;
+  if (only) list0 = maps[0];
+  const uint32_t* list = list0;
+  uint32_t L = L0, side = only ? 1u : 0u;
+  uint32_t h[2] = {0, 0};
+  for (uint32_t tier = first; tier < FX_NUM_TIERS && L; tier = escalate(tier)) {
     if (tier == FX_TIER_WIDE && !wide_lds_fits(in->n, in->dmax)) continue;  // straight to the HBM tables
-    const uint32_t L = (uint32_t)todo.size();
     if (tier_counts) tier_counts[tier] = L;
-    const bool whole = !only && tier == first;
-    uint32_t* dmap = nullptr;
     void* dstate = nullptr;
-    if (!whole && !(dmap = (uint32_t*)scratch(SCRATCH_TIERED_MAP, (size_t)L * 4))) return FX_ERR_HIP;
     if ((tier == FX_TIER_GLOBAL || tier == FX_TIER_SPLIT || tier == FX_TIER_WIDE_HBM) &&
         !(dstate = scratch(SCRATCH_TIERED_STATE, fx_batch_state_bytes(tier, in->n, L))))
       return FX_ERR_HIP;
-    if (dmap) (void)hipMemcpyAsync(dmap, todo.data(), (size_t)L * 4, hipMemcpyHostToDevice, hs);
-    st = fx_batch_execute(in, out, tier, dmap, L, dstate, 0, in->steps, flags, nullptr, hip_stream);
-    if (!st && hipMemcpyAsync(err.data(), out->err, (size_t)S * 4, hipMemcpyDeviceToHost, hs) != hipSuccess)
-      st = FX_ERR_HIP;
-    if (!st && hipStreamSynchronize(hs) != hipSuccess) st = FX_ERR_HIP;
+    st = fx_batch_execute(in, out, tier, list, L, dstate, 0, in->steps, flags, nullptr, hip_stream);
     if (st) return st;
-    std::vector<uint32_t> redo;
-    for (uint32_t x : todo)
-      if (err[x] == FX_ERR_CAPACITY) redo.push_back(x);
-    todo.swap(redo);
+    uint32_t* next = maps[side];
+    if (next == list) next = maps[side ^ 1u];
+    if (hipMemsetAsync(cnt, 0, 4, hs) != hipSuccess) return FX_ERR_HIP;
+    hipLaunchKernelGGL(k_collect_capacity, dim3((L + 255) / 256), dim3(256), 0, hs, out->err, list, L, next, cnt);
+    if (hipMemcpyAsync(h, cnt, 4, hipMemcpyDeviceToHost, hs) != hipSuccess || hipStreamSynchronize(hs) != hipSuccess)
+      return FX_ERR_HIP;
+    L = h[0];
+    list = next;
+    side = (next == maps[0]) ? 1u : 0u;
   }
-  if (only) {
-    for (uint32_t x : *only)
-      if (err[x]) return (int)err[x];
-  } else {
-    for (uint32_t s = 0; s < S; ++s)
-      if (err[s]) return (int)err[s];
-  }
-  return FX_OK;
+  // status: the lowest failing stream's (streams still at FX_ERR_CAPACITY
+  // after the last tier included)
+  const uint32_t init[2] = {0, 0xFFFFFFFFu};
+  if (hipMemcpyAsync(cnt, init, 8, hipMemcpyHostToDevice, hs) != hipSuccess) return FX_ERR_HIP;
+  if (only && hipMemcpyAsync(maps[0], only->data(), (size_t)L0 * 4, hipMemcpyHostToDevice, hs) != hipSuccess)
+    return FX_ERR_HIP;
+  hipLaunchKernelGGL(k_first_error, dim3((L0 + 255) / 256), dim3(256), 0, hs, out->err, only ? maps[0] : nullptr,
+                     L0, cnt);
+  uint32_t e = 0;
+  if (hipMemcpyAsync(h, cnt, 8, hipMemcpyDeviceToHost, hs) != hipSuccess || hipStreamSynchronize(hs) != hipSuccess)
+    return FX_ERR_HIP;
+  if (h[1] != 0xFFFFFFFFu &&
+      (hipMemcpyAsync(&e, out->err + h[1], 4, hipMemcpyDeviceToHost, hs) != hipSuccess ||
+       hipStreamSynchronize(hs) != hipSuccess))
+    return FX_ERR_HIP;
+  return h[1] == 0xFFFFFFFFu ? FX_OK : (int)e;
 }
 
 }  // namespace fx

@@ -13,8 +13,9 @@
 //   1. k_split_score: one wavefront per tile reads the header plane of the
 //      first SPLIT_SAMPLE_STEPS steps and quantises the tile's mean deps per
 //      Add to a bucket (deps x 8, 0..63);
-//   2. k_split_plan: one workgroup lists the tiles by descending bucket
-//      (heaviest first, so the longest chains start first) into a heavy map
+//   2. k_plan_*: a grid-wide stable counting sort lists the tiles by
+//      descending bucket (heaviest first, so the longest chains start first)
+//      into a heavy map
 //      (bucket >= threshold, group tier) and a light map (lane tier), 64
 //      entries per tile (padding lanes of a ragged last tile get a sentinel
 //      stream index >= S and stay idle), and writes both lane counts;
@@ -36,7 +37,6 @@ namespace split {
 
 constexpr uint32_t NB = 64;                  // score buckets (mean deps x 8)
 constexpr uint32_t SAMPLE_BLOCKS = 64;       // 4-step blocks sampled per tile
-constexpr uint32_t PLAN_THREADS = 1024;
 constexpr uint32_t SENTINEL = 0xFFFFFFFFu;
 
 __global__ __launch_bounds__(64) void k_split_score(const uint32_t* __restrict__ hdr,
@@ -65,46 +65,92 @@ __global__ __launch_bounds__(64) void k_split_score(const uint32_t* __restrict__
   if (l == 0) score[t] = min((nd * 8u) / max(cnt, 1u), NB - 1);
 }
 
-// One workgroup: stable counting sort of the tiles by descending bucket.
-__global__ __launch_bounds__(PLAN_THREADS) void k_split_plan(const uint32_t* __restrict__ score,
-                                                             uint32_t tiles, uint32_t S, uint32_t thr,
-                                                             uint32_t* __restrict__ heavy,
-                                                             uint32_t* __restrict__ light,
-                                                             uint32_t* __restrict__ counts) {
-  __shared__ uint32_t wsum[PLAN_THREADS / 64];
-  const uint32_t tid = threadIdx.x, w = tid >> 6, l = tid & 63u;
-  uint32_t nh = 0, nl = 0;  // tiles placed so far (block-uniform)
+// Stable counting sort of the tiles by descending bucket (heavy map: buckets
+// >= thr, light map: the rest), in four grid-wide passes:
+//   k_plan_count  per block of PB tiles, a histogram of its buckets;
+//   k_plan_scan   one workgroup: each (bucket, block)'s first position in its
+//                 map (buckets descending, blocks ascending) and both counts;
+//   k_plan_place  each tile's position = its (bucket, block) offset + its rank
+//                 among the block's tiles of that bucket; inv[pos] = tile;
+//   k_plan_fill   one thread per map entry: stream = inv[entry / 64] * 64 + i.
+// The order is the one-workgroup sort's (bucket descending, tile ascending).
+constexpr uint32_t PB = 256;  // tiles per block of the plan passes
+
+__global__ __launch_bounds__(PB) void k_plan_count(const uint32_t* __restrict__ score, uint32_t tiles,
+                                                   uint32_t nblk, uint32_t* __restrict__ bh) {
+  __shared__ uint32_t h[NB];
+  const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+  if (tid < NB) h[tid] = 0;
+  __syncthreads();
+  const uint32_t t = blk * PB + tid;
+  if (t < tiles) atomicAdd(&h[score[t]], 1u);
+  __syncthreads();
+  if (tid < NB) bh[tid * nblk + blk] = h[tid];
+}
+
+__global__ __launch_bounds__(1024) void k_plan_scan(uint32_t* __restrict__ bh, uint32_t nblk, uint32_t thr,
+                                                    uint32_t* __restrict__ counts) {
+  // bh[b * nblk + k] -> exclusive offset in map(b) in the order (b desc, k asc)
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry[2];
+  const uint32_t tid = threadIdx.x, l = tid & 63u, w = tid >> 6;
+  if (tid < 2) carry[tid] = 0;
+  __syncthreads();
   for (int b = NB - 1; b >= 0; --b) {
-    const bool hv = (uint32_t)b >= thr;
-    uint32_t* map = hv ? heavy : light;
-    for (uint32_t c0 = 0; c0 < tiles; c0 += PLAN_THREADS) {
-      const uint32_t t = c0 + tid;
-      const bool f = t < tiles && score[t] == (uint32_t)b;
-      const uint64_t m = __ballot(f);
-      const uint32_t below = __popcll(m & ((1ull << l) - 1ull));
-      if (l == 0) wsum[w] = __popcll(m);
+    const uint32_t side = (uint32_t)b >= thr ? 0u : 1u;
+    for (uint32_t k0 = 0; k0 < nblk; k0 += 1024) {
+      const uint32_t k = k0 + tid;
+      const uint32_t v = k < nblk ? bh[(uint32_t)b * nblk + k] : 0u;
+      uint32_t x = v;  // inclusive scan within the wavefront
+#pragma unroll
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (l >= o) x += y;
+      }
+      if (l == 63) wsum[w] = x;
       __syncthreads();
-      uint32_t off = 0, tot = 0;
-      for (uint32_t q = 0; q < PLAN_THREADS / 64; ++q) {
-        off += q < w ? wsum[q] : 0u;
+      uint32_t before = 0, tot = 0;
+      for (uint32_t q = 0; q < 16; ++q) {
+        before += q < w ? wsum[q] : 0u;
         tot += wsum[q];
       }
-      if (f) {
-        const uint32_t pos = (hv ? nh : nl) + off + below;
-        uint32_t* e = map + (size_t)pos * 64;
-        for (uint32_t i = 0; i < 64; ++i) {
-          const uint32_t s = t * 64 + i;
-          e[i] = s < S ? s : SENTINEL;
-        }
-      }
-      if (hv) nh += tot; else nl += tot;
+      const uint32_t c = carry[side];
+      if (k < nblk) bh[(uint32_t)b * nblk + k] = c + before + x - v;
+      __syncthreads();
+      if (tid == 0) carry[side] = c + tot;
       __syncthreads();
     }
   }
   if (tid == 0) {
-    counts[0] = nh * 64;
-    counts[1] = nl * 64;
+    counts[0] = carry[0] * 64;
+    counts[1] = carry[1] * 64;
   }
+}
+
+__global__ __launch_bounds__(PB) void k_plan_place(const uint32_t* __restrict__ score, uint32_t tiles,
+                                                   uint32_t nblk, uint32_t thr, const uint32_t* __restrict__ bh,
+                                                   uint32_t* __restrict__ inv_heavy,
+                                                   uint32_t* __restrict__ inv_light) {
+  __shared__ uint32_t sc[PB];
+  const uint32_t tid = threadIdx.x, blk = blockIdx.x;
+  const uint32_t t = blk * PB + tid;
+  sc[tid] = t < tiles ? score[t] : 0xFFFFFFFFu;
+  __syncthreads();
+  if (t >= tiles) return;
+  const uint32_t b = sc[tid];
+  uint32_t r = 0;
+  for (uint32_t q = 0; q < tid; ++q) r += sc[q] == b ? 1u : 0u;
+  const uint32_t pos = bh[b * nblk + blk] + r;
+  (b >= thr ? inv_heavy : inv_light)[pos] = t;
+}
+
+__global__ __launch_bounds__(256) void k_plan_fill(const uint32_t* __restrict__ inv, const uint32_t* __restrict__ counts,
+                                                   uint32_t which, uint32_t entries, uint32_t S,
+                                                   uint32_t* __restrict__ map) {
+  const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= entries || e >= counts[which]) return;
+  const uint32_t s = inv[e >> 6] * 64 + (e & 63u);
+  map[e] = s < S ? s : SENTINEL;
 }
 
 static hipStream_t g_aux = nullptr;
@@ -123,8 +169,10 @@ static uint32_t threshold() {
 }  // namespace split
 
 size_t split_scratch_bytes(uint32_t streams) {
-  const size_t tiles = (streams + 63) / 64;
-  return (tiles + 2 * tiles * 64 + 4) * 4;
+  using namespace split;
+  const size_t tiles = (streams + 63) / 64, nblk = (tiles + PB - 1) / PB;
+  // score, heavy / light maps, counts, per-(bucket, block) offsets, inverse maps
+  return (tiles + 2 * tiles * 64 + 4 + NB * nblk + 2 * tiles) * 4;
 }
 
 int launch_split(const KArgs& a0, void* scratch, hipStream_t hs) {
@@ -137,6 +185,10 @@ int launch_split(const KArgs& a0, void* scratch, hipStream_t hs) {
   uint32_t* heavy = score + tiles;
   uint32_t* light = heavy + (size_t)tiles * 64;
   uint32_t* counts = light + (size_t)tiles * 64;
+  const uint32_t nblk = (tiles + PB - 1) / PB;
+  uint32_t* bh = counts + 4;
+  uint32_t* inv_heavy = bh + (size_t)NB * nblk;
+  uint32_t* inv_light = inv_heavy + tiles;
   // the lane tier holds n <= 8 sources and <= LANE_MAX_DEPS deps and reads
   // planes of < 4 GiB: otherwise every tile is heavy
   const bool lane_ok = a0.n <= 8 && a0.dmax <= LANE_MAX_DEPS && a0.plane * 4 <= LANE_MAX_PLANE_BYTES;
@@ -148,8 +200,14 @@ int launch_split(const KArgs& a0, void* scratch, hipStream_t hs) {
       return FX_ERR_HIP;
   }
   hipLaunchKernelGGL(k_split_score, dim3(tiles), dim3(64), 0, hs, a0.hdr, a0.lengths, S, a0.steps, score);
-  hipLaunchKernelGGL(k_split_plan, dim3(1), dim3(PLAN_THREADS), 0, hs, score, tiles, S, thr, heavy, light,
-                     counts);
+  hipLaunchKernelGGL(k_plan_count, dim3(nblk), dim3(PB), 0, hs, score, tiles, nblk, bh);
+  hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, hs, bh, nblk, thr, counts);
+  hipLaunchKernelGGL(k_plan_place, dim3(nblk), dim3(PB), 0, hs, score, tiles, nblk, thr, bh, inv_heavy, inv_light);
+  const uint32_t entries = tiles * 64;
+  hipLaunchKernelGGL(k_plan_fill, dim3((entries + 255) / 256), dim3(256), 0, hs, inv_heavy, counts, 0u, entries, S,
+                     heavy);
+  hipLaunchKernelGGL(k_plan_fill, dim3((entries + 255) / 256), dim3(256), 0, hs, inv_light, counts, 1u, entries, S,
+                     light);
   if (hipGetLastError() != hipSuccess) return FX_ERR_HIP;
   KArgs h = a0, lt = a0;
   h.stream_map = heavy;
