@@ -198,11 +198,13 @@ int flush(fx_graph_executor* ex) {
         hipMemcpyAsync(&err, ex->d_err.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipStreamSynchronize(ex->stream))
       return ex->sticky = FX_ERR_HIP;
-    if (err == FX_ERR_CAPACITY && ex->tier != FX_TIER_GLOBAL) {
-      // rerun the whole log one tier up; the already-consumed prefix of the
-      // (deterministic) order is skipped below
-      ex->tier = ex->tier == FX_TIER_WAVE || ex->tier == FX_TIER_LDS_LARGE ? FX_TIER_GLOBAL
-                                                                         : FX_TIER_LDS_LARGE;
+    if (err == FX_ERR_CAPACITY && ex->tier != FX_TIER_WIDE_HBM) {
+      // rerun the whole log one tier up (group -> LDS -> HBM slots -> HBM
+      // tables, the last one resumable like the others); the already-consumed
+      // prefix of the (deterministic) order is skipped below
+      ex->tier = ex->tier == FX_TIER_GROUP ? FX_TIER_LDS_LARGE
+               : ex->tier == FX_TIER_WAVE || ex->tier == FX_TIER_LDS_LARGE ? FX_TIER_GLOBAL
+                                                                          : FX_TIER_WIDE_HBM;
       ex->processed = 0;
       continue;
     }
@@ -430,10 +432,13 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
   if (hipMemcpyAsync(block.data(), ex->d_state.p, block.size() * 4, hipMemcpyDeviceToHost, ex->stream) ||
       hipStreamSynchronize(ex->stream))
     return FX_ERR_HIP;
-  std::vector<uint32_t> d(64), w(64);
-  const uint32_t c = fx::decode_pending(ex->tier, block.data(), 0, d.data(), w.data(), 64);
+  const uint32_t slots = ex->tier == FX_TIER_WIDE_HBM ? 16384 : 64;
+  std::vector<uint32_t> d(slots), w(slots);
+  const uint32_t c = ex->tier == FX_TIER_WIDE_HBM
+                         ? fx::wide_decode_pending(block.data(), ex->cfg.n, d.data(), w.data(), slots)
+                         : fx::decode_pending(ex->tier, block.data(), 0, d.data(), w.data(), slots);
   std::vector<std::pair<uint32_t, uint32_t>> pw;
-  for (uint32_t i = 0; i < c && i < 64; ++i) pw.emplace_back(d[i], w[i]);
+  for (uint32_t i = 0; i < c && i < slots; ++i) pw.emplace_back(d[i], w[i]);
   std::sort(pw.begin(), pw.end());
   uint32_t m = 0;
   for (const auto& e : pw) {

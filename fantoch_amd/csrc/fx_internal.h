@@ -105,10 +105,12 @@ enum : uint32_t {
   SCRATCH_SLOTS = 40
 };
 
-// The wide tiers (graph_wide.hip): whole streams, tables in LDS or HBM.
+// The wide tiers (graph_wide.hip): tables in LDS (whole streams) or HBM (also resumable).
 int launch_wide(const KArgs& a, bool hbm, hipStream_t stream);
 size_t wide_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes);
 bool wide_lds_fits(uint32_t n, uint32_t dmax);  // the LDS wide tier's tables fit a workgroup
+// pending (dot, waiting_on) pairs of a saved HBM wide-tier table block (one stream)
+uint32_t wide_decode_pending(const uint32_t* block, uint32_t n, uint32_t* dots, uint32_t* waits, uint32_t cap);
 
 // fx_batch_run_tiered over all streams (only == NULL) or the listed ones.
 int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,

@@ -35,7 +35,7 @@ enum : uint32_t { FOUND = 0, MISSING = 1, NOT_PENDING = 2 };
 
 struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-bit clock windows
   uint32_t P, Q, WB, n, D;
-  uint32_t vdot, vrec, vnd, vdeps, vwait, vid, vlow, vmark, vfree, tstk, fv, fi, wl, tl, tmp, hidx, front, bits, words;
+  uint32_t vdot, vrec, vnd, vdeps, vwait, vid, vlow, vmark, vfree, tstk, fv, fi, wl, tl, tmp, hidx, front, bits, sc, words;
   __host__ __device__ void make(uint32_t P_, uint32_t Q_, uint32_t WB_, uint32_t n_, uint32_t D_) {
     P = P_;
     Q = Q_;
@@ -61,6 +61,7 @@ struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-
     hidx = o; o += n * Q;
     front = o; o += 8;
     bits = o; o += n * WB;
+    sc = o; o += 4;  // saved scalars of a resumable (HBM) stream: nfree, nexec, epoch
     words = o;
   }
 };
@@ -344,15 +345,23 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
   w.lid = threadIdx.x;
   w.s = a.stream_map ? a.stream_map[lane_idx] : lane_idx;
   w.m = HBM ? a.state + (size_t)lane_idx * L.words : smem;
-  // init tables
-  for (uint32_t i = w.lid; i < L.words; i += 64) w.m[i] = 0;
-  __syncthreads();
-  for (uint32_t i = w.lid; i < L.P; i += 64) w.m[L.vfree + i] = L.P - 1u - i;
-  if (a.init_frontier && w.lid < L.n) w.m[L.front + w.lid] = a.init_frontier[(size_t)w.s * 8 + w.lid];
-  __syncthreads();
-  w.nfree = L.P;
   const uint32_t len = a.lengths ? min(a.lengths[w.s], a.steps) : a.steps;
-  for (uint32_t r = 0; r < len && !w.err; ++r) {
+  if (a.flags & FX_FLAG_INIT) {
+    // init tables (the dep rows are written before they are read)
+    for (uint32_t i = w.lid; i < L.words; i += 64)
+      if (i < L.vdeps || i >= L.vdeps + L.P * L.D) w.m[i] = 0;
+    __syncthreads();
+    for (uint32_t i = w.lid; i < L.P; i += 64) w.m[L.vfree + i] = L.P - 1u - i;
+    if (a.init_frontier && w.lid < L.n) w.m[L.front + w.lid] = a.init_frontier[(size_t)w.s * 8 + w.lid];
+    __syncthreads();
+    w.nfree = L.P;
+  } else {  // resume (HBM tables only): the tables are in place, the scalars saved
+    w.nfree = w.rd(L.sc, 0);
+    w.nexec = w.rd(L.sc, 1);
+    w.epoch = w.rd(L.sc, 2);
+  }
+  const uint32_t end = min(len, a.step_end);
+  for (uint32_t r = a.step_begin; r < end && !w.err; ++r) {
     w.step = r;
     if (a.flags & FX_FLAG_EXECUTE_AT_COMMIT) {  // executor.rs:72-73
       if (w.lid == 0) {
@@ -364,6 +373,11 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
     }
     w.handle_add(r);
   }
+  if (HBM && (a.flags & FX_FLAG_SAVE_STATE)) {
+    w.put(L.sc, 0, w.nfree);
+    w.put(L.sc, 1, w.nexec);
+    w.put(L.sc, 2, w.epoch);
+  }
   if (w.lid == 0) {
     a.nexec[w.s] = w.nexec;
     a.err[w.s] = w.err;
@@ -373,10 +387,11 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
 }  // namespace wide
 
 // LDS tables: 1024 vertices, 2048 index slots per source, 2048-bit windows;
-// HBM tables: 16384 vertices, 32768 index slots, 32768-bit windows
+// HBM tables: 16384 vertices, 32768 index slots, 32768-bit windows, dep rows of
+// the widest Add (31) so a saved table stays valid when later Adds are wider
 static wide::Lay wide_layout(bool hbm, uint32_t n, uint32_t dmax) {
   wide::Lay L;
-  if (hbm) L.make(16384, 32768, 1024, n, std::max(dmax, 1u));
+  if (hbm) L.make(16384, 32768, 1024, n, 31);
   else L.make(1024, 2048, 64, n, std::max(dmax, 1u));
   return L;
 }
@@ -387,9 +402,27 @@ size_t wide_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes) {
   return tier == FX_TIER_WIDE_HBM ? (size_t)wide_layout(true, n, 31).words * 4 * lanes : 0;
 }
 
+uint32_t wide_decode_pending(const uint32_t* block, uint32_t n, uint32_t* dots, uint32_t* waits, uint32_t cap) {
+  const wide::Lay L = wide_layout(true, n, 31);
+  uint32_t c = 0;
+  for (uint32_t v = 0; v < L.P; ++v) {
+    const uint32_t d = block[L.vdot + v];
+    if (!d) continue;
+    if (c < cap) {
+      dots[c] = d;
+      waits[c] = block[L.vwait + v];
+    }
+    ++c;
+  }
+  return c;
+}
+
 int launch_wide(const KArgs& a, bool hbm, hipStream_t hs) {
-  if (a.step_begin != 0 || a.step_end != a.steps || !(a.flags & FX_FLAG_INIT) || (a.flags & FX_FLAG_SAVE_STATE))
-    return FX_ERR_INVALID_ARG;  // whole streams only (a rerun tier)
+  // the LDS tables live for one launch: whole streams only (a rerun tier); the
+  // HBM tables persist in `state`, so that tier also resumes (the executor handle)
+  if (!hbm && (a.step_begin != 0 || a.step_end != a.steps || !(a.flags & FX_FLAG_INIT) ||
+               (a.flags & FX_FLAG_SAVE_STATE)))
+    return FX_ERR_INVALID_ARG;
   if (a.num_lanes == 0) return FX_OK;
   const wide::Lay L = wide_layout(hbm, a.n, a.dmax);
   if (!hbm && (size_t)L.words * 4 > 160 * 1024) return FX_ERR_UNSUPPORTED;

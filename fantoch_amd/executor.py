@@ -116,12 +116,15 @@ class GraphExecutor:
 
     def pending(self):
         """[(dot, waiting_on)] of the pending vertices, ascending."""
-        buf = (CDot * 64)()
-        wb = (CDot * 64)()
         got = ctypes.c_uint32()
-        check(_lib.load().fx_graph_executor_pending(self._h, buf, wb, 64, ctypes.byref(got)))
+        lib = _lib.load()
+        check(lib.fx_graph_executor_pending(self._h, None, None, 0, ctypes.byref(got)))
+        n = got.value
+        buf = (CDot * max(n, 1))()
+        wb = (CDot * max(n, 1))()
+        check(lib.fx_graph_executor_pending(self._h, buf, wb, n, ctypes.byref(got)))
         return [((buf[i].source, buf[i].seq), (wb[i].source, wb[i].seq))
-                for i in range(min(got.value, 64))]
+                for i in range(min(got.value, n))]
 
     def transfer_stats(self):
         """(host-to-device, device-to-host) bytes moved by this handle so far."""

@@ -158,7 +158,8 @@ typedef struct fx_hist_batch {
 #define FX_TIER_WIDE 7       /* one wavefront per stream, the graph as tables in LDS: 1024
                                 pending, 2048-bit windows (rerun tier after tier 2) */
 #define FX_TIER_WIDE_HBM 8   /* the same over HBM tables: 16384 pending, 32768-bit windows;
-                                `state` = fx_batch_state_bytes(8, n, lanes) bytes */
+                                `state` = fx_batch_state_bytes(8, n, lanes) bytes; the one
+                                wide tier that resumes (FX_FLAG_SAVE_STATE / no FX_FLAG_INIT) */
 #define FX_NUM_TIERS 9
 #define FX_TIER_DEFAULT FX_TIER_SPLIT
 
@@ -329,7 +330,11 @@ typedef struct fx_executor_result {
 
 typedef struct fx_graph_executor fx_graph_executor;
 
-/* Executor::new (executor.rs:34-51). NULL on bad config or no GPU. */
+/* Executor::new (executor.rs:34-51). NULL on bad config or no GPU.
+ * The handle starts on tier 0 and, when its stream outgrows a tier, reruns its
+ * log one tier up (0 -> 1 -> 2 -> 8): up to 16384 pending vertices, beyond
+ * which the handle reports FX_ERR_CAPACITY (the reference's indexes are
+ * unbounded, index.rs:18-51). */
 fx_graph_executor* fx_graph_executor_new(uint8_t process_id, uint64_t shard_id, const fx_config* config);
 /* Drop. */
 void fx_graph_executor_free(fx_graph_executor* ex);

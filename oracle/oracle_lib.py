@@ -176,12 +176,12 @@ class Graph:
             if m < 256:
                 return out
 
-    def pending(self):
-        src = (ctypes.c_uint32 * 256)()
-        seq = (ctypes.c_uint64 * 256)()
-        ws = (ctypes.c_uint32 * 256)()
-        wq = (ctypes.c_uint64 * 256)()
-        m = self.lib.oracle_graph_pending(self.h, src, seq, ws, wq, 256)
+    def pending(self, cap=256):
+        src = (ctypes.c_uint32 * cap)()
+        seq = (ctypes.c_uint64 * cap)()
+        ws = (ctypes.c_uint32 * cap)()
+        wq = (ctypes.c_uint64 * cap)()
+        m = self.lib.oracle_graph_pending(self.h, src, seq, ws, wq, cap)
         return [((src[i], seq[i]), (ws[i], wq[i])) for i in range(m)]
 
     def metrics(self, kind):

@@ -401,6 +401,35 @@ def test_executor_drain_after_every_add_is_linear(gpu):
     assert per_add_large < 2.0 * per_add_small + 64, (per_add_small, per_add_large)
 
 
+def test_executor_many_pending_escalates_to_hbm_tables(gpu):
+    """configs[3]-shaped log (64 clients per process, 100 % conflicts): the
+    pending set passes the 64 slots of tier 2, so the handle reruns its log on
+    the resumable HBM tables (tier 8) and keeps resuming there; results, metrics
+    and the pending set equal the oracle's at every pull."""
+    p = fs.synth_params(seed=5, instances=1, n=5, cmds=640, window=320, cycle_pct=30, conflicts=(100,),
+                        clients=64)
+    stream = fs.synth_host(p).stream(0)
+    ex = GraphExecutor(1, 0, 5, monitor=True)
+    g = oracle_lib.Graph(1, 5)
+    got, exp = [], []
+    max_pending = 0
+    for i, (dot, deps, t, _kind) in enumerate(stream):
+        ex.handle_add(dot, dot, [0], deps, t)
+        g.handle_add(dot, deps, t)
+        if i % 97 == 0 or i == len(stream) - 1:
+            got += [d for d, _ in ex.drain_dots()]
+            exp += [d for d, _, _ in g.drain()]
+            assert got == exp, i
+            pend = ex.pending()
+            max_pending = max(max_pending, len(pend))
+            if i % 388 == 0:
+                assert pend == sorted(g.pending(cap=20_000)), i
+    assert max_pending > 64
+    assert ex.metrics(CHAIN_SIZE) == g.metrics(1)
+    assert ex.metrics(EXECUTION_DELAY) == g.metrics(0)
+    assert max(ex.metrics(CHAIN_SIZE)) > 5
+
+
 def test_executor_u32_sequences_above_the_frontier(gpu):
     """Sequences near 2^32 - 1: the handle starts from an executed frontier F
     and holds seq - F on the device; the run equals the same stream at F = 0."""
