@@ -236,6 +236,9 @@ def _sim_lib():
         lib.oracle_sim_batch.restype = ctypes.c_int
         lib.oracle_sim_batch.argtypes = [ctypes.c_char_p, ctypes.POINTER(SimSpec), ctypes.c_uint32,
                                          ctypes.POINTER(SimOut), ctypes.c_int]
+        lib.oracle_sim_capture.restype = ctypes.c_int
+        lib.oracle_sim_capture.argtypes = [ctypes.c_char_p, ctypes.POINTER(SimSpec), ctypes.c_uint64] + \
+            [ctypes.c_void_p] * 7
         lib._sim_bound = True
     return lib
 
@@ -451,3 +454,36 @@ def workload_keys(spec, client, count):
     lib.oracle_workload_keys(ctypes.byref(spec), ctypes.c_uint64(client), ctypes.c_uint32(count),
                              ctypes.c_void_p(keys.ctypes.data), ctypes.c_void_p(ro.ctypes.data))
     return keys.reshape(count, spec.keys_per_command), ro
+
+
+def sim_capture_raw(spec, cap=None, planet_dir=PLANET_DIR):
+    """One instance through the simulator oracle, capturing each process's
+    executor input (the Adds its GraphExecutor receives, in handle order).
+    Returns dict of arrays: dot, t_ms, nd [n][cap], deps [n][cap][8], len [n],
+    executed [n][cap] (the simulation's execution order), exec_len [n]."""
+    lib = _sim_lib()
+    n = spec.n
+    if cap is None:
+        cap = spec.clients_per_region * spec.num_client_regions * spec.commands_per_client
+    out = {"dot": np.zeros((n, cap), np.uint32), "t_ms": np.zeros((n, cap), np.uint32),
+           "nd": np.zeros((n, cap), np.uint32), "deps": np.zeros((n, cap, 8), np.uint32),
+           "len": np.zeros(n, np.uint64), "executed": np.zeros((n, cap), np.uint32),
+           "exec_len": np.zeros(n, np.uint64)}
+    st = lib.oracle_sim_capture(planet_dir.encode(), ctypes.byref(spec), cap, out["dot"].ctypes.data,
+                                out["t_ms"].ctypes.data, out["nd"].ctypes.data, out["deps"].ctypes.data,
+                                out["len"].ctypes.data, out["executed"].ctypes.data, out["exec_len"].ctypes.data)
+    if st != 0:
+        raise RuntimeError("oracle_sim_capture status %d" % st)
+    return out
+
+
+def sim_capture(spec, planet_dir=PLANET_DIR):
+    """sim_capture_raw as lists: (streams, executed), streams[p] = [(dot, deps,
+    t_ms)] with dots as (source, seq), executed[p] = packed dots in order."""
+    r = sim_capture_raw(spec, planet_dir=planet_dir)
+    streams = []
+    for p in range(spec.n):
+        k = int(r["len"][p])
+        streams.append([(unpack(r["dot"][p, i]), [unpack(x) for x in r["deps"][p, i, :r["nd"][p, i]]],
+                         int(r["t_ms"][p, i])) for i in range(k)])
+    return streams, [r["executed"][p, :int(r["exec_len"][p])].copy() for p in range(spec.n)]

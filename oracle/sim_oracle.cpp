@@ -448,6 +448,10 @@ struct Process {
   uint32_t graph_rec = 0;
   std::vector<ExecResult> exec_to_clients;  // drained after each handle
   std::vector<uint32_t> executed;           // packed dots, execution order
+  // optional capture of the executor's input (oracle_sim_capture): per Add
+  // packed dot, time_ms, ndeps, deps ascending (C1)
+  bool capture = false;
+  std::vector<uint32_t> adds;
   std::map<uint32_t, std::vector<Rifl>> monitor;
   // AggregatePending (aggregate.rs:9-88)
   std::map<Rifl, uint32_t> pending;  // rifl -> results still missing
@@ -733,6 +737,16 @@ struct Process {
       return;
     }
     graph_cmds[e.dot] = e.cmd;
+    if (capture) {
+      std::vector<uint32_t> dv;
+      for (const Dot& d : e.deps) dv.push_back(FX_PACK_DOT(d.source, d.sequence));
+      std::sort(dv.begin(), dv.end());
+      dv.erase(std::unique(dv.begin(), dv.end()), dv.end());
+      adds.push_back(FX_PACK_DOT(e.dot.source, e.dot.sequence));
+      adds.push_back((uint32_t)time_ms);
+      adds.push_back((uint32_t)dv.size());
+      adds.insert(adds.end(), dv.begin(), dv.end());
+    }
     if (!graph->handle_add(e.dot, graph_rec++, e.deps, time_ms))
       throw std::logic_error("tried to index already indexed dot");
     for (const auto& x : graph->to_execute) {
@@ -819,6 +833,7 @@ struct SchedAction {
 
 struct Result {
   std::vector<std::vector<uint32_t>> executed;       // per process
+  std::vector<std::vector<uint32_t>> adds;           // per process, when captured
   std::vector<std::map<uint32_t, std::vector<Rifl>>> monitors;
   std::map<uint32_t, std::map<uint64_t, uint64_t>> latency;  // region -> (ms -> count)
   std::map<uint32_t, uint64_t> issued;                       // region -> issued
@@ -829,6 +844,9 @@ struct Result {
 
 class Runner {
  public:
+  void set_capture() {
+    for (auto& p : procs) p.capture = true;
+  }
   Runner(const Planet& pl, const fx_sim_spec& s) : planet(pl), spec(s) {
     const uint32_t n = s.n;
     if (n < 1 || n > FX_SIM_MAX_N) throw std::logic_error("bad n");
@@ -911,6 +929,7 @@ class Runner {
     for (uint32_t i = 1; i <= n; ++i) {
       Process& p = procs[i];
       r.executed.push_back(p.executed);
+      r.adds.push_back(std::move(p.adds));
       r.monitors.push_back(p.monitor);
       r.fast.push_back(p.fast_paths);
       r.slow.push_back(p.slow_paths);
@@ -1338,6 +1357,51 @@ int oracle_sim_run(const char* planet_dir, const fx_sim_spec* spec, oracle_sim_o
     out->status = 1;
   }
   return out->status;
+}
+
+// Runs one instance capturing each process's executor input (the commit
+// stream its GraphExecutor receives, in handle order) as fixed-width rows:
+// process p's Add i at [p * cap + i] of dot / t_ms / nd, its deps (ascending,
+// C1) at deps[(p * cap + i) * 8 + j]; len[p] Adds.  The execution order the
+// simulation produced at p: executed[p * cap + k], k < exec_len[p].
+// Status 2 if a stream is longer than cap or an Add has more than 8 deps.
+int oracle_sim_capture(const char* planet_dir, const fx_sim_spec* spec, uint64_t cap, uint32_t* dot,
+                       uint32_t* t_ms, uint32_t* nd, uint32_t* deps, uint64_t* len, uint32_t* executed,
+                       uint64_t* exec_len) {
+  simo::Planet pl;
+  if (!pl.load(planet_dir)) return -1;
+  try {
+    simo::Runner runner(pl, *spec);
+    runner.set_capture();
+    simo::Result r = runner.run();
+    int st = 0;
+    for (uint32_t p = 0; p < spec->n; ++p) {
+      const auto& a = r.adds[p];
+      const auto& e = r.executed[p];
+      uint64_t i = 0;
+      for (size_t w = 0; w < a.size(); ++i) {
+        const uint32_t k = a[w + 2];
+        if (i < cap && k <= 8) {
+          const uint64_t at = p * cap + i;
+          dot[at] = a[w];
+          t_ms[at] = a[w + 1];
+          nd[at] = k;
+          for (uint32_t j = 0; j < 8; ++j) deps[at * 8 + j] = j < k ? a[w + 3 + j] : 0u;
+        } else {
+          st = 2;
+        }
+        w += 3 + k;
+      }
+      len[p] = i;
+      exec_len[p] = e.size();
+      if (e.size() > cap) st = 2;
+      for (size_t k = 0; k < e.size() && k < cap; ++k) executed[p * cap + k] = e[k];
+    }
+    return st;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "oracle_sim_capture: %s\n", e.what());
+    return 1;
+  }
 }
 
 // Runs `count` instances on `nthreads` std::threads (the reference's rayon
