@@ -44,6 +44,7 @@ FX_SEQ_BITS = 24
 FX_SEQ_MASK = (1 << 24) - 1
 FX_KIND_ADD = 0
 FX_KIND_INDEX_ONLY = 1
+FX_KIND_EXECUTED = 2
 FX_ORDER_SCC_START = 0x80000000
 FX_RELEASE_NONE = 0xFFFFFFFF
 FX_FLAG_INIT = 1
@@ -205,6 +206,10 @@ SIGNATURES = [
     ("fx_pred_state_bytes", ctypes.c_size_t, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
     ("fx_pred_run", ctypes.c_int,
      [ctypes.POINTER(PredBatch), ctypes.POINTER(OrderBatch), ctypes.c_uint32, ctypes.c_void_p, u32p]),
+    ("fx_partial_state_bytes", ctypes.c_size_t, [ctypes.c_uint32, ctypes.c_uint32]),
+    ("fx_batch_execute_partial", ctypes.c_int,
+     [ctypes.POINTER(StreamBatch), ctypes.POINTER(OrderBatch), ctypes.c_void_p, ctypes.c_uint32,
+      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
     ("fx_batch_run_cut", ctypes.c_int,
      [ctypes.POINTER(StreamBatch), ctypes.POINTER(OrderBatch), ctypes.c_uint32, ctypes.c_void_p,
       ctypes.c_void_p]),
@@ -237,6 +242,15 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(CRifl), ctypes.c_uint32, u32p]),
     ("fx_graph_executor_pending", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.POINTER(CDot), ctypes.c_uint32, u32p]),
+    ("fx_graph_executor_handle_add_sharded", ctypes.c_int,
+     [ctypes.c_void_p, CDot, CRifl, u32p, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.POINTER(CDot), u32p, ctypes.c_uint32, ctypes.c_uint64]),
+    ("fx_graph_executor_handle_executed", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.c_uint32, ctypes.c_uint64]),
+    ("fx_graph_executor_requests", ctypes.c_int,
+     [ctypes.c_void_p, u64p, ctypes.POINTER(CDot), ctypes.c_uint32, u32p]),
+    ("fx_graph_executor_to_executors", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.c_uint32, u32p]),
     ("fx_graph_executor_parallel", ctypes.c_int, []),
     ("fx_graph_executor_transfer_stats", ctypes.c_int, [ctypes.c_void_p, u64p, u64p]),
     ("fx_sim_plan", ctypes.c_int,

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <set>
 #include <vector>
 
 #include "fantoch_amd.h"
@@ -74,6 +75,15 @@ struct fx_graph_executor {
   // at or below it are executed, which handle_add skips (mod.rs find_scc), so
   // they are dropped on the way in.
   uint32_t base[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t nsrc = 0;  // process ids 1..=nsrc: n x shard_count (util::all_process_ids)
+
+  // partial replication (shard_count > 1, graph/mod.rs:82-406)
+  bool partial = false;
+  std::map<uint32_t, uint32_t> dep_mask;              // device dot -> Dependency::shards bitmask
+  std::set<std::pair<uint64_t, uint32_t>> requests;   // out_requests: (target shard, device dot)
+  std::set<uint32_t> added;                           // added_to_executed_clock (device dots)
+  DevBuf d_req;                                       // first-missing ring (fx_batch_execute_partial)
+  uint32_t req_cap = 0;
 
   // device mirror
   uint32_t cap = 0;      // plane rows
@@ -175,10 +185,49 @@ int flush(fx_graph_executor* ex) {
   in.num_streams = 1;
   in.steps = ex->cap;
   in.dmax = ex->dmax;
-  in.n = ex->cfg.n;
+  in.n = ex->nsrc;
   fx_order_batch out{ex->d_order.u32(), ex->d_release.u32(), ex->d_nexec.u32(), ex->d_err.u32()};
   uint32_t nexec = 0, err = 0;
-  while (true) {
+  while (ex->partial) {  // one resumable tier: the HBM tables with partial-replication semantics
+    // the ring holds this flush's first-missing parents (<= its deps + records)
+    const uint32_t want = std::max<uint32_t>(1024, (N - ex->processed) * (ex->dmax + 1) * 2);
+    if (want > ex->req_cap) {
+      if (!ex->d_req.ensure((size_t)(1 + 2 * (size_t)want) * 4)) return ex->sticky = FX_ERR_HIP;
+      ex->req_cap = want;
+    }
+    if (!ex->d_state.ensure(fx_partial_state_bytes(ex->nsrc, 1))) return ex->sticky = FX_ERR_HIP;
+    uint32_t flags = FX_FLAG_SAVE_STATE;
+    if (ex->processed == 0) flags |= FX_FLAG_INIT;
+    else if (hipMemsetAsync(ex->d_req.p, 0, 4, ex->stream)) return ex->sticky = FX_ERR_HIP;
+    int st = fx_batch_execute_partial(&in, &out, ex->d_state.p, ex->processed, N, flags, nullptr, ex->d_req.u32(),
+                                      ex->req_cap, ex->stream);
+    if (st) return ex->sticky = st;
+    uint32_t nreq = 0;
+    if (hipMemcpyAsync(&nexec, ex->d_nexec.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
+        hipMemcpyAsync(&err, ex->d_err.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
+        hipMemcpyAsync(&nreq, ex->d_req.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
+        hipStreamSynchronize(ex->stream))
+      return ex->sticky = FX_ERR_HIP;
+    if (err) return ex->sticky = (int)err;
+    std::vector<uint32_t> ring((size_t)2 * nreq);
+    if (nreq && (hipMemcpyAsync(ring.data(), ex->d_req.u32() + 1, ring.size() * 4, hipMemcpyDeviceToHost,
+                                ex->stream) ||
+                 hipStreamSynchronize(ex->stream)))
+      return ex->sticky = FX_ERR_HIP;
+    ex->bytes_d2h += 4 + ring.size() * 4;
+    // PendingIndex::index: a first-missing parent this shard does not
+    // replicate is requested from its target shard (index.rs:187-197)
+    for (uint32_t k = 0; k < nreq; ++k) {
+      const uint32_t m = ring[2 * k + 1];
+      auto it = ex->dep_mask.find(m);
+      const uint32_t mask = it == ex->dep_mask.end() ? 0u : it->second;
+      if (mask == 0) return ex->sticky = FX_ERR_UNSUPPORTED;  // "shards should be set if it's not a noop"
+      if (!((mask >> ex->shard_id) & 1u))
+        ex->requests.insert({(uint64_t)(FX_DOT_SRC(m) - 1) / ex->cfg.n, m});  // Dot::target_shard (id.rs:59-61)
+    }
+    break;
+  }
+  while (!ex->partial) {
     // wider Adds than the current tier reads start over one tier up, as
     // fx_batch_run_tiered picks its first tier (group: <= GROUP_LANES deps,
     // wave: <= WAVE_MAX_DEPS)
@@ -187,7 +236,7 @@ int flush(fx_graph_executor* ex) {
       ex->tier = FX_TIER_LDS_LARGE;
       ex->processed = 0;
     }
-    if (!ex->d_state.ensure(fx_batch_state_bytes(ex->tier, ex->cfg.n, 1))) return ex->sticky = FX_ERR_HIP;
+    if (!ex->d_state.ensure(fx_batch_state_bytes(ex->tier, ex->nsrc, 1))) return ex->sticky = FX_ERR_HIP;
     uint32_t flags = FX_FLAG_SAVE_STATE;
     if (ex->processed == 0) flags |= FX_FLAG_INIT;
     if (ex->cfg.execute_at_commit) flags |= FX_FLAG_EXECUTE_AT_COMMIT;
@@ -253,6 +302,7 @@ int flush(fx_graph_executor* ex) {
       ex->execution_delay[delay] += 1;  // ExecutionDelay (mod.rs:514-518)
     }
     ex->executed.emplace_back(ex->dots[rec], start);  // device-local sequence
+    if (ex->partial) ex->added.insert(ex->dots[rec]);  // added_to_executed_clock (tarjan.rs:294-296)
     const Cmd& c = ex->cmds[rec];
     for (uint32_t key : c.keys) {
       ex->to_clients.push_back(fx_executor_result{c.rifl, key, c.read_only});
@@ -264,11 +314,12 @@ int flush(fx_graph_executor* ex) {
 }
 
 int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys, uint32_t nkeys,
-           uint32_t read_only, const fx_dot* deps, uint32_t ndeps, uint64_t now_ms, uint32_t kind) {
+           uint32_t read_only, const fx_dot* deps, uint32_t ndeps, uint64_t now_ms, uint32_t kind,
+           const uint32_t* dep_shards = nullptr) {
   if (!ex) return FX_ERR_INVALID_ARG;
   if (ex->sticky) return ex->sticky;
   if (ex->executor_index != 0) return FX_ERR_INVALID_ARG;  // mod.rs:220 assert_eq!(executor_index, 0)
-  if (dot.source < 1 || dot.source > ex->cfg.n || dot.seq <= ex->base[dot.source - 1] ||
+  if (dot.source < 1 || dot.source > ex->nsrc || dot.seq <= ex->base[dot.source - 1] ||
       dot.seq - ex->base[dot.source - 1] > FX_SEQ_MASK)
     return FX_ERR_DOT_RANGE;
   if (ndeps && !deps) return FX_ERR_INVALID_ARG;
@@ -282,10 +333,16 @@ int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys
   dv.reserve(ndeps);
   for (uint32_t j = 0; j < ndeps; ++j) {
     if (deps[j].source < 1 || deps[j].source > 255 || deps[j].seq < 1) return FX_ERR_DOT_RANGE;
-    const uint32_t b = deps[j].source <= ex->cfg.n ? ex->base[deps[j].source - 1] : 0;
+    const uint32_t b = deps[j].source <= ex->nsrc ? ex->base[deps[j].source - 1] : 0;
     if (deps[j].seq <= b) continue;  // executed before the handle started
     if (deps[j].seq - b > FX_SEQ_MASK) return FX_ERR_DOT_RANGE;
     dv.push_back(FX_PACK_DOT(deps[j].source, deps[j].seq - b));
+    if (ex->partial) {
+      const uint32_t mask = dep_shards ? dep_shards[j] : 1u << ex->shard_id;
+      auto it = ex->dep_mask.find(dv.back());
+      if (it != ex->dep_mask.end() && it->second != mask) return FX_ERR_INVALID_ARG;  // one command, one shard set
+      ex->dep_mask[dv.back()] = mask;
+    }
   }
   std::sort(dv.begin(), dv.end());  // canonical C1 (executor.rs:76 iterates a HashSet)
   dv.erase(std::unique(dv.begin(), dv.end()), dv.end());
@@ -309,12 +366,18 @@ int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys
 extern "C" {
 
 fx_graph_executor* fx_graph_executor_new(uint8_t process_id, uint64_t shard_id, const fx_config* config) {
-  if (!config || config->n < 1 || config->n > 8 || config->shard_count != 1) return nullptr;
+  if (!config || config->n < 1 || config->shard_count < 1 || (uint64_t)config->n * config->shard_count > 8 ||
+      shard_id >= config->shard_count)
+    return nullptr;
+  if (config->shard_count > 1 && config->execute_at_commit) return nullptr;
   if (fx_device_count() <= 0) return nullptr;  // no CPU fallback
   auto* ex = new fx_graph_executor();
   ex->process_id = process_id;
   ex->shard_id = shard_id;
   ex->cfg = *config;
+  ex->nsrc = config->n * config->shard_count;
+  ex->partial = config->shard_count > 1;
+  if (ex->partial) ex->tier = FX_TIER_WIDE_HBM;
   if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ex;
     return nullptr;
@@ -341,13 +404,70 @@ int fx_graph_executor_handle_add(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl
   return append(ex, dot, rifl, keys, nkeys, read_only, deps, ndeps, now_ms, FX_KIND_ADD);
 }
 
+int fx_graph_executor_handle_add_sharded(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys,
+                                         uint32_t nkeys, uint32_t read_only, const fx_dot* deps,
+                                         const uint32_t* dep_shards, uint32_t ndeps, uint64_t now_ms) {
+  if (!ex || (ndeps && !dep_shards)) return FX_ERR_INVALID_ARG;
+  if (!ex->partial) return FX_ERR_UNSUPPORTED;
+  return append(ex, dot, rifl, keys, nkeys, read_only, deps, ndeps, now_ms, FX_KIND_ADD, dep_shards);
+}
+
+int fx_graph_executor_handle_executed(fx_graph_executor* ex, const fx_dot* dots, uint32_t n, uint64_t now_ms) {
+  if (!ex || (n && !dots)) return FX_ERR_INVALID_ARG;
+  if (!ex->partial) return FX_ERR_UNSUPPORTED;
+  for (uint32_t i = 0; i < n; ++i) {
+    // RequestReply::Executed{dot} (mod.rs:394-402): the dot may be at or below
+    // a source's starting frontier (already executed here: a clock no-op)
+    const fx_dot d = dots[i];
+    if (d.source < 1 || d.source > ex->nsrc || d.seq < 1) return FX_ERR_DOT_RANGE;
+    if (d.seq <= ex->base[d.source - 1]) continue;
+    int st = append(ex, d, fx_rifl{0, 0}, nullptr, 0, 0, nullptr, 0, now_ms, FX_KIND_EXECUTED);
+    if (st) return st;
+    ex->added.insert(FX_PACK_DOT(d.source, d.seq - ex->base[d.source - 1]));
+  }
+  return FX_OK;
+}
+
+int fx_graph_executor_requests(fx_graph_executor* ex, uint64_t* shards, fx_dot* dots, uint32_t cap,
+                               uint32_t* n_out) {
+  if (!ex || !n_out || (cap && (!shards || !dots))) return FX_ERR_INVALID_ARG;
+  int st = flush(ex);
+  if (st) return st;
+  uint32_t c = 0;
+  while (c < cap && !ex->requests.empty()) {
+    const auto e = *ex->requests.begin();
+    ex->requests.erase(ex->requests.begin());
+    const uint32_t src = FX_DOT_SRC(e.second);
+    shards[c] = e.first;
+    dots[c] = fx_dot{src, FX_DOT_SEQ(e.second) + ex->base[src - 1]};
+    ++c;
+  }
+  *n_out = c;
+  return FX_OK;
+}
+
+int fx_graph_executor_to_executors(fx_graph_executor* ex, fx_dot* dots, uint32_t cap, uint32_t* n_out) {
+  if (!ex || !n_out || (cap && !dots)) return FX_ERR_INVALID_ARG;
+  int st = flush(ex);
+  if (st) return st;
+  uint32_t c = 0;
+  while (c < cap && !ex->added.empty()) {
+    const uint32_t d = *ex->added.begin();
+    ex->added.erase(ex->added.begin());
+    const uint32_t src = FX_DOT_SRC(d);
+    dots[c++] = fx_dot{src, FX_DOT_SEQ(d) + ex->base[src - 1]};
+  }
+  *n_out = c;
+  return FX_OK;
+}
+
 int fx_graph_executor_index_only(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys,
                                  uint32_t nkeys, const fx_dot* deps, uint32_t ndeps, uint64_t now_ms) {
   return append(ex, dot, rifl, keys, nkeys, 0, deps, ndeps, now_ms, FX_KIND_INDEX_ONLY);
 }
 
 int fx_graph_executor_set_executed_frontier(fx_graph_executor* ex, const uint64_t* frontier, uint32_t n) {
-  if (!ex || !frontier || n > 8 || n > ex->cfg.n) return FX_ERR_INVALID_ARG;
+  if (!ex || !frontier || n > 8 || n > ex->nsrc) return FX_ERR_INVALID_ARG;
   if (!ex->dots.empty()) return FX_ERR_INVALID_ARG;
   for (uint32_t p = 0; p < n; ++p)
     if (frontier[p] > 0xFFFFFFFFull) return FX_ERR_DOT_RANGE;
@@ -428,14 +548,15 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
   if (st) return st;
   *n_out = 0;
   if (ex->processed == 0) return FX_OK;
-  std::vector<uint32_t> block(fx_batch_state_bytes(ex->tier, ex->cfg.n, 1) / 4);
+  std::vector<uint32_t> block((ex->partial ? fx_partial_state_bytes(ex->nsrc, 1)
+                                           : fx_batch_state_bytes(ex->tier, ex->nsrc, 1)) / 4);
   if (hipMemcpyAsync(block.data(), ex->d_state.p, block.size() * 4, hipMemcpyDeviceToHost, ex->stream) ||
       hipStreamSynchronize(ex->stream))
     return FX_ERR_HIP;
-  const uint32_t slots = ex->tier == FX_TIER_WIDE_HBM ? 16384 : 64;
+  const uint32_t slots = ex->partial ? 16384 * 64 : ex->tier == FX_TIER_WIDE_HBM ? 16384 : 64;
   std::vector<uint32_t> d(slots), w(slots);
   const uint32_t c = ex->tier == FX_TIER_WIDE_HBM
-                         ? fx::wide_decode_pending(block.data(), ex->cfg.n, d.data(), w.data(), slots)
+                         ? fx::wide_decode_pending(block.data(), ex->nsrc, d.data(), w.data(), slots, ex->partial)
                          : fx::decode_pending(ex->tier, block.data(), 0, d.data(), w.data(), slots);
   std::vector<std::pair<uint32_t, uint32_t>> pw;
   for (uint32_t i = 0; i < c && i < slots; ++i) pw.emplace_back(d[i], w[i]);
@@ -445,7 +566,7 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
     if (m < cap) {
       const uint32_t s0 = FX_DOT_SRC(e.first), s1 = FX_DOT_SRC(e.second);
       dots[m] = fx_dot{s0, FX_DOT_SEQ(e.first) + ex->base[s0 - 1]};
-      waiting_on[m] = fx_dot{s1, FX_DOT_SEQ(e.second) + (s1 >= 1 && s1 <= ex->cfg.n ? ex->base[s1 - 1] : 0)};
+      waiting_on[m] = fx_dot{s1, FX_DOT_SEQ(e.second) + (s1 >= 1 && s1 <= ex->nsrc ? ex->base[s1 - 1] : 0)};
     }
     ++m;
   }

@@ -29,6 +29,12 @@ struct KArgs {
   uint32_t* dbg;  // per-lane diagnostic counters (FX_LANE_DEBUG), normally null
   const uint32_t* lanes_dev;  // device lane count (FX_TIER_SPLIT sub-launches), normally null
   uint32_t drift;             // lane tier: max blocks (4 steps) a lane runs ahead of the slowest, 0 = unbounded
+  // partial replication (FX_FLAG_PARTIAL, wide HBM tier): per lane a ring of
+  // (step, parent dot) pairs, one per dep missing for the first time
+  // (PendingIndex::index found no entry, index.rs:180-198): word 0 = count,
+  // then req_cap pairs
+  uint32_t* req;
+  uint32_t req_cap;
 };
 
 // Lane-per-stream executor tiers (graph_exec.hip) and the 16-lanes-per-stream
@@ -109,8 +115,11 @@ enum : uint32_t {
 int launch_wide(const KArgs& a, bool hbm, hipStream_t stream);
 size_t wide_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes);
 bool wide_lds_fits(uint32_t n, uint32_t dmax);  // the LDS wide tier's tables fit a workgroup
-// pending (dot, waiting_on) pairs of a saved HBM wide-tier table block (one stream)
-uint32_t wide_decode_pending(const uint32_t* block, uint32_t n, uint32_t* dots, uint32_t* waits, uint32_t cap);
+// pending (dot, waiting_on) pairs of a saved HBM wide-tier table block (one
+// stream); with partial replication one pair per (vertex, parent) registration
+uint32_t wide_decode_pending(const uint32_t* block, uint32_t n, uint32_t* dots, uint32_t* waits, uint32_t cap,
+                             bool partial = false);
+size_t wide_partial_state_bytes(uint32_t n, uint32_t lanes);  // FX_FLAG_PARTIAL tables
 
 // fx_batch_run_tiered over all streams (only == NULL) or the listed ones.
 int run_tiered(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,

@@ -1060,6 +1060,9 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
   a.init_frontier = init_frontier;
   a.dbg = nullptr;
   a.lanes_dev = nullptr;
+  a.req = nullptr;
+  a.req_cap = 0;
+  if (flags & FX_FLAG_PARTIAL) return FX_ERR_INVALID_ARG;  // fx_batch_execute_partial
   hipStream_t hs = (hipStream_t)hip_stream;
   if (g_profile) {
     if (!g_ev0) {
@@ -1085,6 +1088,44 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
     g_ev_valid = st == FX_OK;
   }
   return st;
+}
+
+size_t fx_partial_state_bytes(uint32_t n, uint32_t num_streams) { return wide_partial_state_bytes(n, num_streams); }
+
+int fx_batch_execute_partial(const fx_stream_batch* in, const fx_order_batch* out, void* state,
+                             uint32_t step_begin, uint32_t step_end, uint32_t flags,
+                             const uint32_t* init_frontier, uint32_t* req, uint32_t req_cap, void* hip_stream) {
+  int st = check_batch(in, out);
+  if (st) return st;
+  if (step_end > in->steps || step_begin > step_end || !state || !req || req_cap == 0) return FX_ERR_INVALID_ARG;
+  if (flags & ~(FX_FLAG_INIT | FX_FLAG_SAVE_STATE)) return FX_ERR_INVALID_ARG;
+  KArgs a;
+  a.dot = in->dot;
+  a.hdr = in->hdr;
+  a.deps = in->deps;
+  a.lengths = in->lengths;
+  a.S = in->num_streams;
+  a.steps = in->steps;
+  a.dmax = in->dmax;
+  a.n = in->n;
+  a.plane = fx_plane_words(in->num_streams, in->steps);
+  a.order = out->order;
+  a.release = out->release;
+  a.nexec = out->nexec;
+  a.err = out->err;
+  a.stream_map = nullptr;
+  a.num_lanes = in->num_streams;
+  a.state = (uint32_t*)state;
+  a.step_begin = step_begin;
+  a.step_end = step_end;
+  a.flags = flags | FX_FLAG_PARTIAL;
+  a.init_frontier = init_frontier;
+  a.dbg = nullptr;
+  a.lanes_dev = nullptr;
+  a.drift = 0;
+  a.req = req;
+  a.req_cap = req_cap;
+  return launch_wide(a, true, (hipStream_t)hip_stream);
 }
 
 int fx_profile_enable(int on) {

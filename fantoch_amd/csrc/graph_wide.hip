@@ -33,10 +33,16 @@ namespace wide {
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 enum : uint32_t { FOUND = 0, MISSING = 1, NOT_PENDING = 2 };
 
+constexpr uint32_t PW = 64;  // partial replication: parents a vertex may wait on at once
+
 struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-bit clock windows
   uint32_t P, Q, WB, n, D;
   uint32_t vdot, vrec, vnd, vdeps, vwait, vid, vlow, vmark, vfree, tstk, fv, fi, wl, tl, tmp, hidx, front, bits, sc, words;
-  __host__ __device__ void make(uint32_t P_, uint32_t Q_, uint32_t WB_, uint32_t n_, uint32_t D_) {
+  // partial replication only (0 words otherwise): per-vertex parent lists
+  // (count + PW dots), per-frame missing-dep counts, the collected missing deps
+  uint32_t vwn, vwl, fm, ml;
+  __host__ __device__ void make(uint32_t P_, uint32_t Q_, uint32_t WB_, uint32_t n_, uint32_t D_,
+                                bool partial = false) {
     P = P_;
     Q = Q_;
     WB = WB_;
@@ -62,6 +68,10 @@ struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-
     front = o; o += 8;
     bits = o; o += n * WB;
     sc = o; o += 4;  // saved scalars of a resumable (HBM) stream: nfree, nexec, epoch
+    vwn = o; o += partial ? P : 0;
+    vwl = o; o += partial ? P * PW : 0;
+    fm = o; o += partial ? P : 0;
+    ml = o; o += partial ? P : 0;
     words = o;
   }
 };
@@ -74,6 +84,8 @@ struct W {
   uint32_t err = 0;
   uint32_t nfree = 0, tsp = 0, fsp = 0, nwl = 0, idc = 0, epoch = 1, nexec = 0, step = 0;
   uint32_t t_now = 0;
+  bool partial = false;  // FX_FLAG_PARTIAL
+  uint32_t nml = 0;      // missing deps collected by a first search (partial)
 
   __device__ __forceinline__ uint32_t& at(uint32_t base, uint32_t i) { return m[base + i]; }
   __device__ __forceinline__ void put(uint32_t base, uint32_t i, uint32_t v) {
@@ -156,6 +168,7 @@ struct W {
       put(L.hidx, hslot(d), 0u);
       put(L.vdot, v, 0u);
       put(L.vwait, v, 0u);
+      if (partial) put(L.vwn, v, 0u);
       put(L.vfree, nfree++, v);
       if (nwl >= 2 * L.P) { err = FX_ERR_CAPACITY; return; }
       put(L.wl, nwl++, d);
@@ -166,19 +179,25 @@ struct W {
   // (tarjan.rs:60-93).  Released dots are appended to the worklist; on a
   // missing dep, *missing = it and the stack members are marked visited with
   // `mark_epoch` (0 = do not mark).
-  __device__ uint32_t find_scc(uint32_t root_dot, uint32_t* missing, uint32_t mark_epoch, bool* saved) {
+  // With partial replication, the first search of an Add (collect = true)
+  // records every missing dep in ml[0, nml) and keeps going; a vertex whose
+  // subtree misses deps is no SCC root (tarjan.rs:148-166, 198-200, 233).
+  __device__ uint32_t find_scc(uint32_t root_dot, uint32_t* missing, uint32_t mark_epoch, bool* saved,
+                               bool collect = false) {
     *saved = false;
     const uint32_t root = find(root_dot);
     if (root == NONE) return NOT_PENDING;
     idc = 1;
     tsp = 0;
     fsp = 0;
+    nml = 0;
     put(L.vid, root, 1);
     put(L.vlow, root, 1);
     put(L.vmark, root, rd(L.vmark, root) | 1u);
     put(L.tstk, tsp++, root);
     put(L.fv, fsp, root);
     put(L.fi, fsp, 0);
+    if (partial) put(L.fm, fsp, 0);
     ++fsp;
     uint32_t result = FOUND;
     while (fsp && !err) {
@@ -188,8 +207,18 @@ struct W {
         const uint32_t d = rd(L.vdeps, v * L.D + i);
         if (d == rd(L.vdot, v) || contains(d)) continue;  // self or executed (tarjan.rs:128-145)
         const uint32_t w = find(d);
-        if (w == NONE) {  // missing (tarjan.rs:148-157, shard_count == 1)
-          *missing = d;
+        if (w == NONE) {
+          if (collect) {  // partial replication, first search (tarjan.rs:158-166)
+            bool seen = false;
+            for (uint32_t k = 0; k < nml && !seen; ++k) seen = rd(L.ml, k) == d;
+            if (!seen) {
+              if (nml >= L.P) { err = FX_ERR_CAPACITY; break; }
+              put(L.ml, nml++, d);
+            }
+            put(L.fm, fsp - 1, rd(L.fm, fsp - 1) + 1u);
+            continue;
+          }
+          *missing = d;  // missing (tarjan.rs:148-157)
           result = MISSING;
           break;
         }
@@ -202,6 +231,7 @@ struct W {
           put(L.tstk, tsp++, w);
           put(L.fv, fsp, w);
           put(L.fi, fsp, 0);
+          if (partial) put(L.fm, fsp, 0);
           ++fsp;
         } else if (rd(L.vmark, w) & 1u) {  // on the stack
           put(L.vlow, v, min(rd(L.vlow, v), idw));
@@ -210,7 +240,8 @@ struct W {
       }
       // v finished
       const uint32_t idv = rd(L.vid, v), lowv = rd(L.vlow, v);
-      if (idv == lowv) {  // SCC root: pop the members (tarjan.rs:233-312)
+      const uint32_t mcount = partial ? rd(L.fm, fsp - 1) : 0u;
+      if (mcount == 0 && idv == lowv) {  // SCC root: pop the members (tarjan.rs:233-312)
         uint32_t base = tsp;
         while (base > 0) {
           --base;
@@ -228,6 +259,9 @@ struct W {
       if (fsp) {
         const uint32_t p = rd(L.fv, fsp - 1);
         put(L.vlow, p, min(rd(L.vlow, p), lowv));
+        if (mcount) put(L.fm, fsp - 1, rd(L.fm, fsp - 1) + mcount);  // tarjan.rs:198-200
+      } else if (mcount) {
+        result = MISSING;  // NotFound -> MissingDependencies(collected) (mod.rs:478-484)
       }
     }
     // finalize: ids of the vertices left on the stack; failed searches mark them visited
@@ -242,6 +276,47 @@ struct W {
     return result;
   }
 
+  // index_pending (mod.rs:525-554) -> PendingIndex::index (index.rs:168-202):
+  // vertex v waits on parent m.  With partial replication v keeps a list of
+  // parents, and a parent no vertex waits on yet (a vacant PendingIndex
+  // entry) is reported in the request ring; the host keeps the ones this
+  // shard does not replicate (is_mine, index.rs:187-197).
+  __device__ void index_pending(uint32_t v, uint32_t m) {
+    if (!partial) {
+      put(L.vwait, v, m);
+      return;
+    }
+    bool seen = false;
+    for (uint32_t v0 = 0; v0 < L.P && !seen; v0 += 64) {
+      const uint32_t x = v0 + lid;
+      bool hit = false;
+      if (at(L.vdot, x) != 0) {
+        const uint32_t c = at(L.vwn, x);
+        for (uint32_t j = 0; j < c && !hit; ++j) hit = at(L.vwl, x * PW + j) == m;
+      }
+      seen = __ballot(hit) != 0;
+    }
+    if (!seen) {
+      uint32_t* ring = a.req + (size_t)blockIdx.x * (1 + 2 * (size_t)a.req_cap);
+      const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)ring[0]);
+      if (k >= a.req_cap) { err = FX_ERR_CAPACITY; return; }
+      if (lid == 0) {
+        ring[1 + 2 * k] = step;
+        ring[2 + 2 * k] = m;
+        ring[0] = k + 1;
+      }
+    } else {
+      const uint32_t c = rd(L.vwn, v);
+      for (uint32_t j = 0; j < c; ++j)
+        if (rd(L.vwl, v * PW + j) == m) return;  // HashSet::insert of a present child
+    }
+    const uint32_t c = rd(L.vwn, v);
+    if (c >= PW) { err = FX_ERR_CAPACITY; return; }
+    put(L.vwl, v * PW + c, m);
+    put(L.vwn, v, c + 1);
+    __syncthreads();
+  }
+
   // check_pending (mod.rs:556-587) + try_pending (589-642)
   __device__ void check_pending() {
     while (nwl && !err) {
@@ -250,11 +325,25 @@ struct W {
       uint32_t cnt = 0;
       for (uint32_t v0 = 0; v0 < L.P; v0 += 64) {
         const uint32_t v = v0 + lid;
-        const bool w = at(L.vdot, v) != 0 && at(L.vwait, v) == d;
+        bool w = false;
+        if (partial) {
+          if (at(L.vdot, v) != 0) {
+            const uint32_t c = at(L.vwn, v);
+            for (uint32_t j = 0; j < c; ++j)
+              if (at(L.vwl, v * PW + j) == d) {  // swap-remove d from v's parents
+                at(L.vwl, v * PW + j) = at(L.vwl, v * PW + c - 1);
+                at(L.vwn, v) = c - 1;
+                w = true;
+                break;
+              }
+          }
+        } else {
+          w = at(L.vdot, v) != 0 && at(L.vwait, v) == d;
+        }
         const uint64_t b = __ballot(w);
         if (w) {
           at(L.tmp, cnt + __builtin_popcountll(b & ((1ull << lid) - 1ull))) = at(L.vdot, v);
-          at(L.vwait, v) = 0;
+          if (!partial) at(L.vwait, v) = 0;
         }
         cnt += __builtin_popcountll(b);
       }
@@ -285,7 +374,7 @@ struct W {
           cur = ++epoch;  // visited.clear()
         } else if (r == MISSING) {
           const uint32_t v2 = find(wd);
-          if (v2 != NONE) put(L.vwait, v2, missing);  // index_pending
+          if (v2 != NONE) index_pending(v2, missing);
           if (saved) cur = ++epoch;
         }
       }
@@ -297,6 +386,15 @@ struct W {
     const uint32_t src = FX_DOT_SRC(d);
     if (src < 1 || src > L.n || FX_DOT_SEQ(d) == 0) { err = FX_ERR_DOT_RANGE; return; }
     const uint32_t kind = FX_HDR_KIND(a.hdr[ix(r)]);
+    if (kind == FX_KIND_EXECUTED && partial) {  // RequestReply::Executed (mod.rs:394-402)
+      clock_add(d);
+      __syncthreads();
+      nwl = 0;
+      put(L.wl, nwl++, d);
+      __syncthreads();
+      check_pending();
+      return;
+    }
     if (kind != FX_KIND_ADD && kind != FX_KIND_INDEX_ONLY) { err = FX_ERR_UNSUPPORTED; return; }
     const uint32_t h = hslot(d);
     const uint32_t old = rd(L.hidx, h);
@@ -315,16 +413,23 @@ struct W {
     put(L.vwait, v, 0);
     put(L.vid, v, 0);
     put(L.vmark, v, 0);
+    if (partial) put(L.vwn, v, 0);
     put(L.hidx, h, v + 1);
     __syncthreads();
     if (kind == FX_KIND_INDEX_ONLY) return;  // VertexIndex::index without a search (test hook)
     uint32_t missing = 0;
     bool saved = false;
     nwl = 0;
-    const uint32_t res = find_scc(d, &missing, 0, &saved);
+    const uint32_t res = find_scc(d, &missing, 0, &saved, partial);
     if (res == MISSING) {
       const uint32_t v2 = find(d);
-      if (v2 != NONE) put(L.vwait, v2, missing);  // index_pending (mod.rs:525-554)
+      if (v2 != NONE) {  // index_pending (mod.rs:525-554)
+        if (partial) {
+          for (uint32_t k = 0; k < nml && !err; ++k) index_pending(v2, rd(L.ml, k));
+        } else {
+          index_pending(v2, missing);
+        }
+      }
     } else if (res == NOT_PENDING) {
       err = FX_ERR_CAPACITY;  // "just added dot must be pending" (mod.rs:257-259)
       return;
@@ -344,6 +449,7 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
   w.L = L;
   w.lid = threadIdx.x;
   w.s = a.stream_map ? a.stream_map[lane_idx] : lane_idx;
+  w.partial = HBM && (a.flags & FX_FLAG_PARTIAL);
   w.m = HBM ? a.state + (size_t)lane_idx * L.words : smem;
   const uint32_t len = a.lengths ? min(a.lengths[w.s], a.steps) : a.steps;
   if (a.flags & FX_FLAG_INIT) {
@@ -355,6 +461,7 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
     if (a.init_frontier && w.lid < L.n) w.m[L.front + w.lid] = a.init_frontier[(size_t)w.s * 8 + w.lid];
     __syncthreads();
     w.nfree = L.P;
+    if (w.partial && w.lid == 0) a.req[(size_t)blockIdx.x * (1 + 2 * (size_t)a.req_cap)] = 0;
   } else {  // resume (HBM tables only): the tables are in place, the scalars saved
     w.nfree = w.rd(L.sc, 0);
     w.nexec = w.rd(L.sc, 1);
@@ -389,9 +496,9 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
 // LDS tables: 1024 vertices, 2048 index slots per source, 2048-bit windows;
 // HBM tables: 16384 vertices, 32768 index slots, 32768-bit windows, dep rows of
 // the widest Add (31) so a saved table stays valid when later Adds are wider
-static wide::Lay wide_layout(bool hbm, uint32_t n, uint32_t dmax) {
+static wide::Lay wide_layout(bool hbm, uint32_t n, uint32_t dmax, bool partial = false) {
   wide::Lay L;
-  if (hbm) L.make(16384, 32768, 1024, n, 31);
+  if (hbm) L.make(16384, 32768, 1024, n, 31, partial);
   else L.make(1024, 2048, 64, n, std::max(dmax, 1u));
   return L;
 }
@@ -402,12 +509,24 @@ size_t wide_state_bytes(uint32_t tier, uint32_t n, uint32_t lanes) {
   return tier == FX_TIER_WIDE_HBM ? (size_t)wide_layout(true, n, 31).words * 4 * lanes : 0;
 }
 
-uint32_t wide_decode_pending(const uint32_t* block, uint32_t n, uint32_t* dots, uint32_t* waits, uint32_t cap) {
-  const wide::Lay L = wide_layout(true, n, 31);
+uint32_t wide_decode_pending(const uint32_t* block, uint32_t n, uint32_t* dots, uint32_t* waits, uint32_t cap,
+                             bool partial) {
+  const wide::Lay L = wide_layout(true, n, 31, partial);
   uint32_t c = 0;
   for (uint32_t v = 0; v < L.P; ++v) {
     const uint32_t d = block[L.vdot + v];
     if (!d) continue;
+    if (partial) {  // one (dot, parent) pair per registration; (dot, 0) if none
+      const uint32_t k = block[L.vwn + v];
+      for (uint32_t j = 0; j < (k ? k : 1u); ++j) {
+        if (c < cap) {
+          dots[c] = d;
+          waits[c] = k ? block[L.vwl + v * wide::PW + j] : 0u;
+        }
+        ++c;
+      }
+      continue;
+    }
     if (c < cap) {
       dots[c] = d;
       waits[c] = block[L.vwait + v];
@@ -417,6 +536,10 @@ uint32_t wide_decode_pending(const uint32_t* block, uint32_t n, uint32_t* dots, 
   return c;
 }
 
+size_t wide_partial_state_bytes(uint32_t n, uint32_t lanes) {
+  return (size_t)wide_layout(true, n, 31, true).words * 4 * lanes;
+}
+
 int launch_wide(const KArgs& a, bool hbm, hipStream_t hs) {
   // the LDS tables live for one launch: whole streams only (a rerun tier); the
   // HBM tables persist in `state`, so that tier also resumes (the executor handle)
@@ -424,7 +547,9 @@ int launch_wide(const KArgs& a, bool hbm, hipStream_t hs) {
                (a.flags & FX_FLAG_SAVE_STATE)))
     return FX_ERR_INVALID_ARG;
   if (a.num_lanes == 0) return FX_OK;
-  const wide::Lay L = wide_layout(hbm, a.n, a.dmax);
+  const bool partial = (a.flags & FX_FLAG_PARTIAL) != 0;
+  if (partial && (!hbm || !a.req || a.stream_map)) return FX_ERR_INVALID_ARG;
+  const wide::Lay L = wide_layout(hbm, a.n, a.dmax, partial);
   if (!hbm && (size_t)L.words * 4 > 160 * 1024) return FX_ERR_UNSUPPORTED;
   if (hbm) {
     if (!a.state) return FX_ERR_INVALID_ARG;

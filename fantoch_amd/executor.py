@@ -15,9 +15,9 @@ CHAIN_SIZE = 1
 
 
 class GraphExecutor:
-    def __init__(self, process_id, shard_id, n, f=1, execute_at_commit=False, monitor=True):
+    def __init__(self, process_id, shard_id, n, f=1, execute_at_commit=False, monitor=True, shard_count=1):
         lib = _lib.load()
-        cfg = _lib.Config(n, f, 1, 1 if execute_at_commit else 0, 1 if monitor else 0)
+        cfg = _lib.Config(n, f, shard_count, 1 if execute_at_commit else 0, 1 if monitor else 0)
         h = lib.fx_graph_executor_new(process_id, shard_id, ctypes.byref(cfg))
         if not h:
             raise _lib.FxError(_lib.FX_ERR_NO_DEVICE if lib.fx_device_count() <= 0
@@ -52,6 +52,49 @@ class GraphExecutor:
         check(_lib.load().fx_graph_executor_handle_add(
             self._h, CDot(*dot), CRifl(*rifl), karr, len(keys), 1 if read_only else 0, darr,
             len(deps), int(time_ms)), "handle_add")
+
+    # ---- partial replication (shard_count > 1, graph/mod.rs:82-406)
+    def handle_add_sharded(self, dot, rifl, keys, deps, shards, time_ms, read_only=False):
+        """handle(Add) / RequestReply::Info with each dep's shard bitmask."""
+        keys = list(keys)
+        karr = (ctypes.c_uint32 * max(len(keys), 1))(*keys)
+        deps = list(deps)
+        darr = (CDot * max(len(deps), 1))(*[CDot(int(s), int(q)) for s, q in deps])
+        sarr = (ctypes.c_uint32 * max(len(deps), 1))(*[int(m) for m in shards])
+        check(_lib.load().fx_graph_executor_handle_add_sharded(
+            self._h, CDot(*dot), CRifl(*rifl), karr, len(keys), 1 if read_only else 0, darr, sarr,
+            len(deps), int(time_ms)), "handle_add_sharded")
+
+    def handle_executed(self, dots, time_ms):
+        """RequestReply::Executed for each dot."""
+        dots = list(dots)
+        darr = (CDot * max(len(dots), 1))(*[CDot(int(s), int(q)) for s, q in dots])
+        check(_lib.load().fx_graph_executor_handle_executed(self._h, darr, len(dots), int(time_ms)),
+              "handle_executed")
+
+    def requests(self):
+        """Drains out-requests: sorted [(target shard, dot)]."""
+        out = []
+        sh = (ctypes.c_uint64 * 256)()
+        buf = (CDot * 256)()
+        got = ctypes.c_uint32()
+        while True:
+            check(_lib.load().fx_graph_executor_requests(self._h, sh, buf, 256, ctypes.byref(got)), "requests")
+            out += [(sh[i], (buf[i].source, buf[i].seq)) for i in range(got.value)]
+            if got.value < 256:
+                return out
+
+    def to_executors(self):
+        """Drains the dots added to the executed clock (Executed info for the other executors)."""
+        out = []
+        buf = (CDot * 256)()
+        got = ctypes.c_uint32()
+        while True:
+            check(_lib.load().fx_graph_executor_to_executors(self._h, buf, 256, ctypes.byref(got)),
+                  "to_executors")
+            out += [(buf[i].source, buf[i].seq) for i in range(got.value)]
+            if got.value < 256:
+                return out
 
     def index_only(self, dot, rifl, keys, deps, time_ms=0):
         keys = list(keys)

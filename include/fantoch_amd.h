@@ -69,6 +69,8 @@ extern "C" {
 #define FX_KIND_ADD 0u        /* GraphExecutionInfo::Add -> handle_add (mod.rs:213-275) */
 #define FX_KIND_INDEX_ONLY 1u /* VertexIndex::index without a search (index.rs:33-37);
                                  the hook the reference's sccs_found_and_missing_dep test uses */
+#define FX_KIND_EXECUTED 2u   /* RequestReply::Executed{dot} (mod.rs:394-402): executed-clock
+                                 add + check_pending; partial replication only */
 
 /* Order-plane word: arrival index of the executed command | SCC-start flag. */
 #define FX_ORDER_SCC_START 0x80000000u
@@ -79,6 +81,10 @@ extern "C" {
 #define FX_FLAG_INIT 1u              /* start from an empty executor (else resume from state) */
 #define FX_FLAG_EXECUTE_AT_COMMIT 2u /* Config::execute_at_commit (executor.rs:72-73)    */
 #define FX_FLAG_SAVE_STATE 4u        /* write the executor state back for a later resume */
+#define FX_FLAG_PARTIAL 8u           /* partial replication (shard_count > 1): the first search
+                                        of an Add collects every missing dep (tarjan.rs:148-166),
+                                        a vertex waits on all of them; FX_TIER_WIDE_HBM only,
+                                        through fx_batch_execute_partial */
 /* fx_batch_run_tiered only: first tier = ((flags >> FX_FLAG_TIER_SHIFT) & 15) - 1
  * (0 = the default tier, FX_TIER_DEFAULT). */
 #define FX_FLAG_TIER_SHIFT 8u
@@ -330,6 +336,22 @@ typedef struct fx_executor_result {
 
 typedef struct fx_graph_executor fx_graph_executor;
 
+/* Partial replication (Config::shard_count > 1, graph/mod.rs:82-406): the
+ * streams run on the HBM wide tables with FX_FLAG_PARTIAL semantics.  A record
+ * of kind FX_KIND_EXECUTED is RequestReply::Executed{dot}; RequestReply::Info
+ * is an Add.  `req` holds per stream 1 + 2 req_cap words: word 0 = count, then
+ * (step, parent dot) for every dep that went missing while no vertex waited on
+ * it (the first PendingIndex::index of that dot, index.rs:180-198), the
+ * candidates for out-requests (the caller keeps those its shard does not
+ * replicate).  n = processes over all shards (<= 8); process ids 1..=n.
+ * `state` = fx_partial_state_bytes(n, S) bytes; flags: FX_FLAG_INIT /
+ * FX_FLAG_SAVE_STATE (resumable).  Device pointers, async on hip_stream. */
+size_t fx_partial_state_bytes(uint32_t n, uint32_t num_streams);
+int fx_batch_execute_partial(const fx_stream_batch* in, const fx_order_batch* out, void* state,
+                             uint32_t step_begin, uint32_t step_end, uint32_t flags,
+                             const uint32_t* init_frontier, uint32_t* req, uint32_t req_cap,
+                             void* hip_stream);
+
 /* Executor::new (executor.rs:34-51). NULL on bad config or no GPU.
  * The handle starts on tier 0 and, when its stream outgrows a tier, reruns its
  * log one tier up (0 -> 1 -> 2 -> 8): up to 16384 pending vertices, beyond
@@ -346,6 +368,24 @@ int fx_graph_executor_set_executor_index(fx_graph_executor* ex, uint32_t index);
 int fx_graph_executor_handle_add(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl,
                                  const uint32_t* keys, uint32_t nkeys, uint32_t read_only,
                                  const fx_dot* deps, uint32_t ndeps, uint64_t now_ms);
+/* Partial replication (fx_config.shard_count > 1; n x shard_count <= 8 process
+ * ids; the handle runs on the HBM wide tables, FX_FLAG_PARTIAL):
+ * handle_add_sharded = handle(Add) and RequestReply::Info (mod.rs:390-393)
+ * with each dep's Dependency::shards as a bitmask (deps/keys/mod.rs:19-22);
+ * handle_executed = RequestReply::Executed for each dot (mod.rs:394-402);
+ * requests drains DependencyGraph::requests (mod.rs:148-151) as (target
+ * shard, dot) pairs, ascending; to_executors drains the dots added to the
+ * executed clock (mod.rs:137-144, the Executed info of fetch_to_executors,
+ * executor.rs:140-152), ascending.  Serving Requests (executor index > 0,
+ * handle_request over the shared VertexIndex, mod.rs:277-355) is not exported. */
+int fx_graph_executor_handle_add_sharded(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl,
+                                         const uint32_t* keys, uint32_t nkeys, uint32_t read_only,
+                                         const fx_dot* deps, const uint32_t* dep_shards, uint32_t ndeps,
+                                         uint64_t now_ms);
+int fx_graph_executor_handle_executed(fx_graph_executor* ex, const fx_dot* dots, uint32_t n, uint64_t now_ms);
+int fx_graph_executor_requests(fx_graph_executor* ex, uint64_t* shards, fx_dot* dots, uint32_t cap,
+                               uint32_t* n_out);
+int fx_graph_executor_to_executors(fx_graph_executor* ex, fx_dot* dots, uint32_t cap, uint32_t* n_out);
 /* Test hook mirroring `queue.vertex_index.index(Vertex::new(..))` (mod.rs:1164-1306). */
 int fx_graph_executor_index_only(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl,
                                  const uint32_t* keys, uint32_t nkeys,

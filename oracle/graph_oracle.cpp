@@ -199,7 +199,8 @@ int oracle_graph_find_scc(void* gp, uint32_t src, uint64_t seq, int first_find,
   auto* g = static_cast<DependencyGraph*>(gp);
   size_t total = 0;
   std::vector<Dot> dots;
-  std::set<Dot> visited, missing;
+  std::set<Dot> visited;
+  std::set<std::pair<Dot, uint32_t>> missing;
   oracle::FinderResult r;
   try {
     r = g->find_scc(first_find != 0, Dot{src, seq}, total, 0, dots, visited, missing);
@@ -207,7 +208,8 @@ int oracle_graph_find_scc(void* gp, uint32_t src, uint64_t seq, int first_find,
     return 99;
   }
   uint32_t m = 0;
-  for (const Dot& d : missing) {
+  for (const auto& dep : missing) {
+    const Dot& d = dep.first;
     if (m < cap) { missing_src[m] = d.source; missing_seq[m] = d.sequence; }
     ++m;
   }
@@ -215,6 +217,91 @@ int oracle_graph_find_scc(void* gp, uint32_t src, uint64_t seq, int first_find,
   *ready_commands = total;
   *n_dots = (uint32_t)dots.size();
   return r == oracle::FinderResult::Found ? 0 : r == oracle::FinderResult::MissingDependencies ? 1 : 2;
+}
+
+// ---- partial replication (shard_count > 1; mod.rs:82-406, tarjan.rs:148-166)
+void* oracle_graph_new_sharded(uint32_t process_id, uint32_t n, uint32_t shard_id, uint32_t shard_count) {
+  return new DependencyGraph(process_id, n, shard_id, shard_count);
+}
+
+// handle_add with each dep's Dependency::shards bitmask (RequestReply::Info
+// is the same call, mod.rs:390-393)
+int oracle_graph_handle_add_sharded(void* gp, uint32_t src, uint64_t seq, const uint32_t* dep_src,
+                                    const uint64_t* dep_seq, const uint32_t* dep_shards, uint32_t nd,
+                                    uint64_t t_ms, uint32_t rec) {
+  auto* g = static_cast<DependencyGraph*>(gp);
+  try {
+    return g->handle_add_sharded(Dot{src, seq}, rec, make_deps(dep_src, dep_seq, nd),
+                                 std::vector<uint32_t>(dep_shards, dep_shards + nd), t_ms)
+               ? 0
+               : 3;
+  } catch (const std::exception&) {
+    return 99;
+  }
+}
+
+// RequestReply::Executed (mod.rs:394-402)
+int oracle_graph_executed_reply(void* gp, uint32_t src, uint64_t seq, uint64_t t_ms) {
+  auto* g = static_cast<DependencyGraph*>(gp);
+  try {
+    g->handle_executed_reply(Dot{src, seq}, t_ms);
+  } catch (const std::exception&) {
+    return 99;
+  }
+  return 0;
+}
+
+// DependencyGraph::requests (mod.rs:148-151), drained: (target shard, dot) ascending
+uint32_t oracle_graph_requests(void* gp, uint32_t* shard, uint32_t* src, uint64_t* seq, uint32_t cap) {
+  auto* g = static_cast<DependencyGraph*>(gp);
+  uint32_t m = 0;
+  for (const auto& kv : g->out_requests)
+    for (const Dot& d : kv.second) {
+      if (m < cap) {
+        shard[m] = kv.first;
+        src[m] = d.source;
+        seq[m] = d.sequence;
+      }
+      ++m;
+    }
+  g->out_requests.clear();
+  return m;
+}
+
+// DependencyGraph::to_executors (mod.rs:137-144), drained: dots added to the
+// executed clock, ascending
+uint32_t oracle_graph_to_executors(void* gp, uint32_t* src, uint64_t* seq, uint32_t cap) {
+  auto* g = static_cast<DependencyGraph*>(gp);
+  uint32_t m = 0;
+  for (const Dot& d : g->added_to_executed_clock) {
+    if (m < cap) {
+      src[m] = d.source;
+      seq[m] = d.sequence;
+    }
+    ++m;
+  }
+  g->added_to_executed_clock.clear();
+  return m;
+}
+
+// Every PendingIndex registration (waiting vertex, missing parent), ascending.
+uint32_t oracle_graph_waits(void* gp, uint32_t* vsrc, uint64_t* vseq, uint32_t* psrc, uint64_t* pseq,
+                            uint32_t cap) {
+  auto* g = static_cast<DependencyGraph*>(gp);
+  std::set<std::pair<Dot, Dot>> all;
+  for (const auto& kv : g->pending_index)
+    for (const Dot& c : kv.second) all.insert({c, kv.first});
+  uint32_t m = 0;
+  for (const auto& e : all) {
+    if (m < cap) {
+      vsrc[m] = e.first.source;
+      vseq[m] = e.first.sequence;
+      psrc[m] = e.second.source;
+      pseq[m] = e.second.sequence;
+    }
+    ++m;
+  }
+  return m;
 }
 
 // DependencyGraph::commands_to_execute (mod.rs:158-160): drains executed dots.

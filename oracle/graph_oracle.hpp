@@ -70,6 +70,7 @@ struct Vertex {
   Dot dot;
   uint32_t rec = 0;              // arrival index in the stream (stands in for `cmd`)
   std::vector<Dot> deps;         // canonical C1: ascending
+  std::vector<uint32_t> dep_shards;  // Dependency::shards as a bitmask (0 = None, a noop)
   uint64_t start_time_ms = 0;
   size_t id = 0;
   size_t low = 0;
@@ -89,6 +90,12 @@ struct Executed {
 struct DependencyGraph {
   uint32_t process_id;
   uint32_t n;
+  // partial replication (mod.rs:82-122, shard_count > 1): this executor's
+  // shard, the number of shards, n processes per shard (ids 1..=n * shards)
+  uint32_t shard_id = 0, shard_count = 1, n_shard = 0;
+  std::set<std::pair<Dot, uint32_t>> missing_deps;  // TarjanSCCFinder::missing_deps (dep, shards)
+  std::map<uint32_t, std::set<Dot>> out_requests;    // mod.rs:61 out_requests (target shard -> dots)
+  std::set<Dot> added_to_executed_clock;             // mod.rs:63 (drained by to_executors)
   AEClock executed_clock;
   std::map<Dot, std::unique_ptr<Vertex>> vertex_index;  // VertexIndex (index.rs:18-51)
   std::map<Dot, std::set<Dot>> pending_index;           // PendingIndex (index.rs:145-208), C2
@@ -102,8 +109,14 @@ struct DependencyGraph {
   std::map<uint64_t, uint64_t> chain_size;
   std::map<uint64_t, uint64_t> execution_delay;
 
-  DependencyGraph(uint32_t pid, uint32_t n_) : process_id(pid), n(n_) {
+  DependencyGraph(uint32_t pid, uint32_t n_) : process_id(pid), n(n_), n_shard(n_) {
     // AEClock::with(all process ids) — mod.rs:90-94
+    for (uint32_t p = 1; p <= n; ++p) executed_clock.clock[p];
+  }
+  // Config::set_shard_count + DependencyGraph::new(process_id, shard_id, ..):
+  // the executed clock spans util::all_process_ids(shard_count, n) (util.rs:135-143)
+  DependencyGraph(uint32_t pid, uint32_t n_, uint32_t shard, uint32_t shards)
+      : process_id(pid), n(n_ * shards), shard_id(shard), shard_count(shards), n_shard(n_) {
     for (uint32_t p = 1; p <= n; ++p) executed_clock.clock[p];
   }
 
@@ -123,12 +136,27 @@ struct DependencyGraph {
 
   // mod.rs:213-275; returns false on the double-index panic (mod.rs:233-237).
   bool handle_add(const Dot& dot, uint32_t rec, std::vector<Dot> deps, uint64_t time_ms) {
+    std::vector<uint32_t> shards(deps.size(), 1u << shard_id);
+    return handle_add_sharded(dot, rec, std::move(deps), std::move(shards), time_ms);
+  }
+  // deps with their Dependency::shards masks (partial replication)
+  bool handle_add_sharded(const Dot& dot, uint32_t rec, std::vector<Dot> deps, std::vector<uint32_t> shards,
+                          uint64_t time_ms) {
     auto v = std::make_unique<Vertex>();
     v->dot = dot;
     v->rec = rec;
-    std::sort(deps.begin(), deps.end());  // C1
-    deps.erase(std::unique(deps.begin(), deps.end()), deps.end());
-    v->deps = std::move(deps);
+    std::vector<std::pair<Dot, uint32_t>> ds;
+    for (size_t i = 0; i < deps.size(); ++i) ds.push_back({deps[i], shards[i]});
+    std::sort(ds.begin(), ds.end());  // C1
+    ds.erase(std::unique(ds.begin(), ds.end(),
+                         [](const std::pair<Dot, uint32_t>& a, const std::pair<Dot, uint32_t>& b) {
+                           return a.first == b.first;
+                         }),
+             ds.end());
+    for (auto& d : ds) {
+      v->deps.push_back(d.first);
+      v->dep_shards.push_back(d.second);
+    }
     v->start_time_ms = time_ms;
     if (!index(std::move(v))) return false;
 
@@ -136,7 +164,7 @@ struct DependencyGraph {
     size_t total_scc_count = 0;
     std::vector<Dot> dots;
     std::set<Dot> visited;
-    std::set<Dot> missing;
+    std::set<std::pair<Dot, uint32_t>> missing;
     FinderResult r = find_scc(true, dot, total_scc_count, time_ms, dots, visited, missing);
     if (r == FinderResult::Found) {
       check_pending(dots, total_scc_count, time_ms);
@@ -153,10 +181,11 @@ struct DependencyGraph {
 
   // mod.rs:409-486.  Out-params: dots of the SCCs saved, visited, missing deps.
   FinderResult find_scc(bool first_find, const Dot& dot, size_t& total_scc_count, uint64_t time_ms,
-                        std::vector<Dot>& dots, std::set<Dot>& visited, std::set<Dot>& missing) {
+                        std::vector<Dot>& dots, std::set<Dot>& visited,
+                        std::set<std::pair<Dot, uint32_t>>& missing) {
     size_t scc_count = 0;
     size_t missing_deps_count = 0;
-    Dot result_missing;
+    std::pair<Dot, uint32_t> result_missing;
     FinderResult fr;
     Vertex* v = find(dot);
     if (v == nullptr) {
@@ -181,25 +210,34 @@ struct DependencyGraph {
       visited.insert(d);
     }
     missing.clear();
+    std::set<std::pair<Dot, uint32_t>> collected;
+    collected.swap(missing_deps);  // finalize returns the collected missing deps (tarjan.rs:91-92)
+    if (collected.size() > missing_deps_count) throw std::logic_error("more missing deps than the ones counted");
     switch (fr) {
       case FinderResult::Found:
         return FinderResult::Found;
       case FinderResult::MissingDependencies:
+        if (!collected.empty())  // mod.rs:468-471
+          throw std::logic_error("if MissingDependencies is returned, missing_deps must be empty");
         missing.insert(result_missing);
         return FinderResult::MissingDependencies;
       case FinderResult::NotPending:
         return FinderResult::NotPending;
       case FinderResult::NotFound:
       default:
-        // only reachable with partial replication (missing deps collected)
-        throw std::logic_error("either there's a missing dependency, or we should find an SCC");
+        // partial replication, first search: every missing dep collected (mod.rs:478-484)
+        if (collected.empty())
+          throw std::logic_error("either there's a missing dependency, or we should find an SCC");
+        missing = std::move(collected);
+        return FinderResult::MissingDependencies;
     }
   }
 
-  // tarjan.rs:96-316 (shard_count == 1: give up on the first missing dep).
+  // tarjan.rs:96-316: shard_count == 1 or a retry gives up on the first
+  // missing dep; the first search with partial replication collects every
+  // missing dep and keeps going (tarjan.rs:148-166).
   FinderResult strong_connect(bool first_find, const Dot& dot, Vertex* vertex, size_t& scc_count,
-                              size_t& missing_deps_count, Dot& missing_out) {
-    (void)first_find;
+                              size_t& missing_deps_count, std::pair<Dot, uint32_t>& missing_out) {
     finder_id += 1;
     vertex->id = finder_id;
     vertex->low = finder_id;
@@ -212,8 +250,15 @@ struct DependencyGraph {
       if (dep_dot == dot || executed_clock.contains(dep_dot.source, dep_dot.sequence)) continue;
       Vertex* dep_vertex = find(dep_dot);
       if (dep_vertex == nullptr) {
-        missing_out = dep_dot;  // tarjan.rs:148-157
-        return FinderResult::MissingDependencies;
+        // vertices indexed without shards (test hook) replicate on this shard
+        const uint32_t sh = i < vertex->dep_shards.size() ? vertex->dep_shards[i] : 1u << shard_id;
+        if (shard_count == 1 || !first_find) {
+          missing_out = {dep_dot, sh};  // tarjan.rs:148-157
+          return FinderResult::MissingDependencies;
+        }
+        missing_deps.insert({dep_dot, sh});  // tarjan.rs:158-166
+        missing_deps_count += 1;
+        continue;
       }
       if (dep_vertex->id == 0) {
         size_t dep_missing_deps_count = 0;
@@ -239,6 +284,7 @@ struct DependencyGraph {
         mv->on_stack = false;
         if (!scc.insert(member).second) throw std::logic_error("duplicate SCC member");
         executed_clock.add(member.source, member.sequence);  // tarjan.rs:293
+        if (shard_count > 1) added_to_executed_clock.insert(member);  // tarjan.rs:294-296
         if (member == dot) break;
       }
       sccs.push_back(std::move(scc));
@@ -264,10 +310,32 @@ struct DependencyGraph {
     }
   }
 
-  // mod.rs:525-554 + PendingIndex::index (index.rs:168-202); shard_count == 1
-  // means every dep is "mine", so no out-requests.
-  void index_pending(const Dot& dot, const std::set<Dot>& missing) {
-    for (const Dot& dep : missing) pending_index[dep].insert(dot);
+  // mod.rs:525-554 + PendingIndex::index (index.rs:168-202): the first time a
+  // dep is missing, a dep this shard does not replicate is requested from
+  // its target shard (Dot::target_shard, id.rs:59-61); with shard_count == 1
+  // every dep is "mine", so no out-requests.
+  void index_pending(const Dot& dot, const std::set<std::pair<Dot, uint32_t>>& missing) {
+    for (const auto& dep : missing) {
+      auto it = pending_index.find(dep.first);
+      if (it == pending_index.end()) {
+        pending_index[dep.first].insert(dot);
+        if (dep.second == 0) throw std::logic_error("shards should be set if it's not a noop");
+        const bool is_mine = (dep.second >> shard_id) & 1u;
+        if (!is_mine) out_requests[(dep.first.source - 1) / n_shard].insert(dep.first);
+      } else {
+        it->second.insert(dot);
+      }
+    }
+  }
+
+  // RequestReply::Executed (mod.rs:394-402): the requested dot was executed
+  // at its shard
+  void handle_executed_reply(const Dot& dot, uint64_t time_ms) {
+    executed_clock.add(dot.source, dot.sequence);
+    added_to_executed_clock.insert(dot);
+    std::vector<Dot> dots{dot};
+    size_t total_scc_count = 0;
+    check_pending(dots, total_scc_count, time_ms);
   }
 
   // mod.rs:556-587 — LIFO over the released dots.
@@ -292,7 +360,7 @@ struct DependencyGraph {
       if (visited.count(d)) continue;
       std::vector<Dot> new_dots;
       std::set<Dot> new_visited;
-      std::set<Dot> missing;
+      std::set<std::pair<Dot, uint32_t>> missing;
       FinderResult r = find_scc(false, d, total_scc_count, time_ms, new_dots, new_visited, missing);
       if (r == FinderResult::Found) {
         visited.clear();

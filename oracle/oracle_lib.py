@@ -57,6 +57,18 @@ def load():
         lib.oracle_graph_pending.argtypes = [vp, P32, P64, P32, P64, u32]
         lib.oracle_graph_metrics.restype = u32
         lib.oracle_graph_metrics.argtypes = [vp, u32, P64, P64, u32]
+        lib.oracle_graph_new_sharded.restype = vp
+        lib.oracle_graph_new_sharded.argtypes = [u32, u32, u32, u32]
+        lib.oracle_graph_handle_add_sharded.restype = ctypes.c_int
+        lib.oracle_graph_handle_add_sharded.argtypes = [vp, u32, u64, P32, P64, P32, u32, u64, u32]
+        lib.oracle_graph_executed_reply.restype = ctypes.c_int
+        lib.oracle_graph_executed_reply.argtypes = [vp, u32, u64, u64]
+        lib.oracle_graph_requests.restype = u32
+        lib.oracle_graph_requests.argtypes = [vp, P32, P32, P64, u32]
+        lib.oracle_graph_to_executors.restype = u32
+        lib.oracle_graph_to_executors.argtypes = [vp, P32, P64, u32]
+        lib.oracle_graph_waits.restype = u32
+        lib.oracle_graph_waits.argtypes = [vp, P32, P64, P32, P64, u32]
         _lib = lib
     return _lib
 
@@ -117,9 +129,12 @@ def pred_batch_execute(planes, clock_lo, clock_hi, execute_at_commit=False, thre
 class Graph:
     """One DependencyGraph (graph/mod.rs:45-677), for the reference's unit-test shapes."""
 
-    def __init__(self, process_id, n):
+    def __init__(self, process_id, n, shard_id=0, shard_count=1):
         self.lib = load()
-        self.h = self.lib.oracle_graph_new(process_id, n)
+        if shard_count > 1:
+            self.h = self.lib.oracle_graph_new_sharded(process_id, n, shard_id, shard_count)
+        else:
+            self.h = self.lib.oracle_graph_new(process_id, n)
         self.rec = 0
 
     def __del__(self):
@@ -140,6 +155,41 @@ class Graph:
         self.rec += 1
         if r:
             raise RuntimeError("oracle handle_add failed (%d)" % r)
+
+    def handle_add_sharded(self, dot, deps, shards, t_ms=0):
+        """handle_add (or RequestReply::Info) with each dep's shard bitmask."""
+        src, seq, nd = self._deps(deps)
+        sh = (ctypes.c_uint32 * max(nd, 1))(*shards)
+        r = self.lib.oracle_graph_handle_add_sharded(self.h, dot[0], dot[1], src, seq, sh, nd, t_ms, self.rec)
+        self.rec += 1
+        if r:
+            raise RuntimeError("oracle handle_add_sharded failed (%d)" % r)
+
+    def executed_reply(self, dot, t_ms=0):
+        """RequestReply::Executed{dot}."""
+        if self.lib.oracle_graph_executed_reply(self.h, dot[0], dot[1], t_ms):
+            raise RuntimeError("oracle executed_reply failed")
+
+    def requests(self):
+        """Drains out-requests: sorted [(target shard, dot)]."""
+        cap = 4096
+        sh, src, seq = (ctypes.c_uint32 * cap)(), (ctypes.c_uint32 * cap)(), (ctypes.c_uint64 * cap)()
+        m = self.lib.oracle_graph_requests(self.h, sh, src, seq, cap)
+        return [(sh[i], (src[i], seq[i])) for i in range(min(m, cap))]
+
+    def to_executors(self):
+        """Drains the dots added to the executed clock (partial replication)."""
+        cap = 1 << 16
+        src, seq = (ctypes.c_uint32 * cap)(), (ctypes.c_uint64 * cap)()
+        m = self.lib.oracle_graph_to_executors(self.h, src, seq, cap)
+        return [(src[i], seq[i]) for i in range(min(m, cap))]
+
+    def waits(self, cap=1 << 16):
+        """Every (waiting dot, missing parent) registration, ascending."""
+        vs, vq = (ctypes.c_uint32 * cap)(), (ctypes.c_uint64 * cap)()
+        ps, pq = (ctypes.c_uint32 * cap)(), (ctypes.c_uint64 * cap)()
+        m = self.lib.oracle_graph_waits(self.h, vs, vq, ps, pq, cap)
+        return [((vs[i], vq[i]), (ps[i], pq[i])) for i in range(min(m, cap))]
 
     def index_only(self, dot, deps, t_ms=0):
         src, seq, nd = self._deps(deps)

@@ -1,0 +1,53 @@
+"""Partial replication (shard_count > 1): the oracle's restatement of
+tarjan.rs:148-166 / mod.rs:277-406 / index.rs:168-202 on a hand-derived known
+answer and on seeded request/reply scenarios (CPU), and the GPU executor
+handle (FX_FLAG_PARTIAL on the HBM wide tables) against it step by step."""
+import pytest
+
+import partial_shapes as P
+
+
+def expect_of(kat):
+    return [(e["executed"], e["requests"], e["to_executors"]) for e in kat["expect"]]
+
+
+def test_oracle_partial_kat():
+    b = P.OracleBackend(P.KAT["n"], P.KAT["shards"], P.KAT["shard"])
+    assert P.run_kat(b) == expect_of(P.KAT)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_oracle_partial_scenario_terminates(seed):
+    hist, order = P.scenario(seed)
+    b = P.OracleBackend(2, 2, 0)
+    log = P.drive(hist, order, b, seed=seed)
+    executed = [d for step in log for d in step[0]]
+    requested = [d for step in log for _, d in step[1]]
+    mine = {hist[i][0] for i in order}
+    # every command of this shard executes exactly once; requests name only
+    # commands this shard does not replicate, each once (PendingIndex::index
+    # asks on the first miss only)
+    assert len(executed) == len(set(executed)) and mine <= set(executed)
+    assert len(requested) == len(set(requested)) and not (set(requested) & mine)
+    assert requested, "the scenario should exercise out-requests"
+    assert b.waits() == []
+
+
+@pytest.mark.gpu
+def test_gpu_partial_kat():
+    b = P.GpuBackend(P.KAT["n"], P.KAT["shards"], P.KAT["shard"])
+    assert P.run_kat(b) == expect_of(P.KAT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,n,shards", [(1, 2, 2), (2, 2, 2), (3, 2, 3), (4, 4, 2)])
+def test_gpu_partial_scenarios_match_oracle(seed, n, shards):
+    hist, order = P.scenario(seed, n=n, shards=shards, shard=seed % shards)
+    o = P.OracleBackend(n, shards, seed % shards)
+    g = P.GpuBackend(n, shards, seed % shards)
+    lo = P.drive(hist, order, o, seed=seed)
+    lg = P.drive(hist, order, g, seed=seed)
+    assert len(lo) == len(lg)
+    for k, (a, b) in enumerate(zip(lo, lg)):
+        assert a == b, k
+    assert o.waits() == g.waits() == []
