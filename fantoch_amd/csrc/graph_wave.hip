@@ -352,7 +352,8 @@ struct Wave {
     const bool valid = lid < nd;
     const uint32_t prev = gather(depj, (lid - 1u) & 63u);
     if (bal(valid && lid > 0 && depj <= prev)) { err = FX_ERR_DEPS_UNSORTED; return; }
-    const bool keep = valid && depj != d && !contains_v(depj);
+    const bool exd = contains_v(depj);  // every lane active: ds_bpermute reads 0 from inactive lanes
+    const bool keep = valid && depj != d && !exd;
     if (kind == FX_KIND_INDEX_ONLY) {
       insert_vertex(i, d, keep, depj);
       return;

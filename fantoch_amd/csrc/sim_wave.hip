@@ -1074,6 +1074,7 @@ struct Sim {
 
   // GraphExecutor::handle(Add) (executor.rs:69-80) -> handle_add (mod.rs:213-275)
   __device__ __forceinline__ void x_add(uint32_t p, uint32_t d) {
+    PROF_T0();
     x_load(p);
     nwl = 0;
     if (find(d) >= 0) { err = FX_ERR_DOUBLE_INDEX; x_store(); return; }
@@ -1081,9 +1082,21 @@ struct Sim {
     deps_total += vc;
     const uint32_t dsl = slot_find(d);
     const uint32_t depj = lid < vc ? S(dsl, g.sl_value + lid) : 0u;
-    const bool keep = lid < vc && depj != d && !contains_v(depj);
+    // the clock gather runs with every lane active: ds_bpermute reads 0 from a
+    // lane that is inactive, and the clock words sit in lanes 8 p + s, mostly
+    // outside [0, vc) (inside `&&` the call would run in the masked branch)
+    const bool exd = contains_v(depj);
+    const bool keep = lid < vc && depj != d && !exd;
+    PROF_ADD(5);
     if (!bal(keep)) {  // fast path: a singleton SCC
+#ifdef FX_SIM_PROFILE
+      const uint64_t pe0 = __builtin_amdgcn_s_memtime();
+#endif
       emit_one(d, now);
+#ifdef FX_SIM_PROFILE
+      prof[13] += __builtin_amdgcn_s_memtime() - pe0;
+      prof[21] += 1;
+#endif
       if (wmask && !err) {
         put(wl(0), d);
         nwl = 1;
@@ -1100,7 +1113,14 @@ struct Sim {
       else check_iter();
       if (++guard > (1u << 22)) fail_cap(__LINE__);
     }
+#ifdef FX_SIM_PROFILE
+    const uint64_t ps0 = __builtin_amdgcn_s_memtime();
+#endif
     x_store();
+#ifdef FX_SIM_PROFILE
+    prof[14] += __builtin_amdgcn_s_memtime() - ps0;
+    prof[22] += 1;
+#endif
   }
 
   // =========================================== send_to_processes_and_executors

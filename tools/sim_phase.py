@@ -28,8 +28,8 @@ specs = [S.spec(a.protocol, a.n, a.f, regs, regs, commands_per_client=a.cmds, co
 res = S.run(specs, pl, lat_cap=0)
 st = res.stats.astype(np.float64)
 ev = st[:, 24].sum()
-names = {0: "pop_min", 1: "run_event (all)", 2: "executor x_add", 3: "send_p", 4: "client R event", 6: "note", 7: "run_handlers"}
-kinds = ["MCollect", "MCollectAck", "MCommit", "MConsensus", "MConsensusAck", "MCommitDot", "-", "Submit"]
+names = {0: "pop_min", 1: "run_event (all)", 2: "executor x_add", 3: "send_p", 4: "client R event", 5: "x_add load+check", 6: "note", 7: "run_handlers"}
+kinds = ["MCollect", "MCollectAck", "MCommit", "MConsensus", "MConsensusAck", "x_add emit_one(fast)", "x_add x_store", "Submit"]
 tot = st[:, 0].sum() + st[:, 1].sum()
 print("events %d, cycles/event %.0f" % (ev, tot / ev))
 for i in sorted(names):
@@ -38,3 +38,11 @@ for k in range(8):
     c, n = st[:, 8 + k].sum(), st[:, 16 + k].sum()
     if n:
         print("  handler %-14s %8.0f cycles/call  %9d calls  %5.1f %%" % (kinds[k], c / n, n, 100 * c / tot))
+# per conflict rate: cycles per instance and the executor's share
+rates = np.array([0, 2, 10, 50, 100] * a.seeds)
+for r in [0, 2, 10, 50, 100]:
+    m = rates == r
+    tr = st[m, 0].sum() + st[m, 1].sum()
+    print("conflict %3d%%: %.3g cycles/instance, events/instance %.0f, executor %.1f %%, handlers %.1f %%, send_p %.1f %%"
+          % (r, tr / m.sum(), st[m, 24].sum() / m.sum(), 100 * st[m, 2].sum() / tr,
+             100 * st[m, 8:16].sum() / tr, 100 * st[m, 3].sum() / tr))
