@@ -175,12 +175,14 @@ def main_sim(args):
         alg_bytes = (36.0 + 8.0 * dbar) * executed_local
         achieved = alg_bytes / (kavg * 1e-3) / 1e9
         traffic = None
+        issue = None
         tj_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "sim_traffic_latest.json")
         if os.path.exists(tj_path):
             try:
                 tj = json.load(open(tj_path))
                 if tj.get("workload_key") == sim_key(args):
                     traffic = tj.get("hbm_bytes_per_launch")
+                    issue = tj.get("issue")
             except Exception:
                 traffic = None
         copy = measured_copy_gbps(torch, dev)
@@ -191,8 +193,13 @@ def main_sim(args):
                 "alg_bytes_definition": "SURVEY.md 8(d): 32 + 4k + 8d per executed command, k = 1, "
                                         "d = mean deps of the executor Adds",
                 "measured_copy_gbps": copy,
-                "note": "the simulator is a chain of dependent LDS operations per event (no "
-                        "HBM-bound phase): events/s per wavefront is the figure that moves"}
+                "note": "the simulator has no HBM-bound phase: it is bound by instruction issue (the "
+                        "scalar unit), see 'issue'"}
+        if issue:
+            # the bound that holds: SALU instructions per CU cycle against the
+            # scalar unit's one per cycle (PMC passes of the same workload)
+            roof["issue"] = dict(issue, bound="salu-issue", frac=issue.get("salu_per_cu_cycle"),
+                                 source="profiles/sim_traffic_latest.json (rocprofv3 --pmc SQ_INSTS_*, GRBM_GUI_ACTIVE)")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_sim(args, specs, rates, executed, executed_len, st, lat_hist, n, exec_cap,

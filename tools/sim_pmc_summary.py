@@ -83,12 +83,25 @@ def main():
             res["wave_cycle_split"] = {"active_inst": round(c["SQ_ACTIVE_INST_ANY"] / wc, 3),
                                        "wait_inst": round(c["SQ_WAIT_INST_ANY"] / wc, 3),
                                        "wait_any": round(c["SQ_WAIT_ANY"] / wc, 3)}
+    if c.get("GRBM_GUI_ACTIVE") and c.get("SQ_INSTS_SALU"):
+        # issue rates: GRBM_GUI_ACTIVE sums the busy cycles of the 8 XCDs, so
+        # cycles per CU = GRBM_GUI_ACTIVE / 8; the CU's scalar unit issues at
+        # most one SALU instruction per cycle (the arbiter serves one SIMD per
+        # cycle), each SIMD at most one VALU instruction per cycle
+        cyc = c["GRBM_GUI_ACTIVE"] / 8.0
+        res["issue"] = {
+            "cycles_per_cu": round(cyc),
+            "salu_per_cu_cycle": round(c["SQ_INSTS_SALU"] / (256 * cyc), 4),
+            "valu_per_simd_cycle": round(c["SQ_INSTS_VALU"] / (1024 * cyc), 4),
+            "all_per_cu_cycle": round(sum(c.get(k, 0.0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM",
+                                                                   "SQ_INSTS_BRANCH", "SQ_INSTS_LDS", "SQ_INSTS_VMEM"))
+                                      / (256 * cyc), 4)}
     json.dump(res, open(prefix + "sim_pmc.json", "w"), indent=1)
     if "read_bytes_raw" in res and "write_bytes" in res and key:
         tj = {"workload_key": key, "kernel": KERNEL,
               "hbm_bytes_per_launch": res["read_bytes_raw"] + res["write_bytes"],
               "read_bytes_raw": res["read_bytes_raw"], "read_bytes_x2": res["read_bytes_x2"],
-              "write_bytes": res["write_bytes"],
+              "write_bytes": res["write_bytes"], "issue": res.get("issue"),
               "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
                         "(tools/sim_measure.sh), per k_sim dispatch; raw FETCH_SIZE (k_sim's loads are "
                         "narrow, not the wide streaming reads the x2 gfx950 correction is documented for; "
