@@ -169,7 +169,7 @@ def main_dense(args):
         raise SystemExit("no GPU visible to libfantoch_amd")
     clients = 64
     cmds = args.cmds if args.cmds is not None else 20  # per client
-    instances = args.seeds if args.seeds != 4096 else 256
+    instances = args.seeds if args.seeds != 4096 else 768  # 3840 streams: 5 rounds of 768 workgroups (3 per CU)
     p = fs.synth_params(seed=args.seed, instances=instances, instance_base=rank * instances, n=5,
                         cmds=clients * cmds, window=5 * clients, cycle_pct=30, conflicts=(100,), clients=clients)
     S, steps, dmax = fs.synth_shape(p)

@@ -991,7 +991,7 @@ int fx_tier_query(uint32_t tier, uint32_t n, fx_tier_info* out) {
     case 4: *out = {8, WAVE_SLOTS, WAVE_WINDOW_BITS, wave_state_words_per_stream()}; break;
     case 5: *out = {8, LANE_SLOTS, LANE_WINDOW_BITS, lane_state_words_per_stream()}; break;
     case 6: *out = {8, std::min(LANE_SLOTS, GROUP_SLOTS), std::min(LANE_WINDOW_BITS, GROUP_WINDOW_BITS), 0}; break;
-    case FX_TIER_WIDE: *out = {8, 1024, 2048, 0}; break;
+    case FX_TIER_WIDE: *out = {8, 512, 1024, 0}; break;
     case FX_TIER_WIDE_HBM: *out = {8, 16384, 32768, (uint32_t)(wide_state_bytes(FX_TIER_WIDE_HBM, n, 1) / 4)}; break;
     default: return FX_ERR_INVALID_ARG;
   }

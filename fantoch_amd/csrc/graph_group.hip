@@ -150,7 +150,8 @@ struct Group {
     const uint32_t fre = ~occ & 0xFFFFu;
     if (!fre) { err = FX_ERR_CAPACITY; return -1; }
     const uint32_t sl = __builtin_ctz(fre);
-    const bool keep = lid < nd && depj != d && !contains(depj);
+    const bool exd = contains(depj);  // every lane active (see step_start)
+    const bool keep = lid < nd && depj != d && !exd;
     const uint32_t km = gb(keep);
     const uint32_t nc = __builtin_popcount(km);
     if (nc > C) { err = FX_ERR_CAPACITY; return -1; }
@@ -349,8 +350,12 @@ struct Group {
       insert_vertex(i, d, nd, depj);
       return;
     }
-    // fast path: every dep is self or executed -> a singleton SCC
-    if (!gb(valid && depj != d && !contains(depj))) {
+    // fast path: every dep is self or executed -> a singleton SCC.  The clock
+    // shuffle runs with every lane active: a __shfl (ds_bpermute) from an
+    // inactive lane reads 0, and the clock of source s sits in lane s, often
+    // outside [0, nd) (inside `&&` it would run in the masked branch)
+    const bool exd = contains(depj);
+    if (!gb(valid && depj != d && !exd)) {
       emit_one(i, d);
       if (wmask && !err) {  // check_pending([dot])
         if (lid == 0) wl(0) = d;

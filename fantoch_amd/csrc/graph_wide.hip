@@ -499,7 +499,7 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
 static wide::Lay wide_layout(bool hbm, uint32_t n, uint32_t dmax, bool partial = false) {
   wide::Lay L;
   if (hbm) L.make(16384, 32768, 1024, n, 31, partial);
-  else L.make(1024, 2048, 64, n, std::max(dmax, 1u));
+  else L.make(512, 512, 32, n, std::max(dmax, 1u));
   return L;
 }
 

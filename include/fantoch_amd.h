@@ -161,8 +161,8 @@ typedef struct fx_hist_batch {
                                 tier 0 for dense ones, both launched concurrently; whole
                                 batches only (FX_FLAG_INIT, no stream_map, no saved state);
                                 `state` = fx_batch_state_bytes(6, n, S) bytes of scratch */
-#define FX_TIER_WIDE 7       /* one wavefront per stream, the graph as tables in LDS: 1024
-                                pending, 2048-bit windows (rerun tier after tier 2) */
+#define FX_TIER_WIDE 7       /* one wavefront per stream, the graph as tables in LDS: 512
+                                pending, 1024-bit windows (rerun tier after tier 2) */
 #define FX_TIER_WIDE_HBM 8   /* the same over HBM tables: 16384 pending, 32768-bit windows;
                                 `state` = fx_batch_state_bytes(8, n, lanes) bytes; the one
                                 wide tier that resumes (FX_FLAG_SAVE_STATE / no FX_FLAG_INIT) */
