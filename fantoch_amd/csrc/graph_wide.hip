@@ -100,10 +100,14 @@ struct W {
   __device__ __forceinline__ uint32_t dep(uint32_t r, uint32_t j) const { return a.deps[j * a.plane + ix(r)]; }
 
   // ------------------------------------------------------------ clock
+  // frv: the frontiers in lanes (lane s = source s + 1), loaded by find_scc
+  // and kept in step by clock_add, so the per-edge check reads no LDS word
+  // unless the seq is above the frontier
+  uint32_t frv = 0;
   __device__ __forceinline__ bool contains(uint32_t d) {
     const uint32_t src = FX_DOT_SRC(d), sq = FX_DOT_SEQ(d);
     if (src < 1 || src > L.n) return false;
-    const uint32_t f = rd(L.front, src - 1);
+    const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)frv, (int)(src - 1));
     if (sq <= f) return true;
     const uint32_t off = sq - f - 1;
     if (off >= L.WB * 32u) return false;
@@ -128,6 +132,7 @@ struct W {
       ++f;
     }
     put(L.front, src - 1, f);
+    if (lid == src - 1) frv = f;
   }
 
   // ------------------------------------------------------- vertex index
@@ -191,21 +196,26 @@ struct W {
     tsp = 0;
     fsp = 0;
     nml = 0;
+    frv = lid < L.n ? at(L.front, lid) : 0u;
     put(L.vid, root, 1);
     put(L.vlow, root, 1);
     put(L.vmark, root, rd(L.vmark, root) | 1u);
     put(L.tstk, tsp++, root);
     put(L.fv, fsp, root);
-    put(L.fi, fsp, 0);
     if (partial) put(L.fm, fsp, 0);
     ++fsp;
+    // the top frame lives in registers: its vertex, next dep, id, low, dot,
+    // dep count and dep row (lane j = dep j); a frame's position and low go
+    // to the tables only when it recurses, and come back when it resumes
+    uint32_t cv = root, ci = 0, cid = 1, clow = 1, cdot = root_dot;
+    uint32_t cnd = rd(L.vnd, root);
+    uint32_t drow = lid < cnd ? at(L.vdeps, root * L.D + lid) : 0u;
     uint32_t result = FOUND;
     while (fsp && !err) {
-      const uint32_t v = rd(L.fv, fsp - 1), i = rd(L.fi, fsp - 1);
-      if (i < rd(L.vnd, v)) {
-        put(L.fi, fsp - 1, i + 1);
-        const uint32_t d = rd(L.vdeps, v * L.D + i);
-        if (d == rd(L.vdot, v) || contains(d)) continue;  // self or executed (tarjan.rs:128-145)
+      if (ci < cnd) {
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)drow, (int)ci);
+        ++ci;
+        if (d == cdot || contains(d)) continue;  // self or executed (tarjan.rs:128-145)
         const uint32_t w = find(d);
         if (w == NONE) {
           if (collect) {  // partial replication, first search (tarjan.rs:158-166)
@@ -224,31 +234,38 @@ struct W {
         }
         const uint32_t idw = rd(L.vid, w);
         if (idw == 0) {  // recurse
+          put(L.fi, fsp - 1, ci);
+          put(L.vlow, cv, clow);
           ++idc;
           put(L.vid, w, idc);
-          put(L.vlow, w, idc);
           put(L.vmark, w, rd(L.vmark, w) | 1u);
           put(L.tstk, tsp++, w);
           put(L.fv, fsp, w);
-          put(L.fi, fsp, 0);
           if (partial) put(L.fm, fsp, 0);
           ++fsp;
+          cv = w;
+          ci = 0;
+          cid = idc;
+          clow = idc;
+          cdot = d;
+          cnd = rd(L.vnd, w);
+          drow = lid < cnd ? at(L.vdeps, w * L.D + lid) : 0u;
         } else if (rd(L.vmark, w) & 1u) {  // on the stack
-          put(L.vlow, v, min(rd(L.vlow, v), idw));
+          clow = min(clow, idw);
         }
         continue;
       }
-      // v finished
-      const uint32_t idv = rd(L.vid, v), lowv = rd(L.vlow, v);
+      // cv finished
+      const uint32_t lowv = clow;
       const uint32_t mcount = partial ? rd(L.fm, fsp - 1) : 0u;
-      if (mcount == 0 && idv == lowv) {  // SCC root: pop the members (tarjan.rs:233-312)
+      if (mcount == 0 && cid == lowv) {  // SCC root: pop the members (tarjan.rs:233-312)
         uint32_t base = tsp;
         while (base > 0) {
           --base;
           const uint32_t x = rd(L.tstk, base);
           put(L.vmark, x, rd(L.vmark, x) & ~1u);
           clock_add(rd(L.vdot, x));  // executed_clock.add at pop time (tarjan.rs:293)
-          if (x == v) break;
+          if (x == cv) break;
         }
         const uint32_t cnt = tsp - base;
         save_scc(base, cnt);
@@ -256,9 +273,15 @@ struct W {
         *saved = true;
       }
       --fsp;
-      if (fsp) {
+      if (fsp) {  // resume the parent frame (tarjan.rs:211: low = min(low, dep low))
         const uint32_t p = rd(L.fv, fsp - 1);
-        put(L.vlow, p, min(rd(L.vlow, p), lowv));
+        cv = p;
+        ci = rd(L.fi, fsp - 1);
+        cid = rd(L.vid, p);
+        clow = min(rd(L.vlow, p), lowv);
+        cdot = rd(L.vdot, p);
+        cnd = rd(L.vnd, p);
+        drow = lid < cnd ? at(L.vdeps, p * L.D + lid) : 0u;
         if (mcount) put(L.fm, fsp - 1, rd(L.fm, fsp - 1) + mcount);  // tarjan.rs:198-200
       } else if (mcount) {
         result = MISSING;  // NotFound -> MissingDependencies(collected) (mod.rs:478-484)
