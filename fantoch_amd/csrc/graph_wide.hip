@@ -139,11 +139,16 @@ struct W {
   __device__ __forceinline__ uint32_t hslot(uint32_t d) const {
     return (FX_DOT_SRC(d) - 1) * L.Q + (FX_DOT_SEQ(d) & (L.Q - 1u));
   }
+  // an index word is (vertex + 1) | seq / Q << 16: it names its dot without
+  // a read of the vertex table (the slot gives the source and seq mod Q)
+  __device__ __forceinline__ uint32_t htag(uint32_t d) const {
+    return (FX_DOT_SEQ(d) >> __builtin_ctz(L.Q)) << 16;
+  }
   __device__ __forceinline__ uint32_t find(uint32_t d) {
     const uint32_t src = FX_DOT_SRC(d);
     if (src < 1 || src > L.n) return NONE;
-    const uint32_t v = rd(L.hidx, hslot(d));
-    return (v != 0 && rd(L.vdot, v - 1) == d) ? v - 1 : NONE;
+    const uint32_t w = rd(L.hidx, hslot(d));
+    return ((w & 0xFFFFu) != 0 && (w & 0xFFFF0000u) == htag(d)) ? (w & 0xFFFFu) - 1u : NONE;
   }
 
   // ------------------------------------------------------- emission
@@ -232,13 +237,13 @@ struct W {
           result = MISSING;
           break;
         }
-        const uint32_t idw = rd(L.vid, w);
+        const uint32_t idw = rd(L.vid, w), mkw = rd(L.vmark, w);  // both reads in flight at once
         if (idw == 0) {  // recurse
           put(L.fi, fsp - 1, ci);
           put(L.vlow, cv, clow);
           ++idc;
           put(L.vid, w, idc);
-          put(L.vmark, w, rd(L.vmark, w) | 1u);
+          put(L.vmark, w, mkw | 1u);
           put(L.tstk, tsp++, w);
           put(L.fv, fsp, w);
           if (partial) put(L.fm, fsp, 0);
@@ -250,7 +255,7 @@ struct W {
           cdot = d;
           cnd = rd(L.vnd, w);
           drow = lid < cnd ? at(L.vdeps, w * L.D + lid) : 0u;
-        } else if (rd(L.vmark, w) & 1u) {  // on the stack
+        } else if (mkw & 1u) {  // on the stack
           clow = min(clow, idw);
         }
         continue;
@@ -422,7 +427,7 @@ struct W {
     const uint32_t h = hslot(d);
     const uint32_t old = rd(L.hidx, h);
     if (old != 0) {
-      if (rd(L.vdot, old - 1) == d) { err = FX_ERR_DOUBLE_INDEX; return; }
+      if ((old & 0xFFFF0000u) == htag(d)) { err = FX_ERR_DOUBLE_INDEX; return; }
       err = FX_ERR_CAPACITY;  // two pending dots of a source share an index slot
       return;
     }
@@ -437,7 +442,7 @@ struct W {
     put(L.vid, v, 0);
     put(L.vmark, v, 0);
     if (partial) put(L.vwn, v, 0);
-    put(L.hidx, h, v + 1);
+    put(L.hidx, h, (v + 1) | htag(d));
     __syncthreads();
     if (kind == FX_KIND_INDEX_ONLY) return;  // VertexIndex::index without a search (test hook)
     uint32_t missing = 0;
