@@ -234,6 +234,8 @@ def main_sim(args):
             "executed_per_step": int(executed_all),
             "client_cmds_per_s": round(client_all * args.steps / elapsed, 1),
             "sim_events_per_s": round(events_all * args.steps / elapsed, 1),
+            # graph edges = deps of every executor Add, per second
+            "edges_per_s": round(deps_all * args.steps / elapsed, 1),
             "fast_paths": fast_all, "slow_paths": slow_all,
             "roofline": roof,
             "cpu_baseline": cpu,
