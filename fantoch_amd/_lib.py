@@ -136,6 +136,11 @@ class ExecutorResultC(ctypes.Structure):
     _fields_ = [("rifl", CRifl), ("key", ctypes.c_uint32), ("read_only", ctypes.c_uint32)]
 
 
+class RequestReplyC(ctypes.Structure):
+    _fields_ = [("to_shard", ctypes.c_uint64), ("kind", ctypes.c_uint32), ("dot", CDot), ("rifl", CRifl),
+                ("ndeps", ctypes.c_uint32), ("first_dep", ctypes.c_uint32)]
+
+
 class LogSummary(ctypes.Structure):
     _fields_ = [(f, ctypes.c_uint64) for f in
                 ("records", "adds", "others", "keys", "deps", "distinct_keys")]
@@ -251,6 +256,15 @@ SIGNATURES = [
      [ctypes.c_void_p, u64p, ctypes.POINTER(CDot), ctypes.c_uint32, u32p]),
     ("fx_graph_executor_to_executors", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.c_uint32, u32p]),
+    ("fx_graph_executor_clone", ctypes.c_void_p, [ctypes.c_void_p]),
+    ("fx_graph_executor_handle_executed_info", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.c_uint32]),
+    ("fx_graph_executor_handle_request", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(CDot), ctypes.c_uint32]),
+    ("fx_graph_executor_cleanup", ctypes.c_int, [ctypes.c_void_p]),
+    ("fx_graph_executor_request_replies", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(RequestReplyC), ctypes.c_uint32, ctypes.POINTER(CDot), u32p,
+      ctypes.c_uint32, u32p]),
     ("fx_graph_executor_parallel", ctypes.c_int, []),
     ("fx_graph_executor_transfer_stats", ctypes.c_int, [ctypes.c_void_p, u64p, u64p]),
     ("fx_sim_plan", ctypes.c_int,

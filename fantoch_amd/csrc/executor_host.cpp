@@ -84,6 +84,24 @@ struct fx_graph_executor {
   std::set<uint32_t> added;                           // added_to_executed_clock (device dots)
   DevBuf d_req;                                       // first-missing ring (fx_batch_execute_partial)
   uint32_t req_cap = 0;
+  std::map<uint32_t, uint32_t> rec_of;                // device dot -> arrival index of its Add (VertexIndex)
+  std::set<uint32_t> executed_set;                    // device dots executed here (left the VertexIndex)
+  // executor index > 0 (fx_graph_executor_clone): the handle whose VertexIndex
+  // it shares (index.rs:21), its own executed clock (per source: contiguous
+  // frontier + exceptions), buffered requests and the replies
+  fx_graph_executor* shared = nullptr;
+  std::map<uint32_t, std::pair<uint64_t, std::set<uint64_t>>> clock;
+  std::map<uint64_t, std::set<std::pair<uint32_t, uint64_t>>> buffered;
+  struct Reply {
+    uint64_t to;
+    bool info;
+    uint32_t src;
+    uint64_t seq;
+    fx_rifl rifl;
+    std::vector<fx_dot> deps;
+    std::vector<uint32_t> shards;
+  };
+  std::deque<Reply> replies;
 
   // device mirror
   uint32_t cap = 0;      // plane rows
@@ -302,7 +320,10 @@ int flush(fx_graph_executor* ex) {
       ex->execution_delay[delay] += 1;  // ExecutionDelay (mod.rs:514-518)
     }
     ex->executed.emplace_back(ex->dots[rec], start);  // device-local sequence
-    if (ex->partial) ex->added.insert(ex->dots[rec]);  // added_to_executed_clock (tarjan.rs:294-296)
+    if (ex->partial) {
+      ex->added.insert(ex->dots[rec]);  // added_to_executed_clock (tarjan.rs:294-296)
+      ex->executed_set.insert(ex->dots[rec]);
+    }
     const Cmd& c = ex->cmds[rec];
     for (uint32_t key : c.keys) {
       ex->to_clients.push_back(fx_executor_result{c.rifl, key, c.read_only});
@@ -355,6 +376,7 @@ int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys
   c.keys.erase(std::unique(c.keys.begin(), c.keys.end()), c.keys.end());
   c.read_only = read_only;
   ex->dots.push_back(FX_PACK_DOT(dot.source, dot.seq - ex->base[dot.source - 1]));
+  if (ex->partial && kind == FX_KIND_ADD) ex->rec_of[ex->dots.back()] = (uint32_t)ex->dots.size() - 1;
   ex->hdrs.push_back(FX_MAKE_HDR((uint32_t)(now_ms - ex->t_base), (uint32_t)dv.size(), kind));
   ex->deps.push_back(std::move(dv));
   ex->cmds.push_back(std::move(c));
@@ -394,6 +416,7 @@ void fx_graph_executor_free(fx_graph_executor* ex) {
 
 int fx_graph_executor_set_executor_index(fx_graph_executor* ex, uint32_t index) {
   if (!ex) return FX_ERR_INVALID_ARG;
+  if (ex->shared && index == 0) return FX_ERR_INVALID_ARG;  // a clone serves requests (index > 0)
   ex->executor_index = index;
   return FX_OK;
 }
@@ -456,6 +479,113 @@ int fx_graph_executor_to_executors(fx_graph_executor* ex, fx_dot* dots, uint32_t
     ex->added.erase(ex->added.begin());
     const uint32_t src = FX_DOT_SRC(d);
     dots[c++] = fx_dot{src, FX_DOT_SEQ(d) + ex->base[src - 1]};
+  }
+  *n_out = c;
+  return FX_OK;
+}
+
+// ---- executor index > 0 (partial replication, mod.rs:183-355)
+fx_graph_executor* fx_graph_executor_clone(fx_graph_executor* main) {
+  if (!main || !main->partial || main->shared) return nullptr;
+  auto* c = new fx_graph_executor();
+  c->process_id = main->process_id;
+  c->shard_id = main->shard_id;
+  c->cfg = main->cfg;
+  c->nsrc = main->nsrc;
+  c->partial = true;
+  c->shared = main;
+  c->executor_index = 1;  // set_executor_index may change it (> 0)
+  return c;
+}
+
+namespace {
+bool clone_clock_contains(const fx_graph_executor* c, uint32_t src, uint64_t seq) {
+  auto it = c->clock.find(src);
+  return it != c->clock.end() && (seq <= it->second.first || it->second.second.count(seq));
+}
+void clone_clock_add(fx_graph_executor* c, uint32_t src, uint64_t seq) {  // AboveExSet::add
+  auto& e = c->clock[src];
+  if (seq <= e.first) return;
+  e.second.insert(seq);
+  while (e.second.count(e.first + 1)) e.second.erase(++e.first);
+}
+// process_requests (mod.rs:294-355): a dot still in the shared VertexIndex is
+// answered with its vertex (Info), an executed one with Executed, the rest
+// are buffered for cleanup
+int process_requests(fx_graph_executor* c, uint64_t from, const std::set<std::pair<uint32_t, uint64_t>>& dots) {
+  fx_graph_executor* m = c->shared;
+  int st = flush(m);
+  if (st) return st;
+  for (const auto& gd : dots) {
+    const uint32_t src = gd.first;
+    const uint64_t seq = gd.second;
+    auto it = m->rec_of.end();
+    uint32_t dd = 0;
+    if (src >= 1 && src <= m->nsrc && seq > m->base[src - 1] && seq - m->base[src - 1] <= FX_SEQ_MASK) {
+      dd = FX_PACK_DOT(src, (uint32_t)(seq - m->base[src - 1]));
+      it = m->rec_of.find(dd);
+    }
+    if (it != m->rec_of.end() && !m->executed_set.count(dd)) {
+      fx_graph_executor::Reply r{from, true, src, seq, m->cmds[it->second].rifl, {}, {}};
+      for (uint32_t x : m->deps[it->second]) {
+        const uint32_t s2 = FX_DOT_SRC(x);
+        r.deps.push_back(fx_dot{s2, FX_DOT_SEQ(x) + (s2 >= 1 && s2 <= m->nsrc ? m->base[s2 - 1] : 0)});
+        auto mk = m->dep_mask.find(x);
+        r.shards.push_back(mk == m->dep_mask.end() ? 0u : mk->second);
+      }
+      c->replies.push_back(std::move(r));
+    } else if (clone_clock_contains(c, src, seq)) {
+      c->replies.push_back(fx_graph_executor::Reply{from, false, src, seq, fx_rifl{0, 0}, {}, {}});
+    } else {
+      c->buffered[from].insert(gd);
+    }
+  }
+  return FX_OK;
+}
+}  // namespace
+
+int fx_graph_executor_handle_executed_info(fx_graph_executor* ex, const fx_dot* dots, uint32_t n) {
+  if (!ex || (n && !dots)) return FX_ERR_INVALID_ARG;
+  if (ex->executor_index == 0 || !ex->shared) return FX_OK;  // handle_executed: index 0 ignores it
+  for (uint32_t i = 0; i < n; ++i) clone_clock_add(ex, dots[i].source, dots[i].seq);
+  return FX_OK;
+}
+
+int fx_graph_executor_handle_request(fx_graph_executor* ex, uint64_t from_shard, const fx_dot* dots, uint32_t n) {
+  if (!ex || (n && !dots)) return FX_ERR_INVALID_ARG;
+  if (ex->executor_index == 0 || !ex->shared) return FX_ERR_INVALID_ARG;  // mod.rs:283 assert!(executor_index > 0)
+  std::set<std::pair<uint32_t, uint64_t>> ds;
+  for (uint32_t i = 0; i < n; ++i) ds.insert({dots[i].source, dots[i].seq});
+  return process_requests(ex, from_shard, ds);
+}
+
+int fx_graph_executor_cleanup(fx_graph_executor* ex) {
+  if (!ex) return FX_ERR_INVALID_ARG;
+  if (ex->executor_index == 0 || !ex->shared) return FX_OK;
+  std::map<uint64_t, std::set<std::pair<uint32_t, uint64_t>>> b;
+  b.swap(ex->buffered);
+  for (const auto& kv : b) {
+    int st = process_requests(ex, kv.first, kv.second);
+    if (st) return st;
+  }
+  return FX_OK;
+}
+
+int fx_graph_executor_request_replies(fx_graph_executor* ex, fx_request_reply* out, uint32_t cap, fx_dot* deps,
+                                      uint32_t* dep_shards, uint32_t deps_cap, uint32_t* n_out) {
+  if (!ex || !n_out || (cap && !out) || (deps_cap && (!deps || !dep_shards))) return FX_ERR_INVALID_ARG;
+  uint32_t c = 0, k = 0;
+  while (c < cap && !ex->replies.empty()) {
+    const auto& r = ex->replies.front();
+    if (k + r.deps.size() > deps_cap) break;
+    out[c] = fx_request_reply{r.to, r.info ? 1u : 0u, fx_dot{r.src, (uint32_t)r.seq}, r.rifl,
+                              (uint32_t)r.deps.size(), k};
+    for (size_t j = 0; j < r.deps.size(); ++j, ++k) {
+      deps[k] = r.deps[j];
+      dep_shards[k] = r.shards[j];
+    }
+    ex->replies.pop_front();
+    ++c;
   }
   *n_out = c;
   return FX_OK;

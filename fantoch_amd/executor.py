@@ -96,6 +96,10 @@ class GraphExecutor:
             if got.value < 256:
                 return out
 
+    def clone(self):
+        """Executor index > 0 sharing this handle's VertexIndex (partial replication)."""
+        return ExecutorClone(self)
+
     def index_only(self, dot, rifl, keys, deps, time_ms=0):
         keys = list(keys)
         karr = (ctypes.c_uint32 * max(len(keys), 1))(*keys)
@@ -175,3 +179,59 @@ class GraphExecutor:
         check(_lib.load().fx_graph_executor_transfer_stats(self._h, ctypes.byref(h2d),
                                                            ctypes.byref(d2h)))
         return h2d.value, d2h.value
+
+
+class ExecutorClone:
+    """Executor index > 0 of a partial-replication process: GraphExecutionInfo::
+    Executed, Request serving and cleanup (graph/mod.rs:183-355)."""
+
+    def __init__(self, main):
+        self.main = main  # freed after the clone
+        h = _lib.load().fx_graph_executor_clone(main._h)
+        if not h:
+            raise _lib.FxError(_lib.FX_ERR_INVALID_ARG, "fx_graph_executor_clone")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            _lib.load().fx_graph_executor_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _dots(self, dots):
+        dots = list(dots)
+        return (CDot * max(len(dots), 1))(*[CDot(int(s), int(q)) for s, q in dots]), len(dots)
+
+    def handle_executed(self, dots):
+        arr, n = self._dots(dots)
+        check(_lib.load().fx_graph_executor_handle_executed_info(self._h, arr, n), "handle_executed_info")
+
+    def handle_request(self, from_shard, dots):
+        arr, n = self._dots(dots)
+        check(_lib.load().fx_graph_executor_handle_request(self._h, int(from_shard), arr, n), "handle_request")
+
+    def cleanup(self):
+        check(_lib.load().fx_graph_executor_cleanup(self._h), "cleanup")
+
+    def replies(self):
+        """Drains [(to shard, 'info' | 'executed', dot, [(dep, shards)])]."""
+        out = []
+        buf = (_lib.RequestReplyC * 256)()
+        deps = (CDot * 8192)()
+        sh = (ctypes.c_uint32 * 8192)()
+        got = ctypes.c_uint32()
+        while True:
+            check(_lib.load().fx_graph_executor_request_replies(self._h, buf, 256, deps, sh, 8192,
+                                                                 ctypes.byref(got)), "request_replies")
+            for i in range(got.value):
+                r = buf[i]
+                d = [((deps[r.first_dep + j].source, deps[r.first_dep + j].seq), sh[r.first_dep + j])
+                     for j in range(r.ndeps)]
+                out.append((r.to_shard, "info" if r.kind else "executed", (r.dot.source, r.dot.seq), d))
+            if got.value < 256:
+                return out

@@ -376,8 +376,7 @@ int fx_graph_executor_handle_add(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl
  * requests drains DependencyGraph::requests (mod.rs:148-151) as (target
  * shard, dot) pairs, ascending; to_executors drains the dots added to the
  * executed clock (mod.rs:137-144, the Executed info of fetch_to_executors,
- * executor.rs:140-152), ascending.  Serving Requests (executor index > 0,
- * handle_request over the shared VertexIndex, mod.rs:277-355) is not exported. */
+ * executor.rs:140-152), ascending.  Requests are served by a clone (below). */
 int fx_graph_executor_handle_add_sharded(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl,
                                          const uint32_t* keys, uint32_t nkeys, uint32_t read_only,
                                          const fx_dot* deps, const uint32_t* dep_shards, uint32_t ndeps,
@@ -386,6 +385,30 @@ int fx_graph_executor_handle_executed(fx_graph_executor* ex, const fx_dot* dots,
 int fx_graph_executor_requests(fx_graph_executor* ex, uint64_t* shards, fx_dot* dots, uint32_t cap,
                                uint32_t* n_out);
 int fx_graph_executor_to_executors(fx_graph_executor* ex, fx_dot* dots, uint32_t cap, uint32_t* n_out);
+/* Executor index > 0 of the same process (run mode clones the executor per
+ * task and shares the VertexIndex, index.rs:21): a clone of a partial-
+ * replication handle reads its main handle's vertices, keeps its own executed
+ * clock (GraphExecutionInfo::Executed -> handle_executed_info, mod.rs:211-223),
+ * serves Requests from other shards (handle_request / process_requests,
+ * mod.rs:277-355: a vertex still pending -> RequestReply::Info with its deps,
+ * an executed dot -> RequestReply::Executed, otherwise buffered) and retries
+ * the buffered ones on cleanup (mod.rs:183-195).  Info replies carry the rifl
+ * and deps; the command's ops stay with the caller (keyed by dot).  Free the
+ * clone before its main handle.  Serving a request flushes the main handle. */
+typedef struct fx_request_reply {
+  uint64_t to_shard;
+  uint32_t kind;      /* 1 = Info{dot, cmd, deps}, 0 = Executed{dot} */
+  fx_dot dot;
+  fx_rifl rifl;       /* Info: the command's rifl */
+  uint32_t ndeps;     /* Info: deps at deps[first_dep, first_dep + ndeps) */
+  uint32_t first_dep;
+} fx_request_reply;
+fx_graph_executor* fx_graph_executor_clone(fx_graph_executor* main);
+int fx_graph_executor_handle_executed_info(fx_graph_executor* ex, const fx_dot* dots, uint32_t n);
+int fx_graph_executor_handle_request(fx_graph_executor* ex, uint64_t from_shard, const fx_dot* dots, uint32_t n);
+int fx_graph_executor_cleanup(fx_graph_executor* ex);
+int fx_graph_executor_request_replies(fx_graph_executor* ex, fx_request_reply* out, uint32_t cap, fx_dot* deps,
+                                      uint32_t* dep_shards, uint32_t deps_cap, uint32_t* n_out);
 /* Test hook mirroring `queue.vertex_index.index(Vertex::new(..))` (mod.rs:1164-1306). */
 int fx_graph_executor_index_only(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl,
                                  const uint32_t* keys, uint32_t nkeys,

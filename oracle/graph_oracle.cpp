@@ -17,7 +17,10 @@
 //   VertexIndex .................. graph/index.rs:18-51
 //   PendingIndex ................. graph/index.rs:145-208
 //   TarjanSCCFinder .............. graph/tarjan.rs:25-316
-//   DependencyGraph .............. graph/mod.rs:45-677 (shard_count == 1)
+//   DependencyGraph .............. graph/mod.rs:45-677 (with partial
+//                                  replication: first-search collection,
+//                                  out-requests, Executed replies and the
+//                                  request-serving clone, graph_oracle.hpp)
 //   GraphExecutor::handle ........ graph/executor.rs:69-93
 //
 // Canonicalisation: C1 a vertex's deps are iterated in
@@ -301,6 +304,46 @@ uint32_t oracle_graph_waits(void* gp, uint32_t* vsrc, uint64_t* vseq, uint32_t* 
     }
     ++m;
   }
+  return m;
+}
+
+// Executor index > 0 sharing `gp`'s VertexIndex (partial replication).
+void* oracle_clone_new(void* gp) { return new oracle::ExecutorClone{static_cast<DependencyGraph*>(gp), {}, {}, {}}; }
+void oracle_clone_free(void* c) { delete static_cast<oracle::ExecutorClone*>(c); }
+void oracle_clone_handle_executed(void* c, const uint32_t* src, const uint64_t* seq, uint32_t n) {
+  std::vector<Dot> dots;
+  for (uint32_t i = 0; i < n; ++i) dots.push_back(Dot{src[i], seq[i]});
+  static_cast<oracle::ExecutorClone*>(c)->handle_executed(dots);
+}
+void oracle_clone_handle_request(void* c, uint32_t from, const uint32_t* src, const uint64_t* seq, uint32_t n) {
+  std::set<Dot> dots;
+  for (uint32_t i = 0; i < n; ++i) dots.insert(Dot{src[i], seq[i]});
+  static_cast<oracle::ExecutorClone*>(c)->handle_request(from, dots);
+}
+void oracle_clone_cleanup(void* c) { static_cast<oracle::ExecutorClone*>(c)->cleanup(); }
+// Drains request replies: per reply (to shard, kind 1 Info / 0 Executed, dot,
+// rec, ndeps) and its deps appended to dep_src / dep_seq / dep_shards.
+uint32_t oracle_clone_replies(void* c, uint32_t* to_shard, uint32_t* kind, uint32_t* src, uint64_t* seq,
+                              uint32_t* rec, uint32_t* ndeps, uint32_t cap, uint32_t* dep_src, uint64_t* dep_seq,
+                              uint32_t* dep_shards, uint32_t dep_cap) {
+  auto* cl = static_cast<oracle::ExecutorClone*>(c);
+  uint32_t m = 0, k = 0;
+  for (const auto& r : cl->out_request_replies) {
+    if (m >= cap || k + r.deps.size() > dep_cap) break;
+    to_shard[m] = r.to_shard;
+    kind[m] = r.info ? 1 : 0;
+    src[m] = r.dot.source;
+    seq[m] = r.dot.sequence;
+    rec[m] = r.rec;
+    ndeps[m] = (uint32_t)r.deps.size();
+    for (size_t j = 0; j < r.deps.size(); ++j, ++k) {
+      dep_src[k] = r.deps[j].source;
+      dep_seq[k] = r.deps[j].sequence;
+      dep_shards[k] = r.dep_shards[j];
+    }
+    ++m;
+  }
+  cl->out_request_replies.erase(cl->out_request_replies.begin(), cl->out_request_replies.begin() + m);
   return m;
 }
 

@@ -379,5 +379,51 @@ struct DependencyGraph {
   }
 };
 
+// An executor with index > 0 of the same process (partial replication, run
+// mode): it clones the DependencyGraph but shares its VertexIndex (index.rs:21,
+// an Arc), keeps its own executed clock fed by GraphExecutionInfo::Executed
+// (handle_executed, mod.rs:211-223) and serves Requests from other shards
+// (handle_request / process_requests, mod.rs:277-355; cleanup retries the
+// buffered ones, mod.rs:183-195, 669-675).
+struct RequestReply {
+  uint32_t to_shard;
+  bool info;  // Info{dot, cmd, deps} or Executed{dot}
+  Dot dot;
+  uint32_t rec;  // the vertex's arrival index (stands in for `cmd`)
+  std::vector<Dot> deps;
+  std::vector<uint32_t> dep_shards;
+};
+
+struct ExecutorClone {
+  DependencyGraph* main;
+  AEClock executed_clock;
+  std::map<uint32_t, std::set<Dot>> buffered_in_requests;
+  std::vector<RequestReply> out_request_replies;
+
+  void handle_executed(const std::vector<Dot>& dots) {
+    for (const Dot& d : dots) executed_clock.add(d.source, d.sequence);
+  }
+  void process_requests(uint32_t from, const std::set<Dot>& dots) {
+    for (const Dot& dot : dots) {  // a HashSet in the reference; ascending here
+      Vertex* v = main->find(dot);
+      if (v != nullptr) {
+        RequestReply r{from, true, dot, v->rec, v->deps, v->dep_shards};
+        if (r.dep_shards.size() < r.deps.size()) r.dep_shards.resize(r.deps.size(), 1u << main->shard_id);
+        out_request_replies.push_back(std::move(r));
+      } else if (executed_clock.contains(dot.source, dot.sequence)) {
+        out_request_replies.push_back(RequestReply{from, false, dot, 0, {}, {}});
+      } else {
+        buffered_in_requests[from].insert(dot);
+      }
+    }
+  }
+  void handle_request(uint32_t from, const std::set<Dot>& dots) { process_requests(from, dots); }
+  void cleanup() {  // check_pending_requests
+    std::map<uint32_t, std::set<Dot>> buffered;
+    buffered.swap(buffered_in_requests);
+    for (auto& kv : buffered) process_requests(kv.first, kv.second);
+  }
+};
+
 }  // namespace oracle
 

@@ -67,6 +67,14 @@ def load():
         lib.oracle_graph_requests.argtypes = [vp, P32, P32, P64, u32]
         lib.oracle_graph_to_executors.restype = u32
         lib.oracle_graph_to_executors.argtypes = [vp, P32, P64, u32]
+        lib.oracle_clone_new.restype = vp
+        lib.oracle_clone_new.argtypes = [vp]
+        lib.oracle_clone_free.argtypes = [vp]
+        lib.oracle_clone_handle_executed.argtypes = [vp, P32, P64, u32]
+        lib.oracle_clone_handle_request.argtypes = [vp, u32, P32, P64, u32]
+        lib.oracle_clone_cleanup.argtypes = [vp]
+        lib.oracle_clone_replies.restype = u32
+        lib.oracle_clone_replies.argtypes = [vp, P32, P32, P32, P64, P32, P32, u32, P32, P64, P32, u32]
         lib.oracle_graph_waits.restype = u32
         lib.oracle_graph_waits.argtypes = [vp, P32, P64, P32, P64, u32]
         _lib = lib
@@ -191,6 +199,10 @@ class Graph:
         m = self.lib.oracle_graph_waits(self.h, vs, vq, ps, pq, cap)
         return [((vs[i], vq[i]), (ps[i], pq[i])) for i in range(min(m, cap))]
 
+    def clone(self):
+        """An executor with index > 0 sharing this graph's VertexIndex."""
+        return GraphClone(self)
+
     def index_only(self, dot, deps, t_ms=0):
         src, seq, nd = self._deps(deps)
         r = self.lib.oracle_graph_index_only(self.h, dot[0], dot[1], src, seq, nd, t_ms, self.rec)
@@ -239,6 +251,47 @@ class Graph:
         c = (ctypes.c_uint64 * 4096)()
         m = self.lib.oracle_graph_metrics(self.h, kind, v, c, 4096)
         return {int(v[i]): int(c[i]) for i in range(min(m, 4096))}
+
+
+class GraphClone:
+    """Executor index > 0 of a partial-replication process (mod.rs:211-355)."""
+
+    def __init__(self, main):
+        self.main = main  # keeps the shared graph alive
+        self.lib = main.lib
+        self.h = self.lib.oracle_clone_new(main.h)
+
+    def __del__(self):
+        try:
+            self.lib.oracle_clone_free(self.h)
+        except Exception:
+            pass
+
+    def handle_executed(self, dots):
+        src, seq, n = self.main._deps(dots)
+        self.lib.oracle_clone_handle_executed(self.h, src, seq, n)
+
+    def handle_request(self, from_shard, dots):
+        src, seq, n = self.main._deps(dots)
+        self.lib.oracle_clone_handle_request(self.h, from_shard, src, seq, n)
+
+    def cleanup(self):
+        self.lib.oracle_clone_cleanup(self.h)
+
+    def replies(self):
+        """Drains [(to shard, 'info' | 'executed', dot, [(dep, shards)])]."""
+        cap, dcap = 4096, 1 << 16
+        to, kind, src, rec, nd = [(ctypes.c_uint32 * cap)() for _ in range(5)]
+        seq = (ctypes.c_uint64 * cap)()
+        ds, dsh = (ctypes.c_uint32 * dcap)(), (ctypes.c_uint32 * dcap)()
+        dq = (ctypes.c_uint64 * dcap)()
+        m = self.lib.oracle_clone_replies(self.h, to, kind, src, seq, rec, nd, cap, ds, dq, dsh, dcap)
+        out, k = [], 0
+        for i in range(m):
+            deps = [((ds[k + j], dq[k + j]), dsh[k + j]) for j in range(nd[i])]
+            k += nd[i]
+            out.append((to[i], "info" if kind[i] else "executed", (src[i], seq[i]), deps))
+        return out
 
 
 # ------------------------------------------------------------ simulator

@@ -159,3 +159,66 @@ def run_kat(backend):
             backend.executed([op[1]], t)
         out.append(backend.pull())
     return out
+
+
+def drive_serving(hist, order, backend, seed=0, req_pct=30):
+    """The main executor of shard 0 takes the Adds of its commands; its clone
+    (executor index 1) gets every step's executed dots (to_executors ->
+    GraphExecutionInfo::Executed) and Requests from shard 1 for random dots of
+    shard-0 commands (delivered, pending or not yet added), with a cleanup
+    every third step.  Returns the replies per step."""
+    rng = np.random.default_rng(seed)
+    by_dot = {d: (m, deps) for d, m, deps in hist}
+    idx_dot = [d for d, _, _ in hist]
+    mine = [idx_dot[i] for i in order]
+    log = []
+    for t, i in enumerate(order):
+        d = idx_dot[i]
+        m, deps = by_dot[d]
+        backend.add(d, [idx_dot[k] for k in deps], [hist[k][1] for k in deps], t)
+        backend.clone_executed(backend.pull()[2])
+        if rng.integers(100) < req_pct:
+            k = int(rng.integers(1, 4))
+            backend.request(1, [mine[int(j)] for j in rng.integers(0, len(mine), size=k)])
+        if t % 3 == 2:
+            backend.cleanup()
+        log.append(backend.replies())
+    backend.cleanup()
+    log.append(backend.replies())
+    return log
+
+
+class OracleServing(OracleBackend):
+    def __init__(self, n, shards, shard):
+        super().__init__(n, shards, shard)
+        self.c = self.g.clone()
+
+    def clone_executed(self, dots):
+        self.c.handle_executed(dots)
+
+    def request(self, from_shard, dots):
+        self.c.handle_request(from_shard, dots)
+
+    def cleanup(self):
+        self.c.cleanup()
+
+    def replies(self):
+        return [(to, kind, dot, deps) for to, kind, dot, deps in self.c.replies()]
+
+
+class GpuServing(GpuBackend):
+    def __init__(self, n, shards, shard):
+        super().__init__(n, shards, shard)
+        self.c = self.ex.clone()
+
+    def clone_executed(self, dots):
+        self.c.handle_executed(dots)
+
+    def request(self, from_shard, dots):
+        self.c.handle_request(from_shard, dots)
+
+    def cleanup(self):
+        self.c.cleanup()
+
+    def replies(self):
+        return self.c.replies()

@@ -51,3 +51,25 @@ def test_gpu_partial_scenarios_match_oracle(seed, n, shards):
     for k, (a, b) in enumerate(zip(lo, lg)):
         assert a == b, k
     assert o.waits() == g.waits() == []
+
+
+def test_oracle_clone_serves_requests():
+    hist, order = P.scenario(5, n=2, shards=2, shard=0)
+    b = P.OracleServing(2, 2, 0)
+    log = P.drive_serving(hist, order, b, seed=5)
+    kinds = [r[1] for step in log for r in step]
+    assert "info" in kinds and "executed" in kinds
+    # every request is answered once its dot is delivered (the final cleanup
+    # runs after the last Add; an Info dot was pending, an Executed one executed)
+    assert b.c.replies() == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [5, 6])
+def test_gpu_clone_serves_requests_like_oracle(seed):
+    hist, order = P.scenario(seed, n=2, shards=2, shard=0)
+    lo = P.drive_serving(hist, order, P.OracleServing(2, 2, 0), seed=seed)
+    lg = P.drive_serving(hist, order, P.GpuServing(2, 2, 0), seed=seed)
+    assert len(lo) == len(lg)
+    for k, (a, b) in enumerate(zip(lo, lg)):
+        assert a == b, k
