@@ -131,49 +131,37 @@ int upload_all(fx_graph_executor* ex, uint32_t new_cap, uint32_t new_dmax) {
       !ex->d_order.ensure(plane * 4) || !ex->d_release.ensure(plane * 4) ||
       !ex->d_nexec.ensure(4) || !ex->d_err.ensure(4))
     return FX_ERR_HIP;
-  std::vector<uint32_t> hd(plane, 0), hh(plane, 0), hp(plane * std::max<uint32_t>(new_dmax, 1), 0);
-  const uint32_t N = (uint32_t)ex->dots.size();
-  for (uint32_t i = 0; i < N; ++i) {
-    const size_t at = fx_index(i, 0, new_cap);
-    hd[at] = ex->dots[i];
-    hh[at] = ex->hdrs[i];
-    for (uint32_t j = 0; j < ex->deps[i].size(); ++j) hp[j * plane + at] = ex->deps[i][j];
-  }
-  ex->bytes_h2d += (uint64_t)(hd.size() + hh.size() + hp.size()) * 4;
-  if (hipMemcpyAsync(ex->d_dot.p, hd.data(), plane * 4, hipMemcpyHostToDevice, ex->stream) ||
-      hipMemcpyAsync(ex->d_hdr.p, hh.data(), plane * 4, hipMemcpyHostToDevice, ex->stream) ||
-      hipMemcpyAsync(ex->d_deps.p, hp.data(), hp.size() * 4, hipMemcpyHostToDevice, ex->stream) ||
-      hipStreamSynchronize(ex->stream))
-    return FX_ERR_HIP;
   ex->cap = new_cap;
   ex->dmax = new_dmax;
-  ex->uploaded = N;
+  ex->uploaded = 0;  // the whole log again, as strided rows (upload_tail)
   return FX_OK;
 }
 
-// Copies rows [from, N) of the single-stream planes to the device.
+// Copies rows [uploaded, N) of the single-stream planes to the device.  The
+// plane is tiled 64 streams x 4 steps; a one-stream handle fills only the
+// first 4 words of each 256-word tile, so each plane goes over as a strided
+// 2-D copy of those words (16 bytes per tile) instead of whole tiles.
 int upload_tail(fx_graph_executor* ex) {
   const uint32_t N = (uint32_t)ex->dots.size();
   if (ex->uploaded >= N) return FX_OK;
   const uint32_t r0 = ex->uploaded & ~3u;
   const uint32_t r1 = (N + 3) & ~3u;
-  const size_t w0 = fx_index(r0, 0, ex->cap), words = (size_t)(r1 - r0) / 4 * 256;
+  const size_t tiles = (r1 - r0) / 4, w0 = fx_index(r0, 0, ex->cap);
   const size_t plane = fx_plane_words(1, ex->cap);
-  std::vector<uint32_t> hd(words, 0), hh(words, 0), hp(words * ex->dmax, 0);
+  std::vector<uint32_t> hd(tiles * 4, 0), hh(tiles * 4, 0), hp(tiles * 4 * ex->dmax, 0);
   for (uint32_t i = r0; i < N; ++i) {
-    const size_t at = fx_index(i, 0, ex->cap) - w0;
+    const size_t at = i - r0;
     hd[at] = ex->dots[i];
     hh[at] = ex->hdrs[i];
-    for (uint32_t j = 0; j < ex->deps[i].size(); ++j) hp[j * words + at] = ex->deps[i][j];
+    for (uint32_t j = 0; j < ex->deps[i].size(); ++j) hp[j * tiles * 4 + at] = ex->deps[i][j];
   }
   ex->bytes_h2d += (uint64_t)(hd.size() + hh.size() + hp.size()) * 4;
-  if (hipMemcpyAsync(ex->d_dot.u32() + w0, hd.data(), words * 4, hipMemcpyHostToDevice, ex->stream) ||
-      hipMemcpyAsync(ex->d_hdr.u32() + w0, hh.data(), words * 4, hipMemcpyHostToDevice, ex->stream))
-    return FX_ERR_HIP;
+  auto put2d = [&](uint32_t* dst, const uint32_t* src) {
+    return hipMemcpy2DAsync(dst, 256 * 4, src, 4 * 4, 4 * 4, tiles, hipMemcpyHostToDevice, ex->stream);
+  };
+  if (put2d(ex->d_dot.u32() + w0, hd.data()) || put2d(ex->d_hdr.u32() + w0, hh.data())) return FX_ERR_HIP;
   for (uint32_t j = 0; j < ex->dmax; ++j)
-    if (hipMemcpyAsync(ex->d_deps.u32() + j * plane + w0, hp.data() + j * words, words * 4,
-                       hipMemcpyHostToDevice, ex->stream))
-      return FX_ERR_HIP;
+    if (put2d(ex->d_deps.u32() + j * plane + w0, hp.data() + j * tiles * 4)) return FX_ERR_HIP;
   if (hipStreamSynchronize(ex->stream)) return FX_ERR_HIP;
   ex->uploaded = N;
   return FX_OK;
@@ -191,7 +179,8 @@ int flush(fx_graph_executor* ex) {
     while (nc < N) nc *= 2;
     int st = upload_all(ex, nc, std::max<uint32_t>(need_dmax, 1));
     if (st) return ex->sticky = st;
-  } else {
+  }
+  {
     int st = upload_tail(ex);
     if (st) return ex->sticky = st;
   }
@@ -285,12 +274,13 @@ int flush(fx_graph_executor* ex) {
   const uint32_t k0 = ex->consumed;
   {
     const uint32_t r0 = k0 & ~3u, r1 = (nexec + 3) & ~3u;
-    std::vector<uint32_t> rows((size_t)(r1 - r0) / 4 * 256);
-    if (hipMemcpyAsync(rows.data(), ex->d_order.u32() + fx_index(r0, 0, ex->cap), rows.size() * 4,
-                       hipMemcpyDeviceToHost, ex->stream) ||
+    // the first 4 words of each tile (this stream's rows), strided
+    std::vector<uint32_t> rows((size_t)(r1 - r0));
+    if (hipMemcpy2DAsync(rows.data(), 4 * 4, ex->d_order.u32() + fx_index(r0, 0, ex->cap), 256 * 4, 4 * 4,
+                         (r1 - r0) / 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipStreamSynchronize(ex->stream))
       return ex->sticky = FX_ERR_HIP;
-    for (uint32_t k = k0; k < nexec; ++k) order[k - k0] = rows[fx_index(k, 0, ex->cap) - fx_index(r0, 0, ex->cap)];
+    for (uint32_t k = k0; k < nexec; ++k) order[k - k0] = rows[k - r0];
   }
   // the release steps of exactly the commands converted below, gathered on
   // the device (bytes moved per flush are linear in its new order entries)

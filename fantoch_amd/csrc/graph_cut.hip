@@ -74,23 +74,38 @@ __device__ __forceinline__ uint64_t pos_slot(const In& in, const uint64_t* base,
   return base[s] + (uint64_t)(src - 1) * (ms + 1) + sq;
 }
 
-// atomicMax(&out[s], v) with one atomic per distinct s in the wavefront
-// (a wave's threads cover consecutive steps, so usually one stream)
-__device__ __forceinline__ void wave_max_per_stream(uint32_t s, uint32_t v, uint32_t* out) {
-  uint64_t todo = __ballot(true);
-  while (todo) {
-    const uint32_t lead = __builtin_ctzll(todo);
-    const uint32_t s0 = (uint32_t)__shfl((int)s, (int)lead);
-    const bool mine = s == s0;
-    uint32_t m = mine ? v : 0u;
-    for (uint32_t off = 32; off; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
-    if ((threadIdx.x & 63u) == lead) atomicMax(&out[s0], m);
-    todo &= ~__ballot(mine);
+// Per-stream max over a grid-stride loop: each wave keeps a running (stream,
+// max) pair and issues one atomicMax per stream it leaves (a handful per wave)
+// instead of one per iteration: with a few long streams, per-iteration
+// atomics on a few addresses serialised at L2 and dominated the cut analysis.
+struct WaveMax {
+  uint32_t s = 0xFFFFFFFFu, m = 0;  // wave-uniform
+  __device__ __forceinline__ void add(uint32_t* out, uint32_t sl, uint32_t v) {
+    uint64_t todo = __ballot(true);
+    while (todo) {
+      const uint32_t lead = __builtin_ctzll(todo);
+      const uint32_t s0 = (uint32_t)__shfl((int)sl, (int)lead);
+      const bool mine = sl == s0;
+      uint32_t mm = mine ? v : 0u;
+      for (uint32_t off = 32; off; off >>= 1) mm = max(mm, (uint32_t)__shfl_xor((int)mm, off));
+      if (s0 == s) {
+        m = max(m, mm);
+      } else {
+        flush(out);
+        s = s0;
+        m = mm;
+      }
+      todo &= ~__ballot(mine);
+    }
   }
-}
+  __device__ __forceinline__ void flush(uint32_t* out) const {
+    if (s != 0xFFFFFFFFu && (threadIdx.x & 63u) == 0) atomicMax(&out[s], m);
+  }
+};
 
 __global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad) {
   const uint64_t total = (uint64_t)in.S * in.steps;
+  WaveMax acc;
   // wave-uniform trip count (the reduction needs every lane active)
   for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x; b0 < total; b0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t t = b0 + threadIdx.x;
@@ -104,8 +119,9 @@ __global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad) {
       if (src < 1 || src > in.n || FX_HDR_KIND(in.hdr[at]) != FX_KIND_ADD) bad[s] = 1;
       sq = FX_DOT_SEQ(d);
     }
-    wave_max_per_stream(s, sq, maxseq);
+    acc.add(maxseq, s, sq);
   }
+  acc.flush(maxseq);
 }
 
 __global__ void k_pos(In in, const uint64_t* base, const uint32_t* maxseq, uint32_t* pos, uint32_t* bad) {
@@ -247,6 +263,7 @@ __global__ void k_segs(In in, const uint8_t* flag, uint32_t nch, const uint32_t*
 // segment starts and lengths; longest segment per stream
 __global__ void k_seglen(uint64_t nseg, const uint64_t* segbase, const uint32_t* seg_end, const uint32_t* seg_stream,
                          uint32_t* seg_start, uint32_t* smax) {
+  WaveMax acc;
   for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x; b0 < nseg; b0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t k = b0 + threadIdx.x;
     const bool valid = k < nseg;
@@ -257,8 +274,9 @@ __global__ void k_seglen(uint64_t nseg, const uint64_t* segbase, const uint32_t*
       seg_start[k] = a;
       len = seg_end[k] - a + 1u;
     }
-    wave_max_per_stream(s, len, smax);
+    acc.add(smax, s, len);
   }
+  acc.flush(smax);
 }
 
 struct Seg {
@@ -359,6 +377,11 @@ struct DevBufs {
 static uint32_t grid_for(uint64_t work) {
   return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((work + BT - 1) / BT, 256u * 64u));
 }
+// per-stream max reductions (WaveMax): fewer, longer-running waves, so each
+// flushes one atomic per stream after many iterations (8 blocks per CU)
+static uint32_t grid_for_max(uint64_t work) {
+  return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((work + BT - 1) / BT, 256u * 8u));
+}
 
 }  // namespace cut
 }  // namespace fx
@@ -389,7 +412,7 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
   uint32_t* maxseq = db.alloc<uint32_t>(S, 0);
   uint32_t* bad = db.alloc<uint32_t>(S, 0);
   if (!maxseq || !bad) return FX_ERR_HIP;
-  hipLaunchKernelGGL(k_maxseq, dim3(grid_for(work)), dim3(BT), 0, hs, in, maxseq, bad);
+  hipLaunchKernelGGL(k_maxseq, dim3(grid_for_max(work)), dim3(BT), 0, hs, in, maxseq, bad);
   std::vector<uint32_t> h_maxseq(S), h_bad(S);
   (void)hipMemcpyAsync(h_maxseq.data(), maxseq, (size_t)S * 4, hipMemcpyDeviceToHost, hs);
   if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
@@ -440,7 +463,7 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
   if (!segbase || !seg_of || !seg_end || !seg_stream || !seg_start || !smax) return FX_ERR_HIP;
   (void)hipMemcpyAsync(segbase, h_segbase.data(), (size_t)S * 8, hipMemcpyHostToDevice, hs);
   hipLaunchKernelGGL(k_segs, dim3(nch * S), dim3(BT), 0, hs, in, flag, nch, ccnt, segbase, seg_of, seg_end, seg_stream);
-  if (NS) hipLaunchKernelGGL(k_seglen, dim3(grid_for(NS)), dim3(BT), 0, hs, NS, segbase, seg_end, seg_stream, seg_start, smax);
+  if (NS) hipLaunchKernelGGL(k_seglen, dim3(grid_for_max(NS)), dim3(BT), 0, hs, NS, segbase, seg_end, seg_stream, seg_start, smax);
   std::vector<uint32_t> h_smax(S);
   (void)hipMemcpyAsync(h_smax.data(), smax, (size_t)S * 4, hipMemcpyDeviceToHost, hs);
   if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
