@@ -123,6 +123,9 @@ def main_sim(args):
         ev0.record(stream)
         _lib.check(lib.fx_sim_run_tiered(ctypes.byref(batch), ctypes.byref(out), hs, None), "fx_sim_run_tiered")
         ev1.record(stream)
+        if world > 1:  # the step's output: histograms summed over every rank's instances (RCCL)
+            for h in (lat_hist, chain, delay):
+                dist.all_reduce(h)
         ev1.synchronize()
         kernel_ms.append(ev0.elapsed_time(ev1))
     torch.cuda.synchronize(dev)
@@ -144,8 +147,6 @@ def main_sim(args):
         dist.all_reduce(sm)
         elapsed = float(mx.item())
         executed_all, events_all, deps_all, client_all = [float(x) for x in sm.tolist()]
-        for h in (lat_hist, chain, delay):
-            dist.all_reduce(h)
     else:
         executed_all, events_all, deps_all, client_all = (float(executed_local), float(events_local),
                                                           float(deps_local), float(client_cmds_local))
