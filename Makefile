@@ -20,13 +20,6 @@ all: $(LIB) $(ORACLE) $(CPPTEST)
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
 
-# experiment build: the simulator at 4 waves per SIMD (FX_LIB=fantoch_amd/build_w4/libfantoch_amd.so)
-W4_LIB := fantoch_amd/build_w4/libfantoch_amd.so
-w4: $(W4_LIB)
-$(W4_LIB): $(SRCS) $(HDRS)
-	@mkdir -p fantoch_amd/build_w4
-	$(HIPCC) $(HIPFLAGS) -DFX_SIM_WAVES=4 -shared -o $@ $(SRCS)
-
 # phase-cycle profile build of the simulator (tools/sim_phase.py; FX_LIB=...)
 PROF_LIB := fantoch_amd/build_prof/libfantoch_amd.so
 prof: $(PROF_LIB)

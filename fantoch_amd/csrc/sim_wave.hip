@@ -63,7 +63,10 @@ constexpr uint32_t FMAX = 12;            // frame stack depth
 constexpr uint32_t RDMAX = 16;           // ready results per frame
 constexpr uint32_t HC_BINS = 64;         // ChainSize bins counted per instance in LDS
 constexpr uint32_t HD_BINS = 256;        // ExecutionDelay bins counted per instance in LDS
-constexpr uint32_t HL_LOG = 7, HL_SLOTS = 1u << HL_LOG;  // client-latency cache entries per instance
+#ifndef FX_SIM_HL_LOG
+#define FX_SIM_HL_LOG 6  // 64 entries: with them the configs[1] geometry fits 16 instances per CU
+#endif
+constexpr uint32_t HL_LOG = FX_SIM_HL_LOG, HL_SLOTS = 1u << HL_LOG;  // client-latency cache entries per instance
 constexpr uint32_t HMAX = 2;             // link heads per lane (links <= 128; a template parameter)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t LNIL = 0xFFFFu;  // end of a link's message list
@@ -1318,11 +1321,12 @@ struct Sim {
   }
 };
 
-template <uint32_t HM, uint32_t DS>
-#ifndef FX_SIM_WAVES
-#define FX_SIM_WAVES 3  // waves per SIMD the register budget of k_sim<., 1> targets
-#endif
-__global__ __launch_bounds__(64, DS == 1 ? FX_SIM_WAVES : 2) void k_sim(SimArgs a) {
+// WPS = waves per SIMD the register budget targets: 4 for launches whose LDS
+// lets 16 instances share a CU (the default configs[1] geometry: 10.0 KB at
+// n = 5 — 4 waves issue more of the scalar unit's slots than 3 even with a few
+// spilled registers, +14 %), 3 otherwise, 2 for the 256-slot dot tables
+template <uint32_t HM, uint32_t DS, uint32_t WPS>
+__global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
@@ -1634,22 +1638,25 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   a.err = o->err;
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 1, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     configured = true;
   }
   // link heads per lane: one when every link fits a lane
   // and one dot-table VGPR when the pool fits a lane each
   const dim3 grid(b->instances), block(64);
   hipStream_t hs = (hipStream_t)hip_stream;
+  const bool four = lds <= 160u * 1024u / 16u;  // 16 instances per CU: 4 waves per SIMD
   if (a.g.W <= 64) {
-    if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 1>), grid, block, lds, hs, a);
-    else hipLaunchKernelGGL((sim::k_sim<2, 1>), grid, block, lds, hs, a);
+    if (a.g.L <= 64 && four) hipLaunchKernelGGL((sim::k_sim<1, 1, 4>), grid, block, lds, hs, a);
+    else if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 1, 3>), grid, block, lds, hs, a);
+    else hipLaunchKernelGGL((sim::k_sim<2, 1, 3>), grid, block, lds, hs, a);
   } else {
-    if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 4>), grid, block, lds, hs, a);
-    else hipLaunchKernelGGL((sim::k_sim<2, 4>), grid, block, lds, hs, a);
+    if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 4, 2>), grid, block, lds, hs, a);
+    else hipLaunchKernelGGL((sim::k_sim<2, 4, 2>), grid, block, lds, hs, a);
   }
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
