@@ -71,7 +71,7 @@ def main():
         res["lds_bank_conflict_frac"] = round(c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"], 5)
     if c.get("GRBM_GUI_ACTIVE"):
         res["mean_waves_per_cu"] = round(4.0 * c["SQ_WAVE_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8) / 256, 2)
-        res["occupancy_frac"] = round(res["mean_waves_per_cu"] / 12.0, 3)  # 3 waves/SIMD (k_sim<1,1>) x 4 SIMDs
+        res["occupancy_frac"] = round(res["mean_waves_per_cu"] / 16.0, 3)  # 4 waves/SIMD (k_sim<1,1,4>) x 4 SIMDs
     if c.get("SQ_WAVES") or c.get("SQ_INSTS_VALU"):
         waves = c.get("SQ_WAVES") or 0
         if waves:
