@@ -171,7 +171,8 @@ __device__ __forceinline__ uint32_t tep(uint32_t t) { return t >> 14; }
 __device__ __forceinline__ uint32_t tmk(uint32_t id, uint32_t low, uint32_t ep) { return id | (low << 7) | (ep << 14); }
 constexpr uint32_t EPOCH_MAX = 0xFFFFu;
 
-template <uint32_t HM, uint32_t DS>
+// NX: processes the executor slot tables are sized for (n <= NX)
+template <uint32_t HM, uint32_t DS, uint32_t NX = NMAX>
 struct Sim {
   // ---------------------------------------------------------------- context
   uint32_t lid;
@@ -223,7 +224,7 @@ struct Sim {
   uint32_t ecf = 0, ecw = 0;
 
   // executor state of every process (lane-owned slot l / clock of source l + 1)
-  uint32_t xdot[NMAX], xrec[NMAX], xwait[NMAX];
+  uint32_t xdot[NX], xrec[NX], xwait[NX];
   // executor working copy (the process being run); the Tarjan words and the
   // DFS frames only live during one handle_add
   uint32_t sdot, srec, swait, stl, sfr;
@@ -1325,12 +1326,12 @@ struct Sim {
 // lets 16 instances share a CU (the default configs[1] geometry: 10.0 KB at
 // n = 5 — 4 waves issue more of the scalar unit's slots than 3 even with a few
 // spilled registers, +14 %), 3 otherwise, 2 for the 256-slot dot tables
-template <uint32_t HM, uint32_t DS, uint32_t WPS>
+template <uint32_t HM, uint32_t DS, uint32_t WPS, uint32_t NX>
 __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
-  Sim<HM, DS> s;
+  Sim<HM, DS, NX> s;
 #pragma unroll
   for (uint32_t k = 0; k < DS; ++k) s.sdv[k] = 0;
   s.lid = threadIdx.x;
@@ -1372,7 +1373,7 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
 #pragma unroll
   for (uint32_t k = 0; k < HM; ++k) s.ht[k] = s.hs[k] = NONE;
 #pragma unroll
-  for (uint32_t k = 0; k < NMAX; ++k) s.xdot[k] = s.xrec[k] = s.xwait[k] = 0;
+  for (uint32_t k = 0; k < NX; ++k) s.xdot[k] = s.xrec[k] = s.xwait[k] = 0;
   const uint32_t RP = a.RP;
   // process regions, quorums (BaseProcess::discover over
   // sort_processes_by_distance, base.rs:62-154, util.rs:153-185)
@@ -1638,11 +1639,12 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   a.err = o->err;
   static bool configured = false;
   if (!configured) {
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 1, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 4, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 3, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 1, 3, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 4, 2, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 4, 2, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     configured = true;
   }
   // link heads per lane: one when every link fits a lane
@@ -1651,12 +1653,15 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   hipStream_t hs = (hipStream_t)hip_stream;
   const bool four = lds <= 160u * 1024u / 16u;  // 16 instances per CU: 4 waves per SIMD
   if (a.g.W <= 64) {
-    if (a.g.L <= 64 && four) hipLaunchKernelGGL((sim::k_sim<1, 1, 4>), grid, block, lds, hs, a);
-    else if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 1, 3>), grid, block, lds, hs, a);
-    else hipLaunchKernelGGL((sim::k_sim<2, 1, 3>), grid, block, lds, hs, a);
+    // n <= 5 (configs[0], configs[1], half of configs[2]): executor tables
+    // for 5 processes, 9 VGPRs fewer under the 4-wave budget
+    if (a.g.L <= 64 && four && a.g.n <= 5) hipLaunchKernelGGL((sim::k_sim<1, 1, 4, 5>), grid, block, lds, hs, a);
+    else if (a.g.L <= 64 && four) hipLaunchKernelGGL((sim::k_sim<1, 1, 4, NMAX>), grid, block, lds, hs, a);
+    else if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 1, 3, NMAX>), grid, block, lds, hs, a);
+    else hipLaunchKernelGGL((sim::k_sim<2, 1, 3, NMAX>), grid, block, lds, hs, a);
   } else {
-    if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 4, 2>), grid, block, lds, hs, a);
-    else hipLaunchKernelGGL((sim::k_sim<2, 4, 2>), grid, block, lds, hs, a);
+    if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 4, 2, NMAX>), grid, block, lds, hs, a);
+    else hipLaunchKernelGGL((sim::k_sim<2, 4, 2, NMAX>), grid, block, lds, hs, a);
   }
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
