@@ -1529,7 +1529,10 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   // table sizes: small by default (LDS decides how many instances share a CU);
   // fx_sim_run_tiered reruns the instances that outgrow them with 256 dots
   const uint32_t cpr = (C + n - 1) / n;  // clients per process region
-  g.W = wslots ? wslots : std::min<uint32_t>(64u, 8u * C);  // live dots per instance
+  // live dots per instance: 8 per client, at most 64; 32 for n > 5 with one
+  // client per region (configs[2]'s n = 7: 12.4 KB instead of 15.4 KB, 13
+  // instances per CU instead of 10, the same reruns; 24 reran more, 16 lost 4x)
+  g.W = wslots ? wslots : (n > 5 && C <= 8 ? 32u : std::min<uint32_t>(64u, 8u * C));
   if (g.W > 256u) return false;
   g.R = ring ? ring : std::min<uint32_t>(4096u, 16u * n * cpr);  // messages in flight per instance
   if (g.R > 65534u) return false;
@@ -1589,7 +1592,7 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   int dc = 0;
   if (hipGetDeviceCount(&dc) != hipSuccess || dc <= 0) return FX_ERR_NO_DEVICE;
   const uint32_t ring = b->ring_entries;  // 0 = min(4096, 64 n)
-  const uint32_t W = b->dot_slots;  // 0 = min(64, 8 n)
+  const uint32_t W = b->dot_slots;  // 0 = the default of sim_geometry
   if (ring > 65534 || W > 256) return FX_ERR_INVALID_ARG;
   const fx_sim_spec& s0 = b->host_specs[0];
   // every instance of a launch shares the geometry (protocol, n, clients, keys)
