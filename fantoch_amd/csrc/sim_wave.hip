@@ -1534,7 +1534,11 @@ static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, 
   // instances per CU instead of 10, the same reruns; 24 reran more, 16 lost 4x)
   g.W = wslots ? wslots : (n > 5 && C <= 8 ? 32u : std::min<uint32_t>(64u, 8u * C));
   if (g.W > 256u) return false;
-  g.R = ring ? ring : std::min<uint32_t>(4096u, 16u * n * cpr);  // messages in flight per instance
+  // messages in flight per instance: 16 per process and client; at least 192
+  // for n > 5, where a lagging far replica overflowed the smaller pool often
+  // enough (reruns at 4x) that the larger table wins despite fewer instances
+  // per CU (configs[2] sweep)
+  g.R = ring ? ring : std::min<uint32_t>(4096u, std::max<uint32_t>(16u * n * cpr, n > 5 ? 192u : 0u));
   if (g.R > 65534u) return false;
   g.NP = n * (n - 1);
   g.L = g.NP + n + 2 * C;
