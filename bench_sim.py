@@ -112,6 +112,7 @@ def main_sim(args):
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     kernel_ms = []
+    reruns = ctypes.c_uint32()  # instances rerun at larger tables (FX_ERR_SIM_CAPACITY) in the last step
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -121,7 +122,8 @@ def main_sim(args):
         chain.zero_()
         delay.zero_()
         ev0.record(stream)
-        _lib.check(lib.fx_sim_run_tiered(ctypes.byref(batch), ctypes.byref(out), hs, None), "fx_sim_run_tiered")
+        _lib.check(lib.fx_sim_run_tiered(ctypes.byref(batch), ctypes.byref(out), hs, ctypes.byref(reruns)),
+                   "fx_sim_run_tiered")
         ev1.record(stream)
         if world > 1:  # the step's output: histograms summed over every rank's instances (RCCL)
             for h in (lat_hist, chain, delay):
@@ -235,6 +237,7 @@ def main_sim(args):
             "executed_per_step": int(executed_all),
             "client_cmds_per_s": round(client_all * args.steps / elapsed, 1),
             "sim_events_per_s": round(events_all * args.steps / elapsed, 1),
+            "reruns_at_larger_tables_rank0": int(reruns.value),
             # graph edges = deps of every executor Add, per second
             "edges_per_s": round(deps_all * args.steps / elapsed, 1),
             "fast_paths": fast_all, "slow_paths": slow_all,
