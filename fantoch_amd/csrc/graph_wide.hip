@@ -220,8 +220,18 @@ struct W {
       if (ci < cnd) {
         const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)drow, (int)ci);
         ++ci;
-        if (d == cdot || contains(d)) continue;  // self or executed (tarjan.rs:128-145)
-        const uint32_t w = find(d);
+        // the clock-window word and the index word both depend on d alone:
+        // read them together (one LDS round trip), then decide
+        const uint32_t src = FX_DOT_SRC(d), sq = FX_DOT_SEQ(d);
+        const bool inr = src >= 1 && src <= L.n;
+        const uint32_t si = inr ? src - 1 : 0u;
+        const uint32_t bb = sq & (L.WB * 32u - 1u);
+        const uint32_t hw = rd(L.hidx, si * L.Q + (sq & (L.Q - 1u)));
+        const uint32_t bw = rd(L.bits, si * L.WB + (bb >> 5));
+        const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)frv, (int)si);
+        const bool executed = inr && (sq <= f || (sq - f - 1u < L.WB * 32u && ((bw >> (bb & 31u)) & 1u)));
+        if (d == cdot || executed) continue;  // self or executed (tarjan.rs:128-145)
+        const uint32_t w = (inr && (hw & 0xFFFFu) != 0 && (hw & 0xFFFF0000u) == htag(d)) ? (hw & 0xFFFFu) - 1u : NONE;
         if (w == NONE) {
           if (collect) {  // partial replication, first search (tarjan.rs:158-166)
             bool seen = false;
