@@ -205,9 +205,31 @@ def test_sim_plan_sizes():
     assert lib.fx_sim_plan(ctypes.byref(s), 32, 8, ctypes.byref(b)) == 0
     small = b.value
     assert 4 * 1024 < small < 64 * 1024
-    # default pools (0 = 64 n messages, 8 n dots) need more LDS than 32 / 8
+    # default pools (0 = 16 n messages per client region, min(64, 8 C) dots) need more LDS than 32 / 8
     assert lib.fx_sim_plan(ctypes.byref(s), 0, 0, ctypes.byref(b)) == 0
     assert small < b.value < 64 * 1024
     assert lib.fx_sim_plan(ctypes.byref(s), 0, 257, ctypes.byref(b)) == _lib.FX_ERR_UNSUPPORTED
     s9 = S.spec(S.EPAXOS, 5, 2, regs, regs, clients_per_region=40)  # 200 clients: too many links
     assert lib.fx_sim_plan(ctypes.byref(s9), 32, 8, ctypes.byref(b)) == _lib.FX_ERR_UNSUPPORTED
+
+
+def test_sim_default_geometry_occupancy():
+    """The default tables keep the benchmarked geometries at their measured
+    occupancy: configs[1] (EPaxos n = 5, one client per region) fits 16
+    instances per CU (the 4-wave kernel, <= 10,240 B of LDS), configs[2]'s n = 7
+    Atlas placements use 32 live dots and >= 192 messages (13 per CU -> 11)."""
+    from fantoch_amd import sim as S
+    import ctypes
+    pl = S.Planet()
+    lib = _lib.load()
+    b = ctypes.c_uint32()
+    r5 = pl.ids(S.GCP5[:5])
+    s5 = S.spec(S.EPAXOS, 5, 2, r5, r5, commands_per_client=1000)
+    assert lib.fx_sim_plan(ctypes.byref(s5), 0, 0, ctypes.byref(b)) == 0
+    assert b.value <= 160 * 1024 // 16, b.value
+    r7 = pl.ids(sorted(pl.names)[:7]) if hasattr(pl, "names") else pl.ids(S.GCP5[:5] + ["us-east1", "us-west1"])
+    s7 = S.spec(S.ATLAS, 7, 1, r7, r7, commands_per_client=100)
+    assert lib.fx_sim_plan(ctypes.byref(s7), 0, 0, ctypes.byref(b)) == 0
+    d7 = b.value
+    assert lib.fx_sim_plan(ctypes.byref(s7), 192, 32, ctypes.byref(b)) == 0
+    assert d7 == b.value and 160 * 1024 // d7 == 11, d7
