@@ -101,6 +101,29 @@ struct WaveMax {
   __device__ __forceinline__ void flush(uint32_t* out) const {
     if (s != 0xFFFFFFFFu && (threadIdx.x & 63u) == 0) atomicMax(&out[s], m);
   }
+  // the block's waves usually end on the same stream: combine them in LDS
+  // first, so a block issues one atomic per distinct stream, not one per wave
+  __device__ __forceinline__ void flush_block(uint32_t* out) const {
+    __shared__ uint32_t bs[BT / 64], bm[BT / 64];
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) {
+      bs[w] = s;
+      bm[w] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (uint32_t i = 0; i < BT / 64; ++i) {
+        if (bs[i] == 0xFFFFFFFFu) continue;
+        uint32_t mx = bm[i];
+        bool first = true;
+        for (uint32_t j = 0; j < i; ++j) first = first && bs[j] != bs[i];
+        if (!first) continue;
+        for (uint32_t j = i + 1; j < BT / 64; ++j)
+          if (bs[j] == bs[i]) mx = max(mx, bm[j]);
+        atomicMax(&out[bs[i]], mx);
+      }
+    }
+  }
 };
 
 __global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad) {
@@ -121,7 +144,7 @@ __global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad) {
     }
     acc.add(maxseq, s, sq);
   }
-  acc.flush(maxseq);
+  acc.flush_block(maxseq);
 }
 
 __global__ void k_pos(In in, const uint64_t* base, const uint32_t* maxseq, uint32_t* pos, uint32_t* bad) {
@@ -276,7 +299,7 @@ __global__ void k_seglen(uint64_t nseg, const uint64_t* segbase, const uint32_t*
     }
     acc.add(smax, s, len);
   }
-  acc.flush(smax);
+  acc.flush_block(smax);
 }
 
 struct Seg {
