@@ -12,7 +12,7 @@ CPPTEST := tests/cpp/build/test_graph_executor
 
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
             -Iinclude -Ifantoch_amd/csrc -mllvm -simplifycfg-sink-common=false
-SRCS := fantoch_amd/csrc/graph_exec.hip fantoch_amd/csrc/graph_group.hip fantoch_amd/csrc/graph_wave.hip fantoch_amd/csrc/graph_lane.hip fantoch_amd/csrc/graph_split.hip fantoch_amd/csrc/graph_cut.hip fantoch_amd/csrc/graph_wide.hip fantoch_amd/csrc/pred_exec.hip fantoch_amd/csrc/executor_host.cpp fantoch_amd/csrc/exec_log.cpp fantoch_amd/csrc/config.cpp fantoch_amd/csrc/planet.cpp fantoch_amd/csrc/sim_wave.hip
+SRCS := fantoch_amd/csrc/graph_exec.hip fantoch_amd/csrc/graph_group.hip fantoch_amd/csrc/graph_wave.hip fantoch_amd/csrc/graph_lane.hip fantoch_amd/csrc/graph_split.hip fantoch_amd/csrc/graph_cut.hip fantoch_amd/csrc/graph_wide.hip fantoch_amd/csrc/pred_exec.hip fantoch_amd/csrc/executor_host.cpp fantoch_amd/csrc/exec_log.cpp fantoch_amd/csrc/config.cpp fantoch_amd/csrc/planet.cpp fantoch_amd/csrc/sim_wave.hip fantoch_amd/csrc/sim_big.hip
 HDRS := include/fantoch_amd.h include/fantoch_amd.hpp fantoch_amd/csrc/fx_synth.h fantoch_amd/csrc/fx_internal.h
 
 all: $(LIB) $(ORACLE) $(CPPTEST)

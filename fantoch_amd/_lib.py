@@ -33,12 +33,14 @@ FX_PROTOCOL_ATLAS = 0
 FX_PROTOCOL_EPAXOS = 1
 FX_PROTOCOL_BASIC = 2
 FX_SIM_FLAG_EXEC_NOTIFICATIONS = 1
+FX_SIM_FLAG_LARGE = 2
 FX_SIM_STAT_FAST, FX_SIM_STAT_SLOW, FX_SIM_STAT_STABLE = 0, 8, 16
 FX_SIM_STAT_EVENTS, FX_SIM_STAT_END_MS, FX_SIM_STAT_TRACE, FX_SIM_STAT_SEQ = 24, 25, 26, 27
 FX_SIM_STAT_DEPS = 28
 FX_SIM_STAT_LAT_SUM = 29
 FX_SIM_STAT_ERR_SITE = 30
-FX_SIM_STATS = 32
+FX_SIM_STAT_FAST_READS, FX_SIM_STAT_SLOW_READS = 32, 40
+FX_SIM_STATS = 48
 
 FX_SEQ_BITS = 24
 FX_SEQ_MASK = (1 << 24) - 1
@@ -188,7 +190,8 @@ class SimOutput(ctypes.Structure):
                 ("chain_hist", ctypes.c_void_p), ("delay_hist", ctypes.c_void_p),
                 ("stats", ctypes.c_void_p), ("err", ctypes.c_void_p),
                 ("lat_bins", ctypes.c_uint32), ("chain_bins", ctypes.c_uint32),
-                ("delay_bins", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("delay_bins", ctypes.c_uint32), ("pad", ctypes.c_uint32),
+                ("dot_client", ctypes.c_void_p)]
 
 
 # (name, restype, argtypes) of every symbol declared in include/fantoch_amd.h
@@ -269,6 +272,8 @@ SIGNATURES = [
     ("fx_graph_executor_transfer_stats", ctypes.c_int, [ctypes.c_void_p, u64p, u64p]),
     ("fx_sim_plan", ctypes.c_int,
      [ctypes.POINTER(SimSpec), ctypes.c_uint32, ctypes.c_uint32, u32p]),
+    ("fx_sim_plan_large", ctypes.c_int,
+     [ctypes.POINTER(SimSpec), ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
     ("fx_sim_run", ctypes.c_int,
      [ctypes.POINTER(SimBatch), ctypes.POINTER(SimOutput), ctypes.c_void_p]),
     ("fx_sim_run_tiered", ctypes.c_int,

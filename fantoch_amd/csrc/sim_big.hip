@@ -1,0 +1,1439 @@
+// sim_big.hip — the batched simulator for the instances the all-on-chip
+// kernel (sim_wave.hip) cannot hold: many clients per instance (BASELINE
+// configs[3]: 64 clients per region, 320 per instance at n = 5, hundreds of
+// commands pending at every executor), message reordering
+// (Runner::reorder_messages, runner.rs:519-524), NFR (keys/mod.rs:44-75,
+// maybe_adjust_fast_quorum) and read-only commands (workload.rs:158-160) —
+// the shapes of the reference's own protocol simulations (protocol/mod.rs:
+// 702-768 sim_test: 10 clients per process, reordering, GC every 100 ms).
+//
+// Still ONE wavefront per simulated instance, wave-uniform control flow; the
+// per-instance state moves from LDS to an HBM arena (about 1 MB at configs[3]),
+// so many instances per CU hide the memory latency:
+//   dot table   one slot per live dot, direct-mapped per source (seq mod Q):
+//               the command (client, keys, read-only), the protocol state
+//               shared by its messages (collect deps, every MCollectAck's deps,
+//               the committed value, quorum, participants / accepts / commit /
+//               execution counts) and, per process, an 8-word record: protocol
+//               status byte, and the GraphExecutor's vertex (start time, the
+//               dot it waits on, Tarjan id / low, on-stack + visited epoch, its
+//               links in the waiter list of the dot it waits on, the head of
+//               its own waiter list).  A slot is freed once every process
+//               executed its dot; a dep whose slot no longer holds it is
+//               therefore executed everywhere (the AEClock test of tarjan.rs:
+//               128-145 needs no clock).
+//   events      every scheduled action (messages, client submits and replies,
+//               the periodic GC and executed-notification events, the
+//               MGarbageCollection deliveries) is a pool entry keyed
+//               (time, class, seq) — the oracle's Schedule order (C3) — and the
+//               next action is found by a two-level 64-ary min tree: the group
+//               minima live in lanes (lane g = group g), the leaves in HBM.
+//               Per pop: one DPP min over the group minima, one coalesced
+//               64-leaf read and a DPP min over it.  With reordering the links
+//               are no longer FIFO, so the per-link merge of sim_wave.hip does
+//               not apply; the tree is exact for any delays.
+//   GC          simulated, not evaluated: with reordering the MGarbageCollection
+//               delays are random draws of the shared reorder stream (runner.rs:
+//               519-524), so sim_wave.hip's closed-form Stable count does not
+//               hold.  The committed frontier per (process, source) lives in
+//               lane 8 p + s and advances over the dot table.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "fantoch_amd.h"
+#include "fx_internal.h"
+
+namespace fx {
+namespace simx {
+
+constexpr uint32_t NMAX = FX_SIM_MAX_N;
+constexpr uint32_t KMAX = 2;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t FMAX = 12;       // handler frame stack depth
+constexpr uint32_t HC_BINS = 64;    // ChainSize bins counted per instance in LDS
+constexpr uint32_t HD_BINS = 256;   // ExecutionDelay bins counted per instance in LDS
+constexpr uint32_t HL_LOG = 6, HL_SLOTS = 1u << HL_LOG;  // client-latency cache
+constexpr uint32_t TIME_LIMIT = 1u << 24;  // ms; the event key holds time << 8
+constexpr uint32_t LDS_WORDS = HC_BINS + HD_BINS + 2 * HL_SLOTS;
+
+// event kinds (protocol kinds numbered as the oracle's trace, sim_oracle.cpp MK)
+enum : uint32_t {
+  M_COLLECT = 0, M_COLLECT_ACK = 1, M_COMMIT = 2, M_CONSENSUS = 3, M_CONSENSUS_ACK = 4,
+  M_GC = 6,        // MGarbageCollection delivery (payload: the sender's committed frontier)
+  M_SUBMIT = 8,    // SubmitToProc
+  E_CLIENT = 9,    // SendToClient
+  E_TICK = 10,     // PeriodicProcessEvent (GarbageCollection)
+  E_NOTIF = 11     // PeriodicExecutedNotification
+};
+enum : uint32_t { ST_START = 0, ST_PAYLOAD = 1, ST_COLLECT = 2, ST_COMMIT = 3 };
+// per-process record word R_PST: status (2) | buffered commit | accepted |
+// buffered-commit sender (4) | in the executor's graph | executed
+constexpr uint32_t PS_BUF = 4u, PS_ACC = 8u, PS_INGRAPH = 1u << 8, PS_EXEC = 1u << 9;
+// dot-slot words (then collect deps [2K] | value [vmax] | ack deps [n][amax])
+enum : uint32_t { SL_DOT = 0, SL_CLIENT = 1, SL_IDX = 2, SL_KEYS = 3, SL_CNT = 4, SL_MASKS = 5,
+                  SL_QUORUM = 6, SL_COLLECT = 8 };
+// SL_CNT:    collect count (8) | value count (8) << 8 | nkeys (2) << 16 | read-only << 18 |
+//            proposer ballot set << 19
+// SL_MASKS:  participants (8) | proposer accepts (8) << 8 | committed (8) << 16 | executed (8) << 24
+// SL_QUORUM: the MCollect's quorum mask (8) | its size << 8
+// per-(slot, process) record words
+enum : uint32_t { R_PST = 0, R_START = 1, R_WAIT = 2, R_TL = 3, R_MARK = 4, R_NEXT = 5, R_PREV = 6,
+                  R_HEAD = 7 };
+// R_TL:   Tarjan id (16) | low (16) << 16
+// R_MARK: on the Tarjan stack | visited epoch << 1 (try_pending's skip rule)
+// R_WAIT / R_NEXT / R_PREV / R_HEAD: slot + 1 (0 = none) — the PendingIndex
+//         entry of a waited-on dot is a doubly linked list through its waiters
+
+struct GeoX {  // launch-uniform geometry (words)
+  uint32_t n, C, K, Q, qlog, NS, R, ncli_keys;
+  uint32_t amax, vmax, sl_value, sl_ack, SW;
+  uint32_t o_slot, o_rec, o_kd, o_cl, o_kh, o_kl, o_inf, o_arg, o_gp, o_free, o_gco, o_tstk, o_fv, o_fi, o_wl,
+      o_tmp, o_tl, o_tw, o_rdy;
+  uint32_t words;  // per instance
+};
+
+struct ArgsX {
+  const fx_sim_spec* specs;
+  uint32_t instances;
+  GeoX g;
+  uint32_t* arena;
+  const uint16_t* ping;
+  const uint8_t* rank;
+  uint32_t RP;
+  uint32_t exec_cap, lat_cap, max_events, sim_exec_notif;
+  uint32_t* executed;
+  uint32_t* executed_len;
+  uint32_t* latency_log;
+  uint32_t* dot_client;
+  unsigned long long* lat_hist;
+  uint32_t lat_bins;
+  unsigned long long* chain_hist;
+  uint32_t chain_bins;
+  unsigned long long* delay_hist;
+  uint32_t delay_bins;
+  unsigned long long* stats;
+  uint32_t* err;
+};
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)src);
+}
+__device__ __forceinline__ uint32_t gather(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+__device__ __forceinline__ uint64_t bal(bool p) { return (uint64_t)__ballot(p); }
+__device__ __forceinline__ uint32_t ctz64(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
+__device__ __forceinline__ uint32_t pop64(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
+__device__ __forceinline__ uint32_t pop32(uint32_t m) { return (uint32_t)__builtin_popcount(m); }
+
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finalizer (C6)
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ uint64_t sim_rand(uint64_t seed, uint64_t inst, uint64_t client, uint64_t idx,
+                                             uint64_t purpose) {
+  return mix64(mix64(mix64(mix64(seed ^ 0x5851F42D4C957F2Dull) + inst) + client) + ((idx << 8) | purpose));
+}
+enum : uint64_t { R_CONFLICT = 1, R_POOL = 2, R_READ_ONLY = 3, R_REORDER = 4 };
+
+// inclusive min-scan over the wavefront (row_shr 1/2/4/8, row_bcast 15/31);
+// every lane gets the minimum
+__device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x111, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x112, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x114, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x118, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x142, 0xA, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)NONE, (int)v, 0x143, 0xC, 0xF, false));
+  return rl(v, 63);
+}
+
+enum : uint32_t { FOUND = 0, MISSING = 1 };
+
+// NG: registers of group minima per lane (message pool <= 4096 NG entries)
+template <uint32_t NG>
+struct Big {
+  // ---------------------------------------------------------------- context
+  uint32_t lid;
+  ArgsX A;
+  GeoX g;
+  uint32_t* M;    // this instance's arena
+  uint32_t* lds;  // histogram caches
+  uint32_t inst;
+  uint64_t seed, rng_inst;
+  uint32_t protocol, n, f, synod_f, gc_ms, en_ms, cmds, conflict_, pool, extra, ro_pct;
+  bool has_extra, reorder, nfr;
+  uint32_t C, K;
+  uint32_t err = 0, err_site = 0;
+  __device__ __forceinline__ void fail_cap(uint32_t line) {
+    if (!err) err_site = line;
+    err = FX_ERR_SIM_CAPACITY;
+  }
+  uint32_t now = 0;  // ms
+  uint32_t seq = 0;  // insertion counter (C3)
+  uint64_t rdraws = 0;
+  uint64_t events = 0, trace = 0, deps_total = 0, lat_sum = 0;
+  uint32_t clients_done = 0;
+  bool done = false, in_extra = false;
+  uint32_t final_ms = 0;
+
+  // event pool: minimum (key hi, key lo) of group 64 k + lane in gh[k], gl[k]
+  uint32_t gh[NG], gl[NG];
+  uint32_t nfree = 0;
+  // lane p: proposal seq, Fast / Slow (and their read-only shares), executed
+  // count, Stable, quorums (fast | write << 8 | majority << 16), GC reporters
+  uint32_t pseq = 0, pfast = 0, pslow = 0, pfr = 0, psr = 0, pexec = 0, pstab = 0, pq = 0, prep = 0;
+  // lane 8 p + s: p's committed frontier of source s + 1 (GC track), its
+  // previous stable frontier, and the link delay p -> s
+  uint32_t gcf = 0, gps = 0, dpq = 0;
+  // handler frames, frame fi in lane fi: action (0 none, 1 ToSend) | kind << 2 |
+  // targets << 8 | next target << 16; dot; base of its ready results
+  uint32_t frw = 0, frd = 0, frb = 0;
+  uint32_t nfrm = 0, xinfo = NONE, rtop = 0;
+  // executor (the process being run)
+  uint32_t xp = 0, xk = 0, epoch = 0, nwl = 0, idc = 0, tsp = 0, fsp = 0;
+
+  // ------------------------------------------------------------ arena views
+  __device__ __forceinline__ uint32_t& S(uint32_t sl, uint32_t w) { return M[g.o_slot + sl * g.SW + w]; }
+  __device__ __forceinline__ uint32_t& RC(uint32_t sl, uint32_t p, uint32_t w) {
+    return M[g.o_rec + (sl * g.n + p) * 8u + w];
+  }
+  __device__ __forceinline__ uint32_t& CL(uint32_t c, uint32_t w) { return M[g.o_cl + c * 8u + w]; }
+  __device__ __forceinline__ uint32_t& KD(uint32_t p, uint32_t key, uint32_t w) {
+    return M[g.o_kd + (p * g.ncli_keys + key) * 2u + w];
+  }
+  __device__ __forceinline__ uint32_t& W(uint32_t off, uint32_t i) { return M[off + i]; }
+  __device__ __forceinline__ uint32_t rd(uint32_t& x) { return uni(x); }
+  __device__ __forceinline__ void put(uint32_t& dst, uint32_t v) {
+    if (lid == 0) dst = v;
+  }
+  __device__ __forceinline__ void lset(uint32_t& reg, uint32_t lane, uint32_t v) {
+    if (lid == lane) reg = v;
+  }
+  // dot table slot of a dot (direct-mapped per source)
+  __device__ __forceinline__ uint32_t hslot(uint32_t d) const {
+    return ((FX_DOT_SRC(d) - 1u) << g.qlog) | (FX_DOT_SEQ(d) & (g.Q - 1u));
+  }
+  __device__ __forceinline__ bool src_ok(uint32_t d) const {
+    const uint32_t s = FX_DOT_SRC(d);
+    return s >= 1u && s <= n;
+  }
+  // slot of a live dot, NONE if its slot no longer holds it
+  __device__ __forceinline__ uint32_t slot_of(uint32_t d) {
+    if (!src_ok(d)) return NONE;
+    const uint32_t sl = hslot(d);
+    return rd(S(sl, SL_DOT)) == d ? sl : NONE;
+  }
+
+  // ------------------------------------------------------------- histograms
+  __device__ __forceinline__ void hist_chain(uint32_t v) {
+    if (!A.chain_hist) return;
+    const uint32_t b = min(v, A.chain_bins - 1u);
+    if (lid == 0) {
+      if (b < HC_BINS) atomicAdd(&lds[b], 1u);
+      else atomicAdd(&A.chain_hist[b], 1ull);
+    }
+  }
+  __device__ __forceinline__ void hist_delay(uint32_t v) {
+    if (!A.delay_hist) return;
+    const uint32_t b = min(v, A.delay_bins - 1u);
+    if (lid == 0) {
+      if (b < HD_BINS) atomicAdd(&lds[HC_BINS + b], 1u);
+      else atomicAdd(&A.delay_hist[b], 1ull);
+    }
+  }
+  __device__ __forceinline__ void hist_lat(uint32_t region, uint32_t lat) {
+    if (!A.lat_hist) return;
+    const uint32_t key = region * A.lat_bins + min(lat, A.lat_bins - 1u);
+    const uint32_t h = (key * 2654435761u) >> (32 - HL_LOG);
+    uint32_t* lc = lds + HC_BINS + HD_BINS;
+    const uint32_t k = uni(lc[h]);
+    if (lid == 0) {
+      if (k == key + 1u) {
+        atomicAdd(&lc[HL_SLOTS + h], 1u);
+      } else if (k == 0) {
+        lc[h] = key + 1u;
+        lc[HL_SLOTS + h] = 1u;
+      } else {
+        atomicAdd(&A.lat_hist[key], 1ull);
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------ trace
+  __device__ __forceinline__ void note(uint64_t kind, uint64_t a, uint64_t b, uint64_t c) {
+    ++events;
+    trace = mix64(trace ^ ((uint64_t)now << 24) ^ (kind << 20) ^ (a << 12) ^ (b << 4)) + c;
+  }
+
+  // ----------------------------------------------------------------- events
+  // key hi = time << 8 | class << 6 | a << 3 | b (class 0 protocol / client /
+  // executed notification; 1 the GC event of process a; 2 the GC delivery
+  // a -> b), key lo = insertion seq: the oracle's (time, class, seq) order
+  __device__ __forceinline__ uint32_t push_event(uint32_t t, uint32_t cls, uint32_t info, uint32_t arg) {
+    if (t >= TIME_LIMIT) {
+      err = FX_ERR_TIME_RANGE;
+      return NONE;
+    }
+    if (nfree == 0) {
+      fail_cap(__LINE__);
+      return NONE;
+    }
+    const uint32_t e = rd(W(g.o_free, --nfree));
+    const uint32_t hi = (t << 8) | cls, lo = seq++;
+    put(W(g.o_kh, e), hi);
+    put(W(g.o_kl, e), lo);
+    put(W(g.o_inf, e), info);
+    put(W(g.o_arg, e), arg);
+    const uint32_t grp = e >> 6;
+    if (lid == (grp & 63u)) {
+#pragma unroll
+      for (uint32_t k = 0; k < NG; ++k)
+        if ((grp >> 6) == k && (hi < gh[k] || (hi == gh[k] && lo < gl[k]))) {
+          gh[k] = hi;
+          gl[k] = lo;
+        }
+    }
+    return e;
+  }
+  // removes the minimum event; returns its entry (NONE if the queue is empty)
+  __device__ __forceinline__ uint32_t pop_event(uint32_t& hi_out) {
+    uint32_t bh = gh[0], bl = gl[0], bk = 0;
+#pragma unroll
+    for (uint32_t k = 1; k < NG; ++k) {
+      const bool lt = gh[k] < bh || (gh[k] == bh && gl[k] < bl);
+      bh = lt ? gh[k] : bh;
+      bl = lt ? gl[k] : bl;
+      bk = lt ? k : bk;
+    }
+    const uint32_t th = dpp_min(bh);
+    hi_out = th;
+    if (th == NONE) return NONE;
+    const uint32_t tl = dpp_min(bh == th ? bl : NONE);
+    const uint32_t ln = ctz64(bal(bh == th && bl == tl));
+    const uint32_t grp = rl(bk, ln) * 64u + ln;
+    const uint32_t e0 = grp * 64u + lid;
+    uint32_t kh = W(g.o_kh, e0), kl = W(g.o_kl, e0);
+    const uint32_t j = ctz64(bal(kh == th && kl == tl));
+    if (lid == j) {
+      kh = NONE;
+      kl = NONE;
+      W(g.o_kh, e0) = NONE;
+    }
+    const uint32_t nh = dpp_min(kh);
+    const uint32_t nl = dpp_min(kh == nh ? kl : NONE);
+    if (lid == (grp & 63u)) {
+#pragma unroll
+      for (uint32_t k = 0; k < NG; ++k)
+        if ((grp >> 6) == k) {
+          gh[k] = nh;
+          gl[k] = nl;
+        }
+    }
+    return grp * 64u + j;
+  }
+  __device__ __forceinline__ void free_event(uint32_t e) { put(W(g.o_free, nfree++), e); }
+
+  // Runner::schedule_message (runner.rs:507-530): distance, times the C6
+  // multiplier in [0, 10) when reordering (one draw per message, in schedule order)
+  __device__ __forceinline__ uint32_t msg_delay(uint32_t d) {
+    if (!reorder) return d;
+    const uint64_t u = sim_rand(seed, rng_inst, 0, rdraws++, R_REORDER);
+    const double mult = (double)(u >> 11) * (1.0 / 9007199254740992.0) * 10.0;
+    return (uint32_t)(uint64_t)((double)d * mult);
+  }
+
+  // ------------------------------------------------------------ workload
+  // Workload::gen_cmd (workload.rs:142-197) of command idx of client cid
+  // (1-based), canonical C6/C7/C11: keys packed key0 | key1 << 16
+  __device__ __forceinline__ uint32_t gen_keys(uint32_t cid, uint32_t idx, uint32_t& nk) {
+    uint32_t k0 = 0xFFFFu, k1 = 0xFFFFu;
+    nk = 0;
+    for (uint32_t draw = 0; nk < K && draw < 65536u; ++draw) {  // gen_unique_keys draws until distinct
+      bool conflict;
+      if (conflict_ == 0) conflict = false;
+      else if (conflict_ >= 100) conflict = true;
+      else conflict = sim_rand(seed, rng_inst, cid, (uint64_t)idx * 64 + draw, R_CONFLICT) % 100ull < conflict_;
+      uint32_t key;
+      if (conflict)
+        key = pool <= 1 ? 0u : (uint32_t)(sim_rand(seed, rng_inst, cid, (uint64_t)idx * 64 + draw, R_POOL) % pool);
+      else
+        key = pool + cid;
+      if (nk == 0) {
+        k0 = key;
+        nk = 1;
+      } else if (key != k0) {
+        k1 = key;
+        nk = 2;
+      }
+    }
+    if (nk != K) fail_cap(__LINE__);
+    if (nk == 2 && k1 < k0) {  // C11
+      const uint32_t t = k0;
+      k0 = k1;
+      k1 = t;
+    }
+    return k0 | (k1 << 16);
+  }
+  __device__ __forceinline__ bool gen_read_only(uint32_t cid, uint32_t idx) {  // workload.rs:158-160
+    if (ro_pct == 0) return false;
+    if (ro_pct >= 100) return true;
+    return sim_rand(seed, rng_inst, cid, idx, R_READ_ONLY) % 100ull < ro_pct;
+  }
+
+  // ------------------------------------------------------- frame stack
+  __device__ __forceinline__ void act_send(uint32_t kind, uint32_t dot, uint32_t tgt) {
+    const uint32_t fi = nfrm - 1;
+    lset(frw, fi, 1u | (kind << 2) | (tgt << 8));
+    lset(frd, fi, dot);
+  }
+
+  // ============================================================ protocol
+  // SequentialKeyDeps::add_cmd (sequential.rs:74-118, keys/mod.rs:44-75): the
+  // latest write per key, and the latest read unless the command is read-only
+  // or NFR is on; `past` merged; returns the sorted distinct deps in lanes
+  // [0, cnt) of outv
+  __device__ __forceinline__ uint32_t add_cmd(uint32_t p, uint32_t dot, uint32_t keys, uint32_t nk, bool ro,
+                                              uint32_t pastv, uint32_t npast, uint32_t& outv) {
+    const uint32_t key0 = keys & 0xFFFFu, key1 = keys >> 16;
+    const uint32_t w0 = rd(KD(p, key0, 0)), r0 = rd(KD(p, key0, 1));
+    put(KD(p, key0, ro ? 1u : 0u), dot);
+    uint32_t w1 = 0, r1 = 0;
+    if (nk > 1) {
+      w1 = rd(KD(p, key1, 0));
+      r1 = rd(KD(p, key1, 1));
+      put(KD(p, key1, ro ? 1u : 0u), dot);
+    }
+    const bool reads = !ro && !nfr;
+    const uint32_t i = lid - npast;
+    uint32_t v = 0;
+    if (lid < npast) v = pastv;
+    else if (i == 0) v = w0;
+    else if (i == 1) v = reads ? r0 : 0u;
+    else if (i == 2) v = w1;
+    else if (i == 3) v = reads ? r1 : 0u;
+    const bool valid = v != 0;
+    bool first = valid;
+    const uint64_t vm = bal(valid);
+    for (uint64_t m = vm; m; m &= m - 1) {
+      const uint32_t j = ctz64(m);
+      if (j < lid && rl(v, j) == v) first = false;
+    }
+    const uint64_t fm = bal(first);
+    uint32_t rank = 0;
+    for (uint64_t m = fm; m; m &= m - 1) rank += rl(v, ctz64(m)) < v ? 1u : 0u;
+    outv = 0;
+    for (uint64_t m = fm; m; m &= m - 1) {
+      const uint32_t j = ctz64(m);
+      const uint32_t vj = rl(v, j), rj = rl(rank, j);
+      if (lid == rj) outv = vj;
+    }
+    return pop64(fm);
+  }
+
+  // Protocol::submit (atlas.rs:210-249, epaxos.rs:199-221)
+  __device__ __forceinline__ void h_submit(uint32_t p, uint32_t c) {
+    const uint32_t s = rl(pseq, p) + 1u;
+    lset(pseq, p, s);
+    if (s > FX_SEQ_MASK) {
+      err = FX_ERR_DOT_RANGE;
+      return;
+    }
+    const uint32_t dot = FX_PACK_DOT(p + 1, s);
+    const uint32_t sl = hslot(dot);
+    if (rd(S(sl, SL_DOT)) != 0) {  // the dot Q seqs back is still live
+      fail_cap(__LINE__);
+      return;
+    }
+    const uint32_t idx = rd(CL(c, 1)) - 1u;
+    uint32_t nk = 0;
+    const uint32_t keys = gen_keys(c + 1, idx, nk);
+    const bool ro = gen_read_only(c + 1, idx);
+    uint32_t depv = 0;
+    const uint32_t nd = add_cmd(p, dot, keys, nk, ro, 0, 0, depv);
+    // maybe_adjust_fast_quorum: a single-key read under NFR goes to a majority
+    const uint32_t qw = rl(pq, p);
+    const uint32_t qm = (nfr && ro && nk == 1) ? (qw >> 16) & 0xFFu : qw & 0xFFu;
+    // the fresh slot in one lane-parallel pass, and its per-process records
+    const uint32_t dv = gather(depv, (lid - SL_COLLECT) & 63u);
+    for (uint32_t i = lid; i < g.SW; i += 64) {
+      uint32_t v = 0;
+      if (i == SL_DOT) v = dot;
+      else if (i == SL_CLIENT) v = c;
+      else if (i == SL_IDX) v = idx;
+      else if (i == SL_KEYS) v = keys;
+      else if (i == SL_CNT) v = nd | (nk << 16) | (ro ? 1u << 18 : 0u);
+      else if (i == SL_QUORUM) v = qm | (pop32(qm) << 8);
+      else if (i >= SL_COLLECT && i < SL_COLLECT + nd) v = dv;
+      S(sl, i) = v;
+    }
+    for (uint32_t i = lid; i < g.n * 8u; i += 64) M[g.o_rec + sl * g.n * 8u + i] = 0;
+    if (A.dot_client && s <= A.exec_cap && lid == 0)
+      A.dot_client[((size_t)inst * n + p) * A.exec_cap + s - 1u] = c + 1u;
+    act_send(M_COLLECT, dot, (1u << n) - 1u);
+  }
+
+  // atlas.rs:251-325 / epaxos.rs:223-301
+  __device__ __forceinline__ void h_mcollect(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (sl == NONE) {
+      err = FX_ERR_SIM_LATE;
+      return;
+    }
+    const uint32_t ps = rd(RC(sl, p, R_PST));
+    if ((ps & 3u) != ST_START) return;
+    const uint32_t qm = rd(S(sl, SL_QUORUM)) & 0xFFu;
+    if (!((qm >> p) & 1u)) {
+      const uint32_t ps2 = (ps & ~3u) | ST_PAYLOAD;
+      if (ps & PS_BUF) {  // buffered commit (atlas.rs:288-292)
+        put(RC(sl, p, R_PST), ps2 & ~PS_BUF);
+        h_mcommit(p, (ps >> 4) & 15u, dot);
+      } else {
+        put(RC(sl, p, R_PST), ps2);
+      }
+      return;
+    }
+    const bool from_self = from == p;
+    const uint32_t cnt = rd(S(sl, SL_CNT));
+    const uint32_t ncol = cnt & 0xFFu, nk = (cnt >> 16) & 3u;
+    const bool ro = (cnt >> 18) & 1u;
+    const uint32_t colv = lid < ncol ? S(sl, SL_COLLECT + lid) : 0u;
+    uint32_t depv = 0, nd = 0;
+    if (from_self) {
+      depv = colv;
+      nd = ncol;
+    } else {
+      nd = add_cmd(p, dot, rd(S(sl, SL_KEYS)), nk, ro, colv, ncol, depv);
+    }
+    if (nd > g.amax) {
+      fail_cap(__LINE__);
+      return;
+    }
+    put(RC(sl, p, R_PST), (ps & ~3u) | ST_COLLECT);
+    if (lid < g.amax) S(sl, g.sl_ack + p * g.amax + lid) = lid < nd ? depv : 0u;
+    if (protocol == FX_PROTOCOL_EPAXOS && from_self) return;  // epaxos.rs:290-300
+    act_send(M_COLLECT_ACK, dot, 1u << from);
+  }
+
+  // atlas.rs:327-402 / epaxos.rs:303-368
+  __device__ __forceinline__ void h_mcollectack(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (sl == NONE) {
+      err = FX_ERR_SIM_LATE;
+      return;
+    }
+    if ((rd(RC(sl, p, R_PST)) & 3u) != ST_COLLECT) return;
+    const uint32_t masks = rd(S(sl, SL_MASKS));
+    const uint32_t part = (masks & 0xFFu) | (1u << from);
+    put(S(sl, SL_MASKS), (masks & ~0xFFu) | part);
+    const uint32_t qs = rd(S(sl, SL_QUORUM)) >> 8;
+    const uint32_t fq_eff = protocol == FX_PROTOCOL_EPAXOS ? qs - 1u : qs;  // EPaxosInfo (epaxos.rs:650-662)
+    if (pop32(part) != fq_eff) return;
+    // QuorumDeps: union + per-dep report counts; lanes [q amax, (q + 1) amax)
+    // hold process q's reported deps
+    const uint32_t q = lid / g.amax, j = lid % g.amax;
+    uint32_t v = 0;
+    if (q < n && ((part >> q) & 1u)) v = S(sl, g.sl_ack + q * g.amax + j);
+    const bool valid = v != 0;
+    uint32_t cnt = 0;
+    bool first = valid;
+    const uint64_t vm = bal(valid);
+    for (uint64_t m = vm; m; m &= m - 1) {
+      const uint32_t l2 = ctz64(m);
+      const uint32_t v2 = rl(v, l2);
+      if (valid && v2 == v) {
+        ++cnt;
+        if (l2 < lid) first = false;
+      }
+    }
+    const uint64_t um = bal(first);
+    const uint32_t nu = pop64(um);
+    if (nu > g.vmax) {
+      fail_cap(__LINE__);
+      return;
+    }
+    bool fast;
+    if (protocol == FX_PROTOCOL_ATLAS) {
+      const uint32_t threshold = qs - n / 2u;  // |quorum| - minority (atlas.rs:361-368)
+      fast = !bal(first && cnt < threshold);
+    } else {
+      fast = nu == 0 || !bal(first && cnt != fq_eff);  // check_equal (quorum.rs:72-103)
+    }
+    uint32_t rank = 0;
+    for (uint64_t m = um; m; m &= m - 1) rank += rl(v, ctz64(m)) < v ? 1u : 0u;
+    if (first) S(sl, g.sl_value + rank) = v;
+    const uint32_t c0 = rd(S(sl, SL_CNT));
+    put(S(sl, SL_CNT), (c0 & ~0xFF00u) | (nu << 8) | (fast ? 0u : (1u << 19)));
+    const bool ro = (c0 >> 18) & 1u;
+    if (lid == p) {  // BaseProcess::path (base.rs:229-243)
+      if (fast) {
+        ++pfast;
+        if (ro) ++pfr;
+      } else {
+        ++pslow;
+        if (ro) ++psr;
+      }
+    }
+    if (fast) act_send(M_COMMIT, dot, (1u << n) - 1u);
+    else act_send(M_CONSENSUS, dot, (rl(pq, p) >> 8) & 0xFFu);  // skip_prepare: ballot = coordinator
+  }
+
+  // the GC track's committed clock at p (MCommitDot, gc/clock.rs:43-48): the
+  // frontier moves over every contiguous seq committed at p; a dot whose slot
+  // was freed was executed, hence committed, everywhere
+  __device__ __forceinline__ void gc_commit(uint32_t p, uint32_t dot) {
+    const uint32_t si = FX_DOT_SRC(dot) - 1u, sq = FX_DOT_SEQ(dot);
+    uint32_t fr = rl(gcf, p * 8u + si);
+    if (sq != fr + 1u) return;
+    const uint32_t top = rl(pseq, si);
+    for (uint32_t guard = 0; guard <= g.NS; ++guard) {
+      const uint32_t nx = fr + 1u;
+      if (nx > top) break;
+      const uint32_t d2 = FX_PACK_DOT(si + 1u, nx);
+      const uint32_t sl = hslot(d2);
+      if (rd(S(sl, SL_DOT)) == d2 && (rd(RC(sl, p, R_PST)) & 3u) != ST_COMMIT) break;
+      fr = nx;
+    }
+    lset(gcf, p * 8u + si, fr);
+  }
+
+  // atlas.rs:404-475 / epaxos.rs:370-428
+  __device__ __forceinline__ void h_mcommit(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (sl == NONE) {
+      err = FX_ERR_SIM_LATE;
+      return;
+    }
+    const uint32_t ps = rd(RC(sl, p, R_PST));
+    if ((ps & 3u) == ST_START) {  // buffered_commits.insert
+      put(RC(sl, p, R_PST), (ps & ~0xF4u) | PS_BUF | (from << 4));
+      return;
+    }
+    if ((ps & 3u) == ST_COMMIT) return;
+    xinfo = sl;  // to_executors.push(GraphExecutionInfo::add(dot, cmd, value.deps))
+    put(RC(sl, p, R_PST), (ps & ~3u) | ST_COMMIT);
+    const uint32_t masks = rd(S(sl, SL_MASKS));
+    put(S(sl, SL_MASKS), masks + (1u << 16));
+    if (gc_ms) gc_commit(p, dot);  // Forward(MCommitDot) to self
+  }
+
+  // atlas.rs:477-524 / epaxos.rs:430-477
+  __device__ __forceinline__ void h_mconsensus(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (sl == NONE) {
+      err = FX_ERR_SIM_LATE;
+      return;
+    }
+    const uint32_t ps = rd(RC(sl, p, R_PST));
+    if ((ps & 3u) == ST_COMMIT) {  // chosen: reply with the chosen value
+      act_send(M_COMMIT, dot, 1u << from);
+      return;
+    }
+    put(RC(sl, p, R_PST), ps | PS_ACC);
+    act_send(M_CONSENSUS_ACK, dot, 1u << from);
+  }
+
+  // atlas.rs:526-558 / epaxos.rs:479-517
+  __device__ __forceinline__ void h_mconsensusack(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (sl == NONE) {
+      err = FX_ERR_SIM_LATE;
+      return;
+    }
+    if (!((rd(S(sl, SL_CNT)) >> 19) & 1u)) return;  // proposer ballot != b
+    const uint32_t masks = rd(S(sl, SL_MASKS));
+    const uint32_t acc = ((masks >> 8) & 0xFFu) | (1u << from);
+    if (pop32(acc) == synod_f + 1u) {
+      put(S(sl, SL_MASKS), masks & ~0xFF00u);  // reset_state
+      if (!(rd(RC(sl, p, R_PST)) & PS_ACC)) {  // single.rs:346-349 panic
+        err = FX_ERR_SIM_LATE;
+        return;
+      }
+      act_send(M_COMMIT, dot, (1u << n) - 1u);
+    } else {
+      put(S(sl, SL_MASKS), (masks & ~0xFF00u) | (acc << 8));
+    }
+  }
+
+  // ------------------------------------------------------------------ GC
+  // periodic GarbageCollection at p (atlas.rs:699-714): MGarbageCollection
+  // with p's committed frontier to every other process (ascending)
+  __device__ __forceinline__ void gc_tick(uint32_t p) {
+    const uint32_t fv = gather(gcf, (p * 8u + lid) & 63u);  // lane s: frontier of source s + 1
+    for (uint32_t q = 0; q < n && !err; ++q) {
+      if (q == p) continue;
+      const uint32_t d = msg_delay(rl(dpq, p * 8u + q));
+      const uint32_t e = push_event(now + d, (2u << 6) | (p << 3) | q, M_GC | (p << 4) | (q << 8), 0);
+      if (e == NONE) return;
+      if (lid < n) W(g.o_gp, e * n + lid) = fv;
+    }
+  }
+  // MGarbageCollection at q from `from` (gc/clock.rs:50-138): merge the
+  // reported frontier; once every other process reported, the stable range of
+  // each source is (previous stable, min over all frontiers]; MStable to self
+  // erases those dots (all committed at q), counted as Stable
+  __device__ __forceinline__ void gc_deliver(uint32_t q, uint32_t from, uint32_t v) {
+    const uint32_t ob = g.o_gco + (q * n + from) * n;
+    if (lid < n) {
+      const uint32_t o = W(ob, lid);
+      W(ob, lid) = max(o, v);
+    }
+    const uint32_t rep = rl(prep, q) | (1u << from);
+    lset(prep, q, rep);
+    uint32_t cur = 0;
+    const uint32_t mine = gather(gcf, (q * 8u + lid) & 63u);
+    if (pop32(rep) == n - 1u) {
+      cur = mine;
+      for (uint32_t r = 0; r < n; ++r) {
+        if (r == q) continue;
+        const uint32_t o = lid < n ? W(g.o_gco + (q * n + r) * n, lid) : 0u;
+        cur = min(cur, o);
+      }
+    }
+    const uint32_t prev = gather(gps, (q * 8u + lid) & 63u);
+    const uint32_t cnt = (lid < n && cur > prev) ? cur - prev : 0u;
+    const uint32_t np = max(cur, prev);
+    const uint32_t t = gather(np, lid & 7u);
+    if ((lid >> 3) == q && (lid & 7u) < n) gps = t;
+    uint32_t total = 0;
+    for (uint32_t s = 0; s < n; ++s) total += rl(cnt, s);
+    if (lid == q) pstab += total;
+  }
+
+  // ===================================================== GraphExecutor
+  // AEClock::contains at xp for a per-lane dot (tarjan.rs:131-132)
+  __device__ __forceinline__ bool contains_v(uint32_t d) {
+    if (!src_ok(d)) return false;
+    const uint32_t sl = hslot(d);
+    if (S(sl, SL_DOT) != d) return true;  // slot freed: executed everywhere
+    return (RC(sl, xp, R_PST) & PS_EXEC) != 0;
+  }
+
+  // one executed command: to_execute -> Command::execute -> to_clients ->
+  // AggregatePending (runner.rs:406-424), executor metrics, execution log
+  __device__ __forceinline__ void on_execute(uint32_t sl, uint32_t d, uint32_t start) {
+    const uint32_t p = xp;
+    if (xk < A.exec_cap && A.executed && lid == 0) A.executed[((size_t)inst * n + p) * A.exec_cap + xk] = d;
+    ++xk;
+    hist_delay(now - start);  // ExecutionDelay (graph/mod.rs:514-518)
+    if (rd(RC(sl, p, R_WAIT))) unlink(sl);
+    const uint32_t c = rd(S(sl, SL_CLIENT));
+    const uint32_t nk = (rd(S(sl, SL_CNT)) >> 16) & 3u;
+    if ((rd(CL(c, 0)) & 0xFFu) == p) {  // pending.wait_for registered this rifl at p
+      const uint32_t pend = rd(CL(c, 3));
+      if (pend < nk) {
+        err = FX_ERR_SIM_LATE;
+        return;
+      }
+      put(CL(c, 3), pend - nk);  // one ExecutorResult per key
+      if (pend == nk) {
+        if (rtop >= g.C + 64u) {
+          fail_cap(__LINE__);
+          return;
+        }
+        put(W(g.o_rdy, rtop++), c);
+      }
+    }
+    const uint32_t masks = rd(S(sl, SL_MASKS));
+    if (((masks >> 24) & 0xFFu) + 1u == n) put(S(sl, SL_DOT), 0u);  // executed everywhere: free the slot
+    else put(S(sl, SL_MASKS), masks + (1u << 24));
+  }
+
+  // PendingIndex (index.rs:145-208): v waits on the dot in slot m
+  __device__ __forceinline__ void unlink(uint32_t v) {
+    const uint32_t p = xp;
+    const uint32_t w = rd(RC(v, p, R_WAIT)), nx = rd(RC(v, p, R_NEXT)), pv = rd(RC(v, p, R_PREV));
+    if (pv) put(RC(pv - 1u, p, R_NEXT), nx);
+    else put(RC(w - 1u, p, R_HEAD), nx);
+    if (nx) put(RC(nx - 1u, p, R_PREV), pv);
+    put(RC(v, p, R_WAIT), 0u);
+    put(RC(v, p, R_NEXT), 0u);
+    put(RC(v, p, R_PREV), 0u);
+  }
+  __device__ __forceinline__ void index_pending(uint32_t v, uint32_t missing) {
+    const uint32_t p = xp;
+    if (rd(RC(v, p, R_WAIT))) unlink(v);
+    const uint32_t m = slot_of(missing);
+    if (m == NONE) {  // a missing dep is never executed at p, so its slot is live
+      err = FX_ERR_SIM_LATE;
+      return;
+    }
+    const uint32_t h = rd(RC(m, p, R_HEAD));
+    put(RC(v, p, R_NEXT), h);
+    put(RC(v, p, R_PREV), 0u);
+    if (h) put(RC(h - 1u, p, R_PREV), v + 1u);
+    put(RC(m, p, R_HEAD), v + 1u);
+    put(RC(v, p, R_WAIT), m + 1u);
+  }
+
+  // sorts the slots W(src, 0 .. cnt) by dot, ascending, into W(dst, ..)
+  // (SCC = BTreeSet<Dot>, tarjan.rs:15; waiters in C2 order)
+  __device__ __forceinline__ void sort_slots(uint32_t src, uint32_t cnt, uint32_t dst) {
+    if (cnt == 1) {
+      put(W(dst, 0), rd(W(src, 0)));
+      return;
+    }
+    for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
+      const uint32_t i = i0 + lid;
+      const uint32_t msl = i < cnt ? W(src, i) : 0u;
+      const uint32_t md = i < cnt ? S(msl, SL_DOT) : NONE;
+      uint32_t rank = 0;
+      for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+        const uint32_t k = k0 + lid;
+        const uint32_t kd = k0 == i0 ? md : (k < cnt ? S(W(src, k), SL_DOT) : NONE);
+        const uint32_t m = min(64u, cnt - k0);
+        for (uint32_t j = 0; j < m; ++j) rank += rl(kd, j) < md ? 1u : 0u;
+      }
+      if (i < cnt) W(dst, rank) = msl;
+    }
+  }
+
+  // save_scc (mod.rs:488-523): the members W(o_tstk, base .. base + cnt)
+  // (already in the executed clock) in ascending dot order; released dots
+  // pushed to the worklist
+  __device__ __forceinline__ void save_scc(uint32_t base, uint32_t cnt) {
+    hist_chain(cnt);
+    sort_slots(g.o_tstk + base, cnt, g.o_tl);
+    for (uint32_t r = 0; r < cnt && !err; ++r) {
+      const uint32_t sl = rd(W(g.o_tl, r));
+      const uint32_t d = rd(S(sl, SL_DOT));
+      const uint32_t st = rd(RC(sl, xp, R_START));
+      if (nwl >= 2u * g.NS) {
+        fail_cap(__LINE__);
+        return;
+      }
+      put(W(g.o_wl, nwl++), sl);
+      on_execute(sl, d, st);
+    }
+  }
+
+  // find_scc (mod.rs:409-486) + strong_connect (tarjan.rs:96-316) + finalize
+  // (tarjan.rs:60-93) from the pending vertex in slot rsl.  On a missing dep,
+  // *missing = it and the vertices left on the stack are marked visited with
+  // mark_epoch (0 = no marks).
+  __device__ __forceinline__ uint32_t find_scc(uint32_t rsl, uint32_t* missing, uint32_t mark_epoch, bool* saved) {
+    const uint32_t p = xp;
+    *saved = false;
+    idc = 1;
+    tsp = 0;
+    fsp = 0;
+    put(RC(rsl, p, R_TL), 1u | (1u << 16));
+    put(RC(rsl, p, R_MARK), rd(RC(rsl, p, R_MARK)) | 1u);
+    put(W(g.o_tstk, tsp++), rsl);
+    put(W(g.o_fv, fsp++), rsl);
+    // the top frame lives in registers: its slot, next dep, id, low, dot and
+    // dep row (lane j = dep j)
+    uint32_t cv = rsl, ci = 0, cid = 1, clow = 1, cdot = rd(S(rsl, SL_DOT));
+    uint32_t cnd = (rd(S(rsl, SL_CNT)) >> 8) & 0xFFu;
+    uint32_t drow = lid < cnd ? S(rsl, g.sl_value + lid) : 0u;
+    uint32_t result = FOUND;
+    for (uint32_t guard = 0; fsp && !err; ++guard) {
+      if (guard > 64u * g.NS + 64u) {
+        fail_cap(__LINE__);
+        break;
+      }
+      if (ci < cnd) {
+        const uint32_t d = rl(drow, ci);
+        ++ci;
+        if (d == cdot || !src_ok(d)) continue;  // self (tarjan.rs:128-130)
+        const uint32_t sl = hslot(d);
+        if (rd(S(sl, SL_DOT)) != d) continue;  // executed everywhere (tarjan.rs:131-145)
+        const uint32_t ps = rd(RC(sl, p, R_PST));
+        if (ps & PS_EXEC) continue;  // executed here
+        if (!(ps & PS_INGRAPH)) {    // missing (tarjan.rs:148-157, shard_count == 1)
+          *missing = d;
+          result = MISSING;
+          break;
+        }
+        const uint32_t tw = rd(RC(sl, p, R_TL)), mk = rd(RC(sl, p, R_MARK));
+        if ((tw & 0xFFFFu) == 0) {  // recurse (tarjan.rs:172-214)
+          put(W(g.o_fi, fsp - 1u), ci);
+          put(RC(cv, p, R_TL), cid | (clow << 16));
+          ++idc;
+          if (idc > 0xFFFFu || tsp >= g.NS || fsp >= g.NS) {
+            fail_cap(__LINE__);
+            break;
+          }
+          put(RC(sl, p, R_TL), idc | (idc << 16));
+          put(RC(sl, p, R_MARK), mk | 1u);
+          put(W(g.o_tstk, tsp++), sl);
+          put(W(g.o_fv, fsp++), sl);
+          cv = sl;
+          ci = 0;
+          cid = idc;
+          clow = idc;
+          cdot = d;
+          cnd = (rd(S(sl, SL_CNT)) >> 8) & 0xFFu;
+          drow = lid < cnd ? S(sl, g.sl_value + lid) : 0u;
+        } else if (mk & 1u) {  // on the stack (tarjan.rs:215-225)
+          clow = min(clow, tw & 0xFFFFu);
+        }
+        continue;
+      }
+      // cv finished
+      const uint32_t lowv = clow;
+      if (cid == lowv) {  // SCC root: pop the members (tarjan.rs:233-312)
+        uint32_t base = tsp;
+        while (base > 0) {
+          --base;
+          const uint32_t x = rd(W(g.o_tstk, base));
+          put(RC(x, p, R_MARK), rd(RC(x, p, R_MARK)) & ~1u);
+          put(RC(x, p, R_PST), rd(RC(x, p, R_PST)) | PS_EXEC);  // executed_clock.add (tarjan.rs:293)
+          if (x == cv) break;
+        }
+        const uint32_t cnt = tsp - base;
+        save_scc(base, cnt);
+        tsp = base;
+        *saved = true;
+        if (err) break;
+      }
+      --fsp;
+      if (fsp) {  // resume the parent frame (tarjan.rs:211: low = min(low, dep low))
+        const uint32_t pp = rd(W(g.o_fv, fsp - 1u));
+        cv = pp;
+        ci = rd(W(g.o_fi, fsp - 1u));
+        const uint32_t tw = rd(RC(pp, p, R_TL));
+        cid = tw & 0xFFFFu;
+        clow = min(tw >> 16, lowv);
+        cdot = rd(S(pp, SL_DOT));
+        cnd = (rd(S(pp, SL_CNT)) >> 8) & 0xFFu;
+        drow = lid < cnd ? S(pp, g.sl_value + lid) : 0u;
+      }
+    }
+    // finalize: ids of the vertices left on the stack; failed searches mark them visited
+    for (uint32_t k = 0; k < tsp; ++k) {
+      const uint32_t x = rd(W(g.o_tstk, k));
+      put(RC(x, p, R_TL), 0u);
+      if (mark_epoch && result == MISSING) put(RC(x, p, R_MARK), (rd(RC(x, p, R_MARK)) & 1u) | (mark_epoch << 1));
+    }
+    tsp = 0;
+    return result;
+  }
+
+  // check_pending (mod.rs:556-587) + try_pending (589-642): LIFO over the
+  // released dots; each one's waiters in ascending dot order (C2)
+  __device__ __forceinline__ void check_pending() {
+    const uint32_t p = xp;
+    while (nwl && !err) {
+      const uint32_t x = rd(W(g.o_wl, --nwl));
+      uint32_t v = rd(RC(x, p, R_HEAD));
+      if (!v) continue;
+      put(RC(x, p, R_HEAD), 0u);
+      // PendingIndex::remove: collect (and unregister) every waiter
+      uint32_t cnt = 0;
+      while (v) {
+        const uint32_t sl = v - 1u;
+        if (cnt >= g.NS) {
+          fail_cap(__LINE__);
+          return;
+        }
+        put(W(g.o_tmp, cnt++), sl);
+        v = rd(RC(sl, p, R_NEXT));
+        put(RC(sl, p, R_WAIT), 0u);
+        put(RC(sl, p, R_NEXT), 0u);
+        put(RC(sl, p, R_PREV), 0u);
+      }
+      sort_slots(g.o_tmp, cnt, g.o_tw);
+      // visited-skip set = vertices marked with this epoch
+      uint32_t cur = ++epoch;
+      for (uint32_t k = 0; k < cnt && !err; ++k) {
+        const uint32_t wsl = rd(W(g.o_tw, k));
+        if (rd(RC(wsl, p, R_PST)) & PS_EXEC) continue;  // no longer pending (NotPending)
+        if ((rd(RC(wsl, p, R_MARK)) >> 1) == cur) continue;  // visited by a failed search
+        uint32_t missing = 0;
+        bool saved = false;
+        const uint32_t r = find_scc(wsl, &missing, cur, &saved);
+        if (err) return;
+        if (r == FOUND) {
+          cur = ++epoch;  // visited.clear()
+        } else {
+          index_pending(wsl, missing);
+          if (saved) cur = ++epoch;
+        }
+      }
+    }
+  }
+
+  // GraphExecutor::handle(Add) (executor.rs:69-80) -> handle_add (mod.rs:213-275)
+  __device__ __forceinline__ void x_add(uint32_t p, uint32_t sl) {
+    xp = p;
+    xk = rl(pexec, p);
+    nwl = 0;
+    const uint32_t d = rd(S(sl, SL_DOT));
+    const uint32_t ps = rd(RC(sl, p, R_PST));
+    if (ps & (PS_INGRAPH | PS_EXEC)) {
+      err = FX_ERR_DOUBLE_INDEX;
+      return;
+    }
+    const uint32_t vc = (rd(S(sl, SL_CNT)) >> 8) & 0xFFu;
+    deps_total += vc;
+    const uint32_t depj = lid < vc ? S(sl, g.sl_value + lid) : 0u;
+    bool keep = false;
+    if (lid < vc && depj != d) keep = !contains_v(depj);
+    if (!bal(keep)) {  // every dep executed: a singleton SCC
+      put(RC(sl, p, R_PST), ps | PS_EXEC);
+      hist_chain(1u);
+      put(W(g.o_wl, nwl++), sl);
+      on_execute(sl, d, now);
+    } else {
+      put(RC(sl, p, R_PST), ps | PS_INGRAPH);
+      put(RC(sl, p, R_START), now);  // Vertex::start_time_ms (tarjan.rs:332-348)
+      uint32_t missing = 0;
+      bool saved = false;
+      const uint32_t r = find_scc(sl, &missing, 0, &saved);
+      if (r == MISSING && !err) index_pending(sl, missing);  // index_pending (mod.rs:525-554)
+    }
+    if (!err) check_pending();
+    lset(pexec, p, xk);
+  }
+
+  // =========================================== send_to_processes_and_executors
+  __device__ __forceinline__ void frame_push() {
+    if (nfrm >= FMAX) {
+      fail_cap(__LINE__);
+      return;
+    }
+    const uint32_t fi = nfrm++;
+    lset(frw, fi, 0);
+    lset(frb, fi, rtop);
+    xinfo = NONE;
+  }
+  __device__ __forceinline__ void send_p(uint32_t from, uint32_t to, uint32_t kind, uint32_t dot) {
+    const uint32_t d = msg_delay(rl(dpq, from * 8u + to));
+    push_event(now + d, 0u, kind | (from << 4) | (to << 8), dot);
+  }
+
+  // handle_send_to_proc / handle_submit_to_proc, then
+  // send_to_processes_and_executors (runner.rs:351-377, 395-488) with every
+  // self-delivery in the reference's recursion order (sim_wave.hip's loop)
+  __device__ __forceinline__ void run_handlers(uint32_t p, uint32_t from, uint32_t kind, uint32_t w2) {
+    bool pend = true;
+    for (uint32_t guard = 0; !err; ++guard) {
+      if (guard > 4096u) {
+        fail_cap(__LINE__);
+        return;
+      }
+      if (pend) {
+        pend = false;
+        frame_push();
+        if (err) return;
+        switch (kind) {
+          case M_SUBMIT: h_submit(p, w2); break;
+          case M_COLLECT: h_mcollect(p, from, w2); break;
+          case M_COLLECT_ACK: h_mcollectack(p, from, w2); break;
+          case M_COMMIT: h_mcommit(p, from, w2); break;
+          case M_CONSENSUS: h_mconsensus(p, from, w2); break;
+          case M_CONSENSUS_ACK: h_mconsensusack(p, from, w2); break;
+          default: err = FX_ERR_INVALID_ARG;
+        }
+        if (xinfo != NONE && !err) {  // to_executors (<= 1 per handler)
+          const uint32_t sl = xinfo;
+          xinfo = NONE;
+          x_add(p, sl);
+        }
+        continue;
+      }
+      if (nfrm == 0) return;
+      const uint32_t fi = nfrm - 1;
+      const uint32_t w = rl(frw, fi);
+      if (w & 3u) {  // ToSend: targets ascending (C4), self recurses in place
+        const uint32_t tgt = (w >> 8) & 0xFFu, k2 = (w >> 2) & 15u, dot = rl(frd, fi);
+        uint32_t nx = (w >> 16) & 15u;
+        while (nx < n) {
+          const uint32_t to = nx++;
+          if (!((tgt >> to) & 1u)) continue;
+          if (to == p) {
+            lset(frw, fi, (w & ~(15u << 16)) | (nx << 16));
+            from = p;
+            kind = k2;
+            w2 = dot;
+            pend = true;
+            break;
+          }
+          send_p(p, to, k2, dot);
+          if (err) return;
+        }
+        if (pend) continue;
+        lset(frw, fi, 0);
+      }
+      // ready results -> schedule_to_client (runner.rs:434-440, 491-504)
+      const uint32_t b = rl(frb, fi);
+      for (uint32_t r = b; r < rtop && !err; ++r) {
+        const uint32_t c = rd(W(g.o_rdy, r));
+        const uint32_t d = msg_delay(rd(CL(c, 5)));
+        push_event(now + d, 0u, E_CLIENT, c);
+      }
+      rtop = b;
+      --nfrm;
+    }
+  }
+
+  // ======================================================= event loop
+  // Client::cmd_send: the next command of client c -> SubmitToProc
+  __device__ __forceinline__ bool client_send(uint32_t c) {
+    const uint32_t issued = rd(CL(c, 1));
+    if (issued >= cmds) return false;
+    put(CL(c, 1), issued + 1u);
+    put(CL(c, 2), now);  // Pending::start
+    const uint32_t d = msg_delay(rd(CL(c, 4)));
+    push_event(now + d, 0u, M_SUBMIT | ((rd(CL(c, 0)) & 0xFFu) << 8), c);
+    return true;
+  }
+
+  __device__ __forceinline__ void run_event(uint32_t kind, uint32_t from, uint32_t to, uint32_t arg, uint32_t gcv) {
+    switch (kind) {
+      case M_SUBMIT: {
+        const uint32_t c = arg, p = to;
+        note(2, p + 1, c + 1, rd(CL(c, 1)));
+        put(CL(c, 3), K);  // AggregatePending::wait_for: key_count results
+        run_handlers(p, p, M_SUBMIT, c);
+        return;
+      }
+      case E_CLIENT: {  // Client::cmd_recv + cmd_send (simulation.rs:132-149)
+        const uint32_t c = arg;
+        const uint32_t issued = rd(CL(c, 1));
+        note(4, c + 1, 0, issued);
+        const uint32_t lat = now - rd(CL(c, 2));  // latency.as_millis()
+        lat_sum += lat;
+        if (lid == 0 && A.latency_log && issued - 1u < A.lat_cap)
+          A.latency_log[((size_t)inst * g.C + c) * A.lat_cap + issued - 1u] = lat;
+        hist_lat(rd(CL(c, 0)) >> 8, lat);
+        if (!client_send(c)) {
+          ++clients_done;
+          if (clients_done == g.C) {
+            if (has_extra) {
+              final_ms = now + extra;
+              in_extra = true;
+            } else {
+              done = true;
+            }
+          }
+        }
+        return;
+      }
+      case E_TICK:
+        gc_tick(to);
+        push_event(now + gc_ms, (1u << 6) | (to << 3), E_TICK | (to << 8), 0);
+        return;
+      case E_NOTIF:  // GraphExecutor::executed is None (executor/mod.rs:74-79)
+        push_event(now + en_ms, 0u, E_NOTIF | (to << 8), 0);
+        return;
+      case M_GC:
+        gc_deliver(to, from, gcv);
+        return;
+      default:
+        note(3, to + 1, from + 1, ((uint64_t)kind << 32) | arg);
+        run_handlers(to, from, kind, arg);
+    }
+  }
+};
+
+template <uint32_t NG>
+__global__ __launch_bounds__(64) void k_simx(ArgsX a) {
+  __shared__ uint32_t smem[LDS_WORDS];
+  const uint32_t inst = blockIdx.x;
+  if (inst >= a.instances) return;
+  Big<NG> s;
+  s.lid = threadIdx.x;
+  s.A = a;
+  s.g = a.g;
+  s.M = a.arena + (size_t)inst * a.g.words;
+  s.lds = smem;
+  s.inst = inst;
+  const fx_sim_spec& sp = a.specs[inst];
+  s.seed = sp.seed;
+  s.rng_inst = sp.instance;
+  s.protocol = sp.protocol;
+  s.n = a.g.n;
+  s.f = sp.f;
+  s.C = a.g.C;
+  s.K = a.g.K;
+  s.gc_ms = sp.gc_interval_ms;
+  s.en_ms = sp.executed_notification_ms;
+  s.cmds = sp.commands_per_client;
+  s.conflict_ = sp.conflict_rate;
+  s.pool = sp.pool_size;
+  s.ro_pct = sp.read_only_pct;
+  s.reorder = sp.reorder_messages != 0;
+  s.nfr = sp.nfr != 0;
+  s.has_extra = sp.extra_sim_time_ms >= 0;
+  s.extra = s.has_extra ? (uint32_t)sp.extra_sim_time_ms : 0u;
+  const uint32_t n = s.n;
+  uint32_t fq, wq;
+  if (s.protocol == FX_PROTOCOL_ATLAS) {
+    fq = n / 2 + s.f;
+    wq = s.f + 1;
+    s.synod_f = s.f;
+  } else {
+    const uint32_t fe = n / 2;
+    fq = fe + (fe + 1) / 2;
+    wq = fe + 1;
+    s.synod_f = fe;  // EPaxos::allowed_faults
+  }
+  const uint32_t maj = n / 2 + 1;
+  const GeoX& g = a.g;
+  uint32_t* M = s.M;
+  // ---------------------------------------------------------------- init
+  for (uint32_t i = s.lid; i < LDS_WORDS; i += 64) smem[i] = 0;
+  for (uint32_t i = s.lid; i < g.NS; i += 64) M[g.o_slot + i * g.SW + SL_DOT] = 0;
+  for (uint32_t i = s.lid; i < g.n * g.ncli_keys * 2u; i += 64) M[g.o_kd + i] = 0;
+  for (uint32_t i = s.lid; i < g.n * g.n * g.n; i += 64) M[g.o_gco + i] = 0;
+  for (uint32_t i = s.lid; i < g.R; i += 64) {
+    M[g.o_kh + i] = NONE;
+    M[g.o_kl + i] = NONE;
+    M[g.o_free + i] = g.R - 1u - i;  // free stack
+  }
+  s.nfree = g.R;
+#pragma unroll
+  for (uint32_t k = 0; k < NG; ++k) s.gh[k] = s.gl[k] = NONE;
+  const uint32_t RP = a.RP;
+  // process quorums (BaseProcess::discover over sort_processes_by_distance,
+  // base.rs:62-154, util.rs:153-185) and link delays
+  for (uint32_t p = 0; p < n; ++p) {
+    const uint32_t rp = sp.process_regions[p];
+    uint32_t pos = 0;
+    if (s.lid < n) {
+      const uint32_t kq = a.rank[rp * RP + sp.process_regions[s.lid]];
+      for (uint32_t q2 = 0; q2 < n; ++q2) {
+        const uint32_t k2 = a.rank[rp * RP + sp.process_regions[q2]];
+        if (k2 < kq || (k2 == kq && q2 < s.lid)) ++pos;
+      }
+    }
+    const uint32_t fqm = (uint32_t)bal(s.lid < n && pos < fq);
+    const uint32_t wqm = (uint32_t)bal(s.lid < n && pos < wq);
+    const uint32_t mqm = (uint32_t)bal(s.lid < n && pos < maj);
+    s.lset(s.pq, p, fqm | (wqm << 8) | (mqm << 16));
+    if (s.lid >= p * 8u && s.lid < p * 8u + n) s.dpq = a.ping[rp * RP + sp.process_regions[s.lid - p * 8u]] / 2u;
+  }
+  // clients: for region in client_regions, clients_per_region each (runner.rs:143-163)
+  {
+    uint32_t c0 = 0;
+    for (uint32_t r = 0; r < sp.num_client_regions; ++r) {
+      const uint32_t rc = sp.client_regions[r];
+      uint32_t best = 0, bk = 0xFFFFFFFFu;
+      for (uint32_t p = 0; p < n; ++p) {  // closest process: minimal (rank, id)
+        const uint32_t k = a.rank[rc * RP + sp.process_regions[p]];
+        if (k < bk) {
+          bk = k;
+          best = p;
+        }
+      }
+      const uint32_t dcs = a.ping[rc * RP + sp.process_regions[best]] / 2u;
+      const uint32_t dcr = a.ping[sp.process_regions[best] * RP + rc] / 2u;
+      for (uint32_t i = s.lid; i < sp.clients_per_region; i += 64) {
+        const uint32_t c = c0 + i;
+        M[g.o_cl + c * 8u + 0] = best | (rc << 8);
+        M[g.o_cl + c * 8u + 1] = 0;
+        M[g.o_cl + c * 8u + 2] = 0;
+        M[g.o_cl + c * 8u + 3] = 0;
+        M[g.o_cl + c * 8u + 4] = dcs;
+        M[g.o_cl + c * 8u + 5] = dcr;
+      }
+      c0 += sp.clients_per_region;
+    }
+  }
+  __syncthreads();
+  // periodic events (runner.rs:179-187), then clients (run(), C5 ascending)
+  if (s.gc_ms)
+    for (uint32_t p = 0; p < n; ++p) s.push_event(s.gc_ms, (1u << 6) | (p << 3), E_TICK | (p << 8), 0);
+  const bool sim_en = a.sim_exec_notif || s.has_extra;
+  for (uint32_t p = 0; p < n; ++p) {
+    if (sim_en) s.push_event(s.en_ms, 0u, E_NOTIF | (p << 8), 0);
+    else ++s.seq;  // keep the insertion numbering of the reference
+  }
+  for (uint32_t c = 0; c < s.C && !s.err; ++c) {
+    if (s.cmds == 0) s.err = FX_ERR_INVALID_ARG;
+    else s.client_send(c);
+  }
+  // ------------------------------------------------------------ loop
+  const uint64_t max_events = a.max_events ? a.max_events : 0xFFFFFFFFull;
+  while (!s.done && !s.err) {
+    uint32_t hi = 0;
+    const uint32_t e = s.pop_event(hi);
+    if (e == NONE) {
+      s.err = FX_ERR_SIM_LATE;  // "there should be a new action"
+      break;
+    }
+    const uint32_t t = hi >> 8;
+    if (t < s.now) {
+      s.err = FX_ERR_TIME_RANGE;
+      break;
+    }
+    s.now = t;
+    const uint32_t info = s.rd(M[g.o_inf + e]), arg = s.rd(M[g.o_arg + e]);
+    const uint32_t kind = info & 15u, from = (info >> 4) & 15u, to = (info >> 8) & 15u;
+    const uint32_t gcv = kind == M_GC && s.lid < n ? M[g.o_gp + e * n + s.lid] : 0u;
+    s.free_event(e);
+    s.run_event(kind, from, to, arg, gcv);
+    if (s.in_extra && s.now > s.final_ms) s.done = true;
+    if (s.events >= max_events) s.err = FX_ERR_SIM_EVENTS;
+  }
+  // ----------------------------------------------------------- outputs
+  __syncthreads();
+  if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = s.pexec;
+  if (a.stats) {
+    unsigned long long* st = a.stats + (size_t)inst * FX_SIM_STATS;
+    if (s.lid < NMAX) {
+      const bool v = s.lid < n;
+      st[FX_SIM_STAT_FAST + s.lid] = v ? s.pfast : 0u;
+      st[FX_SIM_STAT_SLOW + s.lid] = v ? s.pslow : 0u;
+      st[FX_SIM_STAT_STABLE + s.lid] = v ? s.pstab : 0u;
+      st[FX_SIM_STAT_FAST_READS + s.lid] = v ? s.pfr : 0u;
+      st[FX_SIM_STAT_SLOW_READS + s.lid] = v ? s.psr : 0u;
+    }
+    if (s.lid == 0) {
+      st[FX_SIM_STAT_EVENTS] = s.events;
+      st[FX_SIM_STAT_END_MS] = s.now;
+      st[FX_SIM_STAT_TRACE] = s.trace;
+      st[FX_SIM_STAT_SEQ] = s.seq;
+      st[FX_SIM_STAT_DEPS] = s.deps_total;
+      st[FX_SIM_STAT_LAT_SUM] = s.lat_sum;
+      st[FX_SIM_STAT_ERR_SITE] = s.err_site;
+    }
+  }
+  for (uint32_t i = s.lid; i < HC_BINS + HD_BINS; i += 64) {
+    const uint32_t c = smem[i];
+    if (!c) continue;
+    if (i < HC_BINS) {
+      if (a.chain_hist) atomicAdd(&a.chain_hist[i], (unsigned long long)c);
+    } else if (a.delay_hist) {
+      atomicAdd(&a.delay_hist[i - HC_BINS], (unsigned long long)c);
+    }
+  }
+  for (uint32_t i = s.lid; i < HL_SLOTS; i += 64) {
+    const uint32_t k = smem[HC_BINS + HD_BINS + i];
+    if (k && a.lat_hist)
+      atomicAdd(&a.lat_hist[k - 1u], (unsigned long long)smem[HC_BINS + HD_BINS + HL_SLOTS + i]);
+  }
+  if (s.lid == 0) a.err[inst] = s.err;
+}
+
+}  // namespace simx
+
+// Geometry of the large-instance simulator: ring = events in flight (rounded
+// up to a multiple of 64, at most 16384), dots = live dots per instance
+// (per source: the next power of two of dots / n).  Defaults: 16 events per
+// client (plus the GC traffic) and 8 live dots per client per process region.
+bool simx_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t dots, simx::GeoX& g) {
+  using namespace simx;
+  const uint32_t n = sp.n;
+  if (n < 2 || n > NMAX) return false;
+  const uint32_t C = sp.clients_per_region * sp.num_client_regions;
+  if (C < 1 || C > 65535u) return false;
+  g.n = n;
+  g.C = C;
+  g.K = sp.keys_per_command;
+  if (g.K < 1 || g.K > KMAX) return false;
+  const uint32_t cpr = (C + n - 1) / n;
+  uint32_t want = dots ? (dots + n - 1) / n : std::max<uint32_t>(32u, 8u * cpr);
+  uint32_t Q = 16, qlog = 4;
+  while (Q < want && Q < (1u << 16)) {
+    Q <<= 1;
+    ++qlog;
+  }
+  if (Q < want) return false;
+  g.Q = Q;
+  g.qlog = qlog;
+  g.NS = n * Q;
+  uint32_t R = ring ? ring : std::min<uint32_t>(16384u, 16u * C + 8u * n * n + 256u);
+  R = (R + 63u) & ~63u;
+  if (R > 16384u) return false;
+  g.R = R;
+  g.ncli_keys = sp.pool_size + C + 1;
+  // an MCollectAck carries the coordinator's deps (<= 2K: a write and a read
+  // per key) plus the replica's own (<= 2K); a committed value is their union
+  // over the quorum (<= 2K (n + 1))
+  g.amax = 4 * g.K;
+  g.vmax = 2 * g.K * (n + 1);
+  if (n * g.amax > 64 || g.vmax > 64) return false;
+  g.sl_value = SL_COLLECT + 2 * g.K;
+  g.sl_ack = g.sl_value + g.vmax;
+  g.SW = g.sl_ack + n * g.amax;
+  uint64_t o = 0;
+  auto take = [&](uint32_t& off, uint64_t words) {
+    off = (uint32_t)o;
+    o += (words + 15u) & ~15ull;  // 64-byte aligned tables
+  };
+  take(g.o_slot, (uint64_t)g.NS * g.SW);
+  take(g.o_rec, (uint64_t)g.NS * n * 8u);
+  take(g.o_kd, (uint64_t)n * g.ncli_keys * 2u);
+  take(g.o_cl, (uint64_t)C * 8u);
+  take(g.o_kh, R);
+  take(g.o_kl, R);
+  take(g.o_inf, R);
+  take(g.o_arg, R);
+  take(g.o_gp, (uint64_t)R * n);
+  take(g.o_free, R);
+  take(g.o_gco, (uint64_t)n * n * n);
+  take(g.o_tstk, g.NS);
+  take(g.o_fv, g.NS);
+  take(g.o_fi, g.NS);
+  take(g.o_wl, 2ull * g.NS);
+  take(g.o_tmp, g.NS);
+  take(g.o_tl, g.NS);
+  take(g.o_tw, g.NS);
+  take(g.o_rdy, C + 64u);
+  if (o > 0x7FFFFFFFull) return false;
+  g.words = (uint32_t)o;
+  return true;
+}
+
+bool simx_table_sizes(const fx_sim_spec& sp, uint32_t ring, uint32_t dots, uint32_t* R, uint32_t* NS) {
+  simx::GeoX g;
+  if (!simx_geometry(sp, ring, dots, g)) return false;
+  *R = g.R;
+  *NS = g.NS;
+  return true;
+}
+
+size_t simx_arena_bytes(const fx_sim_spec& sp, uint32_t ring, uint32_t dots) {
+  simx::GeoX g;
+  return simx_geometry(sp, ring, dots, g) ? (size_t)g.words * 4 : 0;
+}
+
+// Launches the large-instance simulator (fx_sim_run validated the batch).
+int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
+  using namespace simx;
+  ArgsX a{};
+  if (!simx_geometry(b->host_specs[0], b->ring_entries, b->dot_slots, a.g)) return FX_ERR_UNSUPPORTED;
+  const size_t bytes = (size_t)a.g.words * 4 * b->instances;
+  void* arena = nullptr;
+  if (hipMallocAsync(&arena, bytes, hs) != hipSuccess) return FX_ERR_HIP;
+  a.specs = b->specs;
+  a.instances = b->instances;
+  a.arena = (uint32_t*)arena;
+  a.ping = b->planet_ping;
+  a.rank = b->planet_rank;
+  a.RP = b->planet_stride;
+  a.exec_cap = b->exec_cap;
+  a.lat_cap = b->lat_cap;
+  a.max_events = b->max_events;
+  a.sim_exec_notif = b->flags & FX_SIM_FLAG_EXEC_NOTIFICATIONS;
+  a.executed = o->executed;
+  a.executed_len = o->executed_len;
+  a.latency_log = o->latency_log;
+  a.dot_client = o->dot_client;
+  a.lat_hist = (unsigned long long*)o->latency_hist;
+  a.lat_bins = o->lat_bins ? o->lat_bins : 1;
+  a.chain_hist = (unsigned long long*)o->chain_hist;
+  a.chain_bins = o->chain_bins ? o->chain_bins : 1;
+  a.delay_hist = (unsigned long long*)o->delay_hist;
+  a.delay_bins = o->delay_bins ? o->delay_bins : 1;
+  a.stats = (unsigned long long*)o->stats;
+  a.err = o->err;
+  const dim3 grid(b->instances), block(64);
+  if (a.g.R <= 4096) hipLaunchKernelGGL(k_simx<1>, grid, block, 0, hs, a);
+  else if (a.g.R <= 8192) hipLaunchKernelGGL(k_simx<2>, grid, block, 0, hs, a);
+  else hipLaunchKernelGGL(k_simx<4>, grid, block, 0, hs, a);
+  const hipError_t le = hipGetLastError();
+  (void)hipFreeAsync(arena, hs);
+  return le == hipSuccess ? FX_OK : FX_ERR_HIP;
+}
+
+}  // namespace fx

@@ -1481,6 +1481,8 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
       st[FX_SIM_STAT_FAST + s.lid] = v ? s.pfast : 0u;
       st[FX_SIM_STAT_SLOW + s.lid] = v ? s.pslow : 0u;
       st[FX_SIM_STAT_STABLE + s.lid] = 0u;
+      st[FX_SIM_STAT_FAST_READS + s.lid] = 0u;  // no read-only commands on this kernel
+      st[FX_SIM_STAT_SLOW_READS + s.lid] = 0u;
     }
     if (s.gc_ms && !s.err) s.gc_finish(s.now, gc_pair, st);
     if (s.lid == 0) {
@@ -1517,6 +1519,11 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
 }  // namespace sim
 
 using namespace sim;
+
+// the large-instance kernel (sim_big.hip)
+size_t simx_arena_bytes(const fx_sim_spec& sp, uint32_t ring, uint32_t dots);
+bool simx_table_sizes(const fx_sim_spec& sp, uint32_t ring, uint32_t dots, uint32_t* R, uint32_t* NS);
+int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs);
 
 static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, Geo& g) {
   const uint32_t n = sp.n;
@@ -1590,15 +1597,25 @@ int fx_sim_plan(const fx_sim_spec* sp, uint32_t ring_entries, uint32_t dot_slots
   return FX_OK;
 }
 
+int fx_sim_plan_large(const fx_sim_spec* sp, uint32_t ring_entries, uint32_t dot_slots, uint64_t* arena_bytes) {
+  if (!sp || !arena_bytes) return FX_ERR_INVALID_ARG;
+  const size_t b = simx_arena_bytes(*sp, ring_entries, dot_slots);
+  if (!b) return FX_ERR_UNSUPPORTED;
+  *arena_bytes = b;
+  return FX_OK;
+}
+
 int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) {
   if (!b || !o || !b->specs || !b->host_specs || !o->err || !b->planet_ping || !b->planet_rank) return FX_ERR_INVALID_ARG;
   if (b->instances == 0) return FX_OK;
   int dc = 0;
   if (hipGetDeviceCount(&dc) != hipSuccess || dc <= 0) return FX_ERR_NO_DEVICE;
-  const uint32_t ring = b->ring_entries;  // 0 = min(4096, 64 n)
-  const uint32_t W = b->dot_slots;  // 0 = the default of sim_geometry
-  if (ring > 65534 || W > 256) return FX_ERR_INVALID_ARG;
+  const uint32_t ring = b->ring_entries;  // 0 = the default of the kernel's geometry
+  const uint32_t W = b->dot_slots;
+  if (ring > 65534 || W > 8u * 65536u) return FX_ERR_INVALID_ARG;
   const fx_sim_spec& s0 = b->host_specs[0];
+  // the all-on-chip kernel unless the batch needs the large-instance one
+  bool large = (b->flags & FX_SIM_FLAG_LARGE) != 0 || W > 256;
   // every instance of a launch shares the geometry (protocol, n, clients, keys)
   for (uint32_t i = 0; i < b->instances; ++i) {
     const fx_sim_spec& s = b->host_specs[i];
@@ -1607,7 +1624,8 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
         s.num_client_regions != s0.num_client_regions || s.keys_per_command != s0.keys_per_command ||
         s.pool_size != s0.pool_size)
       return FX_ERR_INVALID_ARG;
-    if (s.read_only_pct != 0 || s.reorder_messages || s.nfr) return FX_ERR_UNSUPPORTED;
+    if (s.read_only_pct > 100) return FX_ERR_INVALID_ARG;
+    if (s.read_only_pct != 0 || s.reorder_messages || s.nfr) large = true;
     if (s.keys_per_command < 1 || s.keys_per_command > KMAX || s.pool_size < 1) return FX_ERR_INVALID_ARG;
     if (s.f > s.n / 2) return FX_ERR_INVALID_ARG;
     if (s.keys_per_command == 2 && s.conflict_rate >= 100) return FX_ERR_INVALID_ARG;  // workload.rs:49-51
@@ -1620,10 +1638,13 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
     if (s.executed_notification_ms == 0 && s.extra_sim_time_ms >= 0) return FX_ERR_INVALID_ARG;
   }
   SimArgs a{};
-  if (!sim_geometry(s0, ring, W, a.g)) return FX_ERR_UNSUPPORTED;
+  if (!large && (!sim_geometry(s0, ring, W, a.g) || (size_t)a.g.words * 4 > 160 * 1024 || a.g.ncli_keys > 0xFFFFu))
+    large = true;
+  if (large) {
+    if (s0.pool_size + s0.clients_per_region * s0.num_client_regions + 1 > 0xFFFFu) return FX_ERR_UNSUPPORTED;
+    return simx_launch(b, o, (hipStream_t)hip_stream);
+  }
   const size_t lds = (size_t)a.g.words * 4;
-  if (lds > 160 * 1024) return FX_ERR_UNSUPPORTED;
-  if (a.g.ncli_keys > 0xFFFFu) return FX_ERR_UNSUPPORTED;
   a.specs = b->specs;
   a.instances = b->instances;
   a.ping = b->planet_ping;
@@ -1716,6 +1737,18 @@ struct Tmp {
 }  // namespace sim
 }  // namespace fx
 
+// whether fx_sim_run runs the batch on the large-instance kernel
+static bool sim_runs_large(const fx_sim_batch* b) {
+  if ((b->flags & FX_SIM_FLAG_LARGE) || b->dot_slots > 256) return true;
+  for (uint32_t i = 0; i < b->instances; ++i) {
+    const fx_sim_spec& s = b->host_specs[i];
+    if (s.read_only_pct != 0 || s.reorder_messages || s.nfr) return true;
+  }
+  Geo g;
+  return !sim_geometry(b->host_specs[0], b->ring_entries, b->dot_slots, g) || (size_t)g.words * 4 > 160 * 1024 ||
+         g.ncli_keys > 0xFFFFu;
+}
+
 extern "C" int fx_sim_run_tiered(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream,
                                  uint32_t* reruns) {
   if (reruns) *reruns = 0;
@@ -1731,17 +1764,36 @@ extern "C" int fx_sim_run_tiered(const fx_sim_batch* b, const fx_sim_output* o, 
   for (uint32_t i = 0; i < N; ++i)
     if (err[i] == FX_ERR_SIM_CAPACITY) fail.push_back(i);
   if (fail.empty()) return FX_OK;
-  Geo g0;
-  if (!sim_geometry(b->host_specs[0], b->ring_entries, b->dot_slots, g0)) return FX_ERR_UNSUPPORTED;
-  // geometries: the caller's, then a 4x (at least 256 n) message pool and 256 dot slots
-  const uint32_t geo_ring[2] = {b->ring_entries,
-                                std::min<uint32_t>(65534u, std::max<uint32_t>(4u * g0.R, 256u * g0.n))};
-  const uint32_t geo_dots[2] = {b->dot_slots, 256u};
+  // the tier ladder (flags, events, dots): the caller's geometry, then larger tables
+  const uint32_t f0 = b->flags & ~FX_SIM_FLAG_LARGE;
+  uint32_t geo_flags[3], geo_ring[3], geo_dots[3];
+  geo_flags[0] = b->flags;
+  geo_ring[0] = b->ring_entries;
+  geo_dots[0] = b->dot_slots;
+  if (!sim_runs_large(b)) {
+    Geo g0;
+    if (!sim_geometry(b->host_specs[0], b->ring_entries, b->dot_slots, g0)) return FX_ERR_UNSUPPORTED;
+    const uint32_t r1 = std::min<uint32_t>(65534u, std::max<uint32_t>(4u * g0.R, 256u * g0.n));
+    geo_flags[1] = f0;
+    geo_ring[1] = r1;
+    geo_dots[1] = 256u;
+    geo_flags[2] = f0 | FX_SIM_FLAG_LARGE;  // then the large-instance kernel
+    geo_ring[2] = std::min<uint32_t>(16384u, std::max<uint32_t>(2u * r1, 1024u));
+    geo_dots[2] = 2048u;
+  } else {
+    uint32_t R0 = 0, NS0 = 0;
+    if (!simx_table_sizes(b->host_specs[0], b->ring_entries, b->dot_slots, &R0, &NS0)) return FX_ERR_UNSUPPORTED;
+    for (uint32_t t = 1; t < 3; ++t) {
+      geo_flags[t] = f0 | FX_SIM_FLAG_LARGE;
+      geo_ring[t] = std::min<uint32_t>(16384u, R0 << t);
+      geo_dots[t] = std::min<uint32_t>(8u * 65536u, NS0 << (2 * t));
+    }
+  }
   const uint32_t C = b->host_specs[0].clients_per_region * b->host_specs[0].num_client_regions;
   const uint32_t n = b->host_specs[0].n;
   const size_t nh_lat = o->latency_hist ? (size_t)b->planet_regions * o->lat_bins : 0;
   const size_t nh_chain = o->chain_hist ? o->chain_bins : 0, nh_delay = o->delay_hist ? o->delay_bins : 0;
-  for (uint32_t tier = 1; tier <= 2 && !fail.empty(); ++tier) {
+  for (uint32_t tier = 1; tier <= 3 && !fail.empty(); ++tier) {
     Tmp tmp;
     const uint32_t F = (uint32_t)fail.size();
     std::vector<fx_sim_spec> sub(F);
@@ -1761,6 +1813,7 @@ extern "C" int fx_sim_run_tiered(const fx_sim_batch* b, const fx_sim_output* o, 
     nb.specs = dspec;
     nb.host_specs = sub.data();
     nb.instances = F;
+    nb.flags = geo_flags[tier - 1];
     nb.ring_entries = geo_ring[tier - 1];
     nb.dot_slots = geo_dots[tier - 1];
     fx_sim_output no{};
@@ -1779,12 +1832,13 @@ extern "C" int fx_sim_run_tiered(const fx_sim_batch* b, const fx_sim_output* o, 
                                      (const unsigned long long*)nchain, (uint32_t)nh_chain);
     if (nh_delay) hipLaunchKernelGGL(k_hist_sub, hg, hb, 0, hs, (unsigned long long*)o->delay_hist,
                                      (const unsigned long long*)ndelay, (uint32_t)nh_delay);
-    if (tier == 2) {  // no larger geometry: these stay failed, without histogram samples
+    if (tier == 3) {  // no larger geometry: these stay failed, without histogram samples
       if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
       break;
     }
     // 2. rerun them with larger tables into temporaries, histograms straight into the caller's
     fx_sim_batch pb = nb;
+    pb.flags = geo_flags[tier];
     pb.ring_entries = geo_ring[tier];
     pb.dot_slots = geo_dots[tier];
     fx_sim_output po = *o;
@@ -1793,6 +1847,7 @@ extern "C" int fx_sim_run_tiered(const fx_sim_batch* b, const fx_sim_output* o, 
     po.latency_log = o->latency_log && b->lat_cap ? tmp.alloc<uint32_t>((size_t)F * C * b->lat_cap, hs, false)
                                                   : nullptr;
     po.stats = o->stats ? tmp.alloc<uint64_t>((size_t)F * FX_SIM_STATS, hs, true) : nullptr;
+    po.dot_client = o->dot_client ? tmp.alloc<uint32_t>((size_t)F * n * b->exec_cap, hs, true) : nullptr;
     po.err = tmp.alloc<uint32_t>(F, hs, true);
     if (!po.err || (o->executed && !po.executed) || (o->executed_len && !po.executed_len) ||
         (o->stats && !po.stats))
@@ -1805,6 +1860,8 @@ extern "C" int fx_sim_run_tiered(const fx_sim_batch* b, const fx_sim_output* o, 
                                             po.executed_len, dmap, F, n);
     if (po.latency_log) hipLaunchKernelGGL(k_rows_scatter<uint32_t>, sg, sb, 0, hs, o->latency_log, po.latency_log,
                                            dmap, F, C * b->lat_cap);
+    if (po.dot_client) hipLaunchKernelGGL(k_rows_scatter<uint32_t>, sg, sb, 0, hs, o->dot_client, po.dot_client,
+                                          dmap, F, n * b->exec_cap);
     if (po.stats) hipLaunchKernelGGL(k_rows_scatter<uint64_t>, sg, sb, 0, hs, o->stats, po.stats, dmap, F,
                                      FX_SIM_STATS);
     hipLaunchKernelGGL(k_rows_scatter<uint32_t>, sg, sb, 0, hs, o->err, po.err, dmap, F, 1u);

@@ -483,12 +483,19 @@ typedef struct fx_sim_spec {
  * All instances of a batch share protocol family geometry: n, clients per
  * region, number of client regions, keys per command and pool size (the
  * conflict rate, f, seeds, regions and intervals may differ per instance).
- * The GPU path simulates Atlas and EPaxos (GraphExecutor protocols) without
- * read-only commands, NFR or message reordering (FX_ERR_UNSUPPORTED). */
+ * The GPU path simulates Atlas and EPaxos (GraphExecutor protocols).  Two
+ * kernels share the entry point: the all-on-chip one (sim_wave.hip: <= 32
+ * clients per instance, no read-only commands, NFR or message reordering) and
+ * the large-instance one (sim_big.hip: up to 65535 clients per instance,
+ * read-only commands, NFR, message reordering; per-instance state in an HBM
+ * arena of fx_sim_plan_large bytes, allocated stream-ordered by fx_sim_run).
+ * fx_sim_run picks the first when the batch fits it, unless
+ * FX_SIM_FLAG_LARGE is set. */
 #define FX_SIM_FLAG_EXEC_NOTIFICATIONS 1u /* simulate the periodic executed notifications
                                              even when they cannot change the outcome
                                              (GraphExecutor::executed is None; they matter
                                              only for where a run with extra time stops) */
+#define FX_SIM_FLAG_LARGE 2u              /* run the large-instance kernel */
 typedef struct fx_sim_batch {
   const fx_sim_spec* specs;        /* [instances] device copy                          */
   const fx_sim_spec* host_specs;   /* [instances] host copy (validation, geometry)     */
@@ -505,7 +512,9 @@ typedef struct fx_sim_batch {
                                       process links (<= 65534; 0 = 16 n x clients per
                                       process region)                                   */
   uint32_t dot_slots;              /* live dots per instance, a pool shared by the
-                                      coordinators (<= 256; 0 = min(64, 8 clients))     */
+                                      coordinators (<= 256; 0 = min(64, 8 clients)); the
+                                      large-instance kernel: <= 8 x 65536, direct-mapped
+                                      per source (0 = 8 per client per process region) */
   uint32_t pad;
 } fx_sim_batch;
 
@@ -520,8 +529,10 @@ typedef struct fx_sim_batch {
 #define FX_SIM_STAT_SEQ 27u     /* schedule insertions                             */
 #define FX_SIM_STAT_DEPS 28u    /* deps of every executor Add (sum over processes) */
 #define FX_SIM_STAT_LAT_SUM 29u /* sum of every client command's latency (ms)       */
-#define FX_SIM_STAT_ERR_SITE 30u /* where FX_ERR_SIM_CAPACITY was raised (sim_wave.hip line) */
-#define FX_SIM_STATS 32u
+#define FX_SIM_STAT_ERR_SITE 30u /* where FX_ERR_SIM_CAPACITY was raised (source line) */
+#define FX_SIM_STAT_FAST_READS 32u /* [n] FastPathReads (base.rs:229-243): read-only commands */
+#define FX_SIM_STAT_SLOW_READS 40u /* [n] SlowPathReads                                   */
+#define FX_SIM_STATS 48u
 
 typedef struct fx_sim_output {  /* device buffers; NULL where not wanted */
   uint32_t* executed;           /* [instances][n][exec_cap] packed dots, execution order */
@@ -533,15 +544,23 @@ typedef struct fx_sim_output {  /* device buffers; NULL where not wanted */
   uint64_t* stats;              /* [instances][FX_SIM_STATS]                        */
   uint32_t* err;                /* [instances] FX_* status                           */
   uint32_t lat_bins, chain_bins, delay_bins, pad;
+  uint32_t* dot_client;         /* [instances][n][exec_cap] client id (1-based) that submitted
+                                   dot (p + 1, s) at [p][s - 1], or NULL (the rifl of an
+                                   executed dot: the client's k-th dot is its command k + 1) */
 } fx_sim_output;
 
 /* LDS bytes one instance of `spec` needs at the given table sizes
  * (FX_ERR_UNSUPPORTED if it does not fit the GPU path). */
 int fx_sim_plan(const fx_sim_spec* spec, uint32_t ring_entries, uint32_t dot_slots, uint32_t* lds_bytes);
+/* Bytes of HBM arena one instance of `spec` takes in the large-instance kernel
+ * at the given table sizes (0 = defaults); FX_ERR_UNSUPPORTED if it cannot run. */
+int fx_sim_plan_large(const fx_sim_spec* spec, uint32_t ring_entries, uint32_t dot_slots, uint64_t* arena_bytes);
 /* Runs every instance to completion (Runner::run, runner.rs:202-231); asynchronous. */
 int fx_sim_run(const fx_sim_batch* batch, const fx_sim_output* out, void* hip_stream);
 /* fx_sim_run, then (synchronously) reruns the instances that stopped with
- * FX_ERR_SIM_CAPACITY with a 4x (at least 256 n) message pool and 256 dot slots, writing their
+ * FX_ERR_SIM_CAPACITY with larger tables (all-on-chip kernel: a 4x, at least
+ * 256 n, message pool and 256 dot slots, then the large-instance kernel;
+ * large-instance kernel: 2x the events and 4x the dots, twice), writing their
  * rows of every output in place.  Histograms stay exact: the samples the
  * failed runs added before failing are removed by replaying just those runs
  * at the first geometry (the kernel is deterministic per instance) and

@@ -320,7 +320,8 @@ class SimOut(ctypes.Structure):
                 ("delay", ctypes.c_void_p), ("chain_bins", ctypes.c_uint32),
                 ("delay_bins", ctypes.c_uint32), ("end_ms", ctypes.c_uint64),
                 ("events", ctypes.c_uint64), ("trace", ctypes.c_uint64), ("status", ctypes.c_int32),
-                ("pad", ctypes.c_int32), ("monitor_hash", ctypes.c_void_p)]
+                ("pad", ctypes.c_int32), ("monitor_hash", ctypes.c_void_p),
+                ("fast_reads", ctypes.c_void_p), ("slow_reads", ctypes.c_void_p)]
 
 
 def _sim_lib():
@@ -405,6 +406,8 @@ class _OutBufs:
         self.chain = np.zeros(chain_bins, np.uint64)
         self.delay = np.zeros(delay_bins, np.uint64)
         self.monitor_hash = np.zeros(n, np.uint64)
+        self.fast_reads = np.zeros(n, np.uint64)
+        self.slow_reads = np.zeros(n, np.uint64)
         o = SimOut()
         o.executed, o.executed_len, o.exec_cap = self.executed.ctypes.data, self.executed_len.ctypes.data, exec_cap
         o.latency, o.issued, o.R, o.lat_bins = self.latency.ctypes.data, self.issued.ctypes.data, R, lat_bins
@@ -412,6 +415,7 @@ class _OutBufs:
         o.chain, o.delay = self.chain.ctypes.data, self.delay.ctypes.data
         o.chain_bins, o.delay_bins = chain_bins, delay_bins
         o.monitor_hash = self.monitor_hash.ctypes.data
+        o.fast_reads, o.slow_reads = self.fast_reads.ctypes.data, self.slow_reads.ctypes.data
         self.out = o
 
     def result(self):
@@ -421,7 +425,8 @@ class _OutBufs:
                 "latency": self.latency, "issued": self.issued, "fast": self.fast,
                 "slow": self.slow, "stable": self.stable, "chain": self.chain, "delay": self.delay,
                 "end_ms": int(o.end_ms), "events": int(o.events), "trace": int(o.trace),
-                "status": int(o.status), "monitor_hash": self.monitor_hash}
+                "status": int(o.status), "monitor_hash": self.monitor_hash,
+                "fast_reads": self.fast_reads, "slow_reads": self.slow_reads}
 
 
 def spec_from(s):

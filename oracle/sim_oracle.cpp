@@ -434,7 +434,7 @@ struct Process {
   std::vector<uint32_t> all, all_but_me, majority_q, fast_q, write_q;
   uint64_t next_seq = 0;
   // metrics (base.rs:229-249)
-  uint64_t fast_paths = 0, slow_paths = 0, stable = 0;
+  uint64_t fast_paths = 0, slow_paths = 0, stable = 0, fast_reads = 0, slow_reads = 0;
   KeyDeps key_deps;
   std::map<Dot, Info> cmds;  // SequentialCommandsInfo
   std::map<Dot, std::pair<uint32_t, std::vector<Dot>>> buffered_commits;  // atlas/epaxos
@@ -608,7 +608,10 @@ struct Process {
     } else {
       fast = in.qd.check_equal();
     }
-    if (fast) fast_paths += 1; else slow_paths += 1;
+    if (fast) fast_paths += 1; else slow_paths += 1;  // BaseProcess::path (base.rs:229-243)
+    if (in.cmd.read_only) {
+      if (fast) fast_reads += 1; else slow_reads += 1;
+    }
     if (fast) {
       Msg c;
       c.kind = MK::MCommit;
@@ -837,7 +840,7 @@ struct Result {
   std::vector<std::map<uint32_t, std::vector<Rifl>>> monitors;
   std::map<uint32_t, std::map<uint64_t, uint64_t>> latency;  // region -> (ms -> count)
   std::map<uint32_t, uint64_t> issued;                       // region -> issued
-  std::vector<uint64_t> fast, slow, stable;
+  std::vector<uint64_t> fast, slow, stable, fast_reads, slow_reads;
   std::map<uint64_t, uint64_t> chain, delay;  // executor metrics summed over processes
   uint64_t end_ms = 0, events = 0, trace = 0;
 };
@@ -934,6 +937,8 @@ class Runner {
       r.fast.push_back(p.fast_paths);
       r.slow.push_back(p.slow_paths);
       r.stable.push_back(p.stable);
+      r.fast_reads.push_back(p.fast_reads);
+      r.slow_reads.push_back(p.slow_reads);
       for (auto& kv : p.graph->chain_size) r.chain[kv.first] += kv.second;
       for (auto& kv : p.graph->execution_delay) r.delay[kv.first] += kv.second;
     }
@@ -1293,6 +1298,8 @@ typedef struct oracle_sim_out {
   int32_t status;          // 0 ok, 1 reference assertion, 2 capacity of this buffer
   int32_t pad;
   uint64_t* monitor_hash;  // [n] hash of the ExecutionOrderMonitor (per key, rifls in order), or NULL
+  uint64_t* fast_reads;    // [n] FastPathReads (base.rs:229-243), or NULL
+  uint64_t* slow_reads;    // [n] SlowPathReads, or NULL
 } oracle_sim_out;
 
 static int fill(const simo::Result& r, const fx_sim_spec& s, oracle_sim_out* o) {
@@ -1306,6 +1313,8 @@ static int fill(const simo::Result& r, const fx_sim_spec& s, oracle_sim_out* o) 
     o->fast[p] = r.fast[p];
     o->slow[p] = r.slow[p];
     o->stable[p] = r.stable[p];
+    if (o->fast_reads) o->fast_reads[p] = r.fast_reads[p];
+    if (o->slow_reads) o->slow_reads[p] = r.slow_reads[p];
   }
   for (auto& kv : r.latency)
     for (auto& h : kv.second) {
