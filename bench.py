@@ -44,9 +44,11 @@ LAYOUT = {0: "16 lanes per stream", 1: "one lane per stream", 2: "one lane per s
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["sim", "executor", "huge", "dense", "placements", "pred"], default="sim",
+    ap.add_argument("--mode", choices=["sim", "dense-sim", "executor", "huge", "dense", "placements", "pred"],
+                    default="sim",
                     help="sim: the batched simulator (BASELINE configs[1], the headline); "
-                         "executor: the GraphExecutor alone over synthetic commit streams")
+                         "dense-sim: the simulator on BASELINE configs[3] (64 clients/region, 100%% "
+                         "conflicts); executor: the GraphExecutor alone over synthetic commit streams")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
@@ -56,7 +58,9 @@ def parse(argv=None):
     ap.add_argument("--cmds", type=int, default=None,
                     help="commands per client (sim default 1000, SURVEY.md §8(a) C2; "
                          "executor default 1000)")
-    ap.add_argument("--protocol", choices=["epaxos", "atlas"], default="epaxos")
+    ap.add_argument("--protocol", choices=["epaxos", "atlas", "both"], default="epaxos")
+    ap.add_argument("--clients-per-region", type=int, default=None,
+                    help="sim: clients per region (default 1; dense-sim 64)")
     ap.add_argument("--f", type=int, default=2)
     ap.add_argument("--window", type=int, default=8)
     ap.add_argument("--cycle-pct", type=int, default=30)
@@ -119,7 +123,7 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(launch_ranks(args))
-    if args.mode == "sim":
+    if args.mode in ("sim", "dense-sim"):
         from bench_sim import main_sim
         return main_sim(args)
     if args.mode == "huge":

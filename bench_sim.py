@@ -5,7 +5,13 @@ planet with fantoch_ps/src/bin/simulation.rs's regions (gcp_planet, first n),
 1 client per region, pool 1, 1 key per command, GC and executed
 notifications every 10 ms (the binary's config! macro), Runner::run(None);
 `--seeds` seeds x conflict {0,2,10,50,100}% instances, `--cmds` commands per
-client (default 200 as the binary).  Rank r simulates global instances
+client (default 1000).
+
+bench.py --mode dense-sim: BASELINE configs[3] on the same entry point (the
+large-instance kernel, sim_big.hip): Atlas n=5 f=1 and EPaxos n=5 f=2
+(`--protocol both`, alternating instances), 64 clients per region (320 per
+instance), 100 % conflicts over a pool of 1, `--cmds` commands per client
+(default 50).  Rank r simulates global instances
 [r P, (r + 1) P), P = seeds x rates, each with its own C6 RNG stream, the
 heaviest conflict rate first.  One step = every instance simulated from
 Runner::new to the end of Runner::run in one kernel launch (inputs resident
@@ -26,17 +32,27 @@ METRIC = "executed cmds/sec (node) for batched Atlas/EPaxos sims; % of HBM roofl
 HBM_PEAK_GBPS = 8000.0
 
 
+def protocol_of(S, args, g):
+    """(protocol, f) of global instance g: --protocol both alternates Atlas
+    n f=1 and EPaxos (f = n / 2), the two configs of BASELINE configs[3]."""
+    if args.protocol == "both":
+        return (S.ATLAS, 1) if g % 2 == 0 else (S.EPAXOS, args.n // 2)
+    return (S.EPAXOS if args.protocol == "epaxos" else S.ATLAS), args.f
+
+
 def local_specs(S, args, rank, planet):
+    """Rank r's instances: global ids [r P, (r + 1) P), P = seeds x rates,
+    heaviest conflict rate first; each with its own C6 RNG stream."""
     conflicts = sorted((int(c) for c in args.conflicts.split(",")), reverse=True)
     regs = planet.ids(S.GCP5[:args.n])
-    proto = S.EPAXOS if args.protocol == "epaxos" else S.ATLAS
     per = args.seeds * len(conflicts)
     specs, rates = [], []
     for ci, c in enumerate(conflicts):
         for k in range(args.seeds):
             g = rank * per + ci * args.seeds + k
-            specs.append(S.spec(proto, args.n, args.f, regs, regs, commands_per_client=args.cmds,
-                                conflict_rate=c, seed=args.seed, instance=g))
+            proto, f = protocol_of(S, args, g)
+            specs.append(S.spec(proto, args.n, f, regs, regs, clients_per_region=args.clients_per_region,
+                                commands_per_client=args.cmds, conflict_rate=c, seed=args.seed, instance=g))
             rates.append(c)
     return specs, rates, conflicts
 
@@ -50,6 +66,19 @@ def main_sim(args):
     from fantoch_amd import metrics as fm
     from fantoch_amd import sim as S
 
+    dense = args.mode == "dense-sim"
+    if dense:  # BASELINE configs[3]
+        args.clients_per_region = 64 if args.clients_per_region is None else args.clients_per_region
+        if args.conflicts == "0,2,10,50,100":
+            args.conflicts = "100"
+        if args.protocol == "epaxos" and args.f == 2:
+            args.protocol = "both"
+        if args.seeds == 4096:
+            args.seeds = 2048
+        if args.cmds is None:
+            args.cmds = 50
+    if args.clients_per_region is None:
+        args.clients_per_region = 1
     if args.cmds is None:
         args.cmds = 1000  # 1 client per region, 1k commands
     if args.cpu_baseline_seconds is None:
@@ -73,7 +102,7 @@ def main_sim(args):
     specs, rates, conflicts = local_specs(S, args, rank, planet)
     N = len(specs)
     n = args.n
-    C = n  # one client per region, clients in the process regions
+    C = n * args.clients_per_region  # clients in the process regions
     exec_cap = C * args.cmds + 8
     LAT_BINS, CHAIN_BINS, DELAY_BINS = 8192, 256, 8192
     host = (_lib.SimSpec * N)(*specs)
@@ -95,7 +124,15 @@ def main_sim(args):
                           args.ring_entries, args.dot_slots, 0)
     out = _lib.SimOutput(executed.data_ptr(), executed_len.data_ptr(), None, lat_hist.data_ptr(),
                          chain.data_ptr(), delay.data_ptr(), stats.data_ptr(), err.data_ptr(),
-                         LAT_BINS, CHAIN_BINS, DELAY_BINS, 0)
+                         LAT_BINS, CHAIN_BINS, DELAY_BINS, 0, None)
+    plan = ctypes.c_uint32()
+    large = lib.fx_sim_plan(ctypes.byref(specs[0]), args.ring_entries, args.dot_slots, ctypes.byref(plan)) != 0 \
+        or args.clients_per_region * n > 32
+    arena = ctypes.c_uint64()
+    if large:
+        _lib.check(lib.fx_sim_plan_large(ctypes.byref(specs[0]), args.ring_entries, args.dot_slots,
+                                         ctypes.byref(arena)), "fx_sim_plan_large")
+    kernel_name = "k_simx" if large else "k_sim"
 
     def step():
         lat_hist.zero_()
@@ -190,7 +227,7 @@ def main_sim(args):
                 traffic = None
         copy = measured_copy_gbps(torch, dev)
         roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic, "kernel": "k_sim",
+                "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic, "kernel": kernel_name,
                 "kernel_ms_avg": round(kavg, 3), "alg_bytes_per_launch": int(alg_bytes),
                 "alg_bytes_per_cmd": round(36.0 + 8.0 * dbar, 3),
                 "alg_bytes_definition": "SURVEY.md 8(d): 32 + 4k + 8d per executed command, k = 1, "
@@ -226,13 +263,17 @@ def main_sim(args):
             "dtype": "u32",
             "data": "synthetic: seeded closed-loop clients (canonical C6 RNG), GCP latency matrix",
             "config": {
-                "workload": "%s n=%d f=%d, %d seeds x conflict {%s}%% per GPU, 1 client/region, "
-                            "%d cmds/client, GCP regions %s (BASELINE configs[1])"
-                            % (args.protocol.capitalize(), n, args.f, args.seeds, args.conflicts,
-                               args.cmds, ",".join(S.GCP5[:n])),
+                "workload": ("%s n=%d, %d seeds x conflict {%s}%% per GPU, %d clients/region, "
+                             "%d cmds/client, GCP regions %s (BASELINE configs[%d])"
+                             % ("Atlas f=1 + EPaxos f=%d (alternating)" % (n // 2) if args.protocol == "both"
+                                else "%s f=%d" % (args.protocol.capitalize(), args.f),
+                                n, args.seeds, args.conflicts, args.clients_per_region, args.cmds,
+                                ",".join(S.GCP5[:n]), 3 if dense else 1)),
                 "instances_per_gpu": N, "client_cmds_per_gpu": client_cmds_local,
                 "parallelism": "instances sharded over %d GPU(s) (weak), one wavefront per "
                                "simulated instance" % world,
+                "kernel": kernel_name,
+                "arena_bytes_per_instance": int(arena.value) if large else 0,
             },
             "executed_per_step": int(executed_all),
             "client_cmds_per_s": round(client_all * args.steps / elapsed, 1),
@@ -254,8 +295,9 @@ def main_sim(args):
 
 
 def sim_key(args):
-    return "sim_%s_n%d_f%d_s%d_c%s_m%d_seed%d" % (args.protocol, args.n, args.f, args.seeds,
-                                                 args.conflicts.replace(",", "-"), args.cmds, args.seed)
+    return "sim_%s_n%d_f%d_s%d_c%s_m%d_seed%d%s" % (
+        args.protocol, args.n, args.f, args.seeds, args.conflicts.replace(",", "-"), args.cmds, args.seed,
+        "" if args.clients_per_region == 1 else "_k%d" % args.clients_per_region)
 
 
 def cpu_baseline_sim(args, specs, rates, executed, executed_len, st, lat_hist, n, exec_cap, planet):
