@@ -140,7 +140,7 @@ class ExecutorResultC(ctypes.Structure):
 
 class RequestReplyC(ctypes.Structure):
     _fields_ = [("to_shard", ctypes.c_uint64), ("kind", ctypes.c_uint32), ("dot", CDot), ("rifl", CRifl),
-                ("ndeps", ctypes.c_uint32), ("first_dep", ctypes.c_uint32)]
+                ("ndeps", ctypes.c_uint32), ("first_dep", ctypes.c_uint32), ("cmd_shards", ctypes.c_uint64)]
 
 
 class LogSummary(ctypes.Structure):
@@ -252,7 +252,7 @@ SIGNATURES = [
      [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.POINTER(CDot), ctypes.c_uint32, u32p]),
     ("fx_graph_executor_handle_add_sharded", ctypes.c_int,
      [ctypes.c_void_p, CDot, CRifl, u32p, ctypes.c_uint32, ctypes.c_uint32,
-      ctypes.POINTER(CDot), u32p, ctypes.c_uint32, ctypes.c_uint64]),
+      ctypes.POINTER(CDot), u32p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64]),
     ("fx_graph_executor_handle_executed", ctypes.c_int,
      [ctypes.c_void_p, ctypes.POINTER(CDot), ctypes.c_uint32, ctypes.c_uint64]),
     ("fx_graph_executor_requests", ctypes.c_int,

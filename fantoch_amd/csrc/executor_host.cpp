@@ -28,6 +28,7 @@ struct Cmd {
   fx_rifl rifl;
   std::vector<uint32_t> keys;  // ascending (canonical C11)
   uint32_t read_only;
+  uint64_t shards = 0;  // shards the command has ops on (partial replication)
 };
 
 struct DevBuf {
@@ -100,6 +101,7 @@ struct fx_graph_executor {
     fx_rifl rifl;
     std::vector<fx_dot> deps;
     std::vector<uint32_t> shards;
+    uint64_t cmd_shards = 0;
   };
   std::deque<Reply> replies;
 
@@ -326,7 +328,7 @@ int flush(fx_graph_executor* ex) {
 
 int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys, uint32_t nkeys,
            uint32_t read_only, const fx_dot* deps, uint32_t ndeps, uint64_t now_ms, uint32_t kind,
-           const uint32_t* dep_shards = nullptr) {
+           const uint32_t* dep_shards = nullptr, uint64_t cmd_shards = 0) {
   if (!ex) return FX_ERR_INVALID_ARG;
   if (ex->sticky) return ex->sticky;
   if (ex->executor_index != 0) return FX_ERR_INVALID_ARG;  // mod.rs:220 assert_eq!(executor_index, 0)
@@ -365,6 +367,7 @@ int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys
   std::sort(c.keys.begin(), c.keys.end());
   c.keys.erase(std::unique(c.keys.begin(), c.keys.end()), c.keys.end());
   c.read_only = read_only;
+  c.shards = cmd_shards ? cmd_shards : (1ull << ex->shard_id);
   ex->dots.push_back(FX_PACK_DOT(dot.source, dot.seq - ex->base[dot.source - 1]));
   if (ex->partial && kind == FX_KIND_ADD) ex->rec_of[ex->dots.back()] = (uint32_t)ex->dots.size() - 1;
   ex->hdrs.push_back(FX_MAKE_HDR((uint32_t)(now_ms - ex->t_base), (uint32_t)dv.size(), kind));
@@ -419,10 +422,12 @@ int fx_graph_executor_handle_add(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl
 
 int fx_graph_executor_handle_add_sharded(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys,
                                          uint32_t nkeys, uint32_t read_only, const fx_dot* deps,
-                                         const uint32_t* dep_shards, uint32_t ndeps, uint64_t now_ms) {
+                                         const uint32_t* dep_shards, uint32_t ndeps, uint64_t now_ms,
+                                         uint64_t cmd_shards) {
   if (!ex || (ndeps && !dep_shards)) return FX_ERR_INVALID_ARG;
   if (!ex->partial) return FX_ERR_UNSUPPORTED;
-  return append(ex, dot, rifl, keys, nkeys, read_only, deps, ndeps, now_ms, FX_KIND_ADD, dep_shards);
+  if (cmd_shards && !((cmd_shards >> ex->shard_id) & 1u)) return FX_ERR_INVALID_ARG;  // a command of this shard
+  return append(ex, dot, rifl, keys, nkeys, read_only, deps, ndeps, now_ms, FX_KIND_ADD, dep_shards, cmd_shards);
 }
 
 int fx_graph_executor_handle_executed(fx_graph_executor* ex, const fx_dot* dots, uint32_t n, uint64_t now_ms) {
@@ -516,7 +521,10 @@ int process_requests(fx_graph_executor* c, uint64_t from, const std::set<std::pa
       it = m->rec_of.find(dd);
     }
     if (it != m->rec_of.end() && !m->executed_set.count(dd)) {
-      fx_graph_executor::Reply r{from, true, src, seq, m->cmds[it->second].rifl, {}, {}};
+      const Cmd& cmd = m->cmds[it->second];
+      // the requesting shard replicates the command: the reference panics (graph/mod.rs:308-316)
+      if (from < 64 && ((cmd.shards >> from) & 1u)) return FX_ERR_INVALID_ARG;
+      fx_graph_executor::Reply r{from, true, src, seq, cmd.rifl, {}, {}, cmd.shards};
       for (uint32_t x : m->deps[it->second]) {
         const uint32_t s2 = FX_DOT_SRC(x);
         r.deps.push_back(fx_dot{s2, FX_DOT_SEQ(x) + (s2 >= 1 && s2 <= m->nsrc ? m->base[s2 - 1] : 0)});
@@ -569,7 +577,7 @@ int fx_graph_executor_request_replies(fx_graph_executor* ex, fx_request_reply* o
     const auto& r = ex->replies.front();
     if (k + r.deps.size() > deps_cap) break;
     out[c] = fx_request_reply{r.to, r.info ? 1u : 0u, fx_dot{r.src, (uint32_t)r.seq}, r.rifl,
-                              (uint32_t)r.deps.size(), k};
+                              (uint32_t)r.deps.size(), k, r.info ? r.cmd_shards : 0u};
     for (size_t j = 0; j < r.deps.size(); ++j, ++k) {
       deps[k] = r.deps[j];
       dep_shards[k] = r.shards[j];

@@ -508,6 +508,14 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
       nseg_used += h_nseg[s];
     }
   }
+  if (NS >= (1ull << 31)) {  // too many segments for one batch: every stream runs whole
+    for (uint32_t s = 0; s < S; ++s)
+      if (!h_whole[s]) {
+        h_whole[s] = 1;
+        whole_list.push_back(s);
+      }
+    nseg_used = 0;
+  }
   uint32_t* whole = db.alloc<uint32_t>(S);
   uint32_t* fail = db.alloc<uint32_t>(S, 0);
   if (!whole || !fail) return FX_ERR_HIP;
@@ -516,7 +524,7 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
     stats->segments = nseg_used;
     stats->max_segment = seg_steps;
   }
-  if (NS && NS < (1ull << 31) && nseg_used) {
+  if (nseg_used) {
     // 4. the segment batch: one stream per segment
     const uint32_t SS = (uint32_t)NS;
     Seg sg;
@@ -542,8 +550,10 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
     hipLaunchKernelGGL(k_scatter, dim3(grid_for((uint64_t)SS * seg_steps)), dim3(BT), 0, hs, (uint64_t)SS, seg_steps,
                        seg_stream, seg_start, sg.lengths, sorder, srelease, snexec, serr, in.steps, out->order,
                        out->release, fail);
-    hipLaunchKernelGGL(k_finish, dim3((S + 255) / 256), dim3(256), 0, hs, in, whole, fail, out->nexec, out->err);
   }
+  // every stream that neither runs whole nor failed a segment executed all
+  // its Adds — including the empty ones, which have no segment at all
+  hipLaunchKernelGGL(k_finish, dim3((S + 255) / 256), dim3(256), 0, hs, in, whole, fail, out->nexec, out->err);
   std::vector<uint32_t> h_fail(S);
   (void)hipMemcpyAsync(h_fail.data(), fail, (size_t)S * 4, hipMemcpyDeviceToHost, hs);
   if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;

@@ -531,8 +531,9 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
 
 }  // namespace wide
 
-// LDS tables: 1024 vertices, 2048 index slots per source, 2048-bit windows;
-// HBM tables: 16384 vertices, 32768 index slots, 32768-bit windows, dep rows of
+// LDS tables: 512 vertices, 512 index slots per source, 1024-bit windows
+// (32 words); HBM tables: 16384 vertices, 32768 index slots, 32768-bit
+// windows, dep rows of
 // the widest Add (31) so a saved table stays valid when later Adds are wider
 static wide::Lay wide_layout(bool hbm, uint32_t n, uint32_t dmax, bool partial = false) {
   wide::Lay L;

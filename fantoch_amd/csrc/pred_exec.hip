@@ -287,6 +287,9 @@ struct Pr {
     const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.k.dot[at]);
     const uint32_t src = FX_DOT_SRC(d);
     if (src < 1 || src > L.n || FX_DOT_SEQ(d) == 0) { err = FX_ERR_DOT_RANGE; return; }
+    // assert!(self.committed_clock.add(..)) (mod.rs:123): a dot commits once,
+    // also after it executed (its index slot is gone by then)
+    if (contains(L.cfront, L.cbits, d)) { err = FX_ERR_DOUBLE_INDEX; return; }
     clock_add(L.cfront, L.cbits, d);
     if (a.k.flags & FX_FLAG_EXECUTE_AT_COMMIT) {
       execute(d, r);

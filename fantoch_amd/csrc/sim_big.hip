@@ -156,6 +156,22 @@ __device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
 
 enum : uint32_t { FOUND = 0, MISSING = 1 };
 
+// FX_SIM_PROFILE builds (make prof): shader-clock cycles and counts per phase
+// in the stats rows (slots 0-23) instead of the counters (tools/simx_phase.py)
+#ifdef FX_SIM_PROFILE
+#define XPROF_T0() const uint64_t xprof_t0_ = __builtin_amdgcn_s_memtime()
+#define XPROF_ADD(cat) prof[cat] += __builtin_amdgcn_s_memtime() - xprof_t0_
+#define XPROF_CNT(cat, v) prof[cat] += (v)
+#else
+#define XPROF_T0() (void)0
+#define XPROF_ADD(cat) (void)0
+#define XPROF_CNT(cat, v) (void)0
+#endif
+enum : uint32_t { PF_POP = 0, PF_EVENT = 1, PF_XADD = 2, PF_FIND = 3, PF_CHECK = 4, PF_SORT = 5, PF_EMIT = 6,
+                  PF_HANDLER = 7, PF_SEND = 8, PF_GC = 9, PF_CLIENT = 10,
+                  PC_EDGES = 16, PC_RECURSE = 17, PC_XADD = 18, PC_FIND = 19, PC_WAITERS = 20, PC_FAST = 21,
+                  PC_EVENTS = 22, PC_SEND = 23 };
+
 // NG: registers of group minima per lane (message pool <= 4096 NG entries)
 template <uint32_t NG>
 struct Big {
@@ -198,6 +214,9 @@ struct Big {
   uint32_t nfrm = 0, xinfo = NONE, rtop = 0;
   // executor (the process being run)
   uint32_t xp = 0, xk = 0, epoch = 0, nwl = 0, idc = 0, tsp = 0, fsp = 0;
+#ifdef FX_SIM_PROFILE
+  uint64_t prof[24] = {};
+#endif
 
   // ------------------------------------------------------------ arena views
   __device__ __forceinline__ uint32_t& S(uint32_t sl, uint32_t w) { return M[g.o_slot + sl * g.SW + w]; }
@@ -799,7 +818,12 @@ struct Big {
   // pushed to the worklist
   __device__ __forceinline__ void save_scc(uint32_t base, uint32_t cnt) {
     hist_chain(cnt);
-    sort_slots(g.o_tstk + base, cnt, g.o_tl);
+    {
+      XPROF_T0();
+      sort_slots(g.o_tstk + base, cnt, g.o_tl);
+      XPROF_ADD(PF_SORT);
+    }
+    XPROF_T0();
     for (uint32_t r = 0; r < cnt && !err; ++r) {
       const uint32_t sl = rd(W(g.o_tl, r));
       const uint32_t d = rd(S(sl, SL_DOT));
@@ -811,6 +835,7 @@ struct Big {
       put(W(g.o_wl, nwl++), sl);
       on_execute(sl, d, st);
     }
+    XPROF_ADD(PF_EMIT);
   }
 
   // find_scc (mod.rs:409-486) + strong_connect (tarjan.rs:96-316) + finalize
@@ -818,6 +843,13 @@ struct Big {
   // *missing = it and the vertices left on the stack are marked visited with
   // mark_epoch (0 = no marks).
   __device__ __forceinline__ uint32_t find_scc(uint32_t rsl, uint32_t* missing, uint32_t mark_epoch, bool* saved) {
+    XPROF_T0();
+    XPROF_CNT(PC_FIND, 1);
+    const uint32_t r = find_scc_(rsl, missing, mark_epoch, saved);
+    XPROF_ADD(PF_FIND);
+    return r;
+  }
+  __device__ __forceinline__ uint32_t find_scc_(uint32_t rsl, uint32_t* missing, uint32_t mark_epoch, bool* saved) {
     const uint32_t p = xp;
     *saved = false;
     idc = 1;
@@ -841,6 +873,7 @@ struct Big {
       if (ci < cnd) {
         const uint32_t d = rl(drow, ci);
         ++ci;
+        XPROF_CNT(PC_EDGES, 1);
         if (d == cdot || !src_ok(d)) continue;  // self (tarjan.rs:128-130)
         const uint32_t sl = hslot(d);
         if (rd(S(sl, SL_DOT)) != d) continue;  // executed everywhere (tarjan.rs:131-145)
@@ -853,6 +886,7 @@ struct Big {
         }
         const uint32_t tw = rd(RC(sl, p, R_TL)), mk = rd(RC(sl, p, R_MARK));
         if ((tw & 0xFFFFu) == 0) {  // recurse (tarjan.rs:172-214)
+          XPROF_CNT(PC_RECURSE, 1);
           put(W(g.o_fi, fsp - 1u), ci);
           put(RC(cv, p, R_TL), cid | (clow << 16));
           ++idc;
@@ -919,6 +953,11 @@ struct Big {
   // check_pending (mod.rs:556-587) + try_pending (589-642): LIFO over the
   // released dots; each one's waiters in ascending dot order (C2)
   __device__ __forceinline__ void check_pending() {
+    XPROF_T0();
+    check_pending_();
+    XPROF_ADD(PF_CHECK);
+  }
+  __device__ __forceinline__ void check_pending_() {
     const uint32_t p = xp;
     while (nwl && !err) {
       const uint32_t x = rd(W(g.o_wl, --nwl));
@@ -939,6 +978,7 @@ struct Big {
         put(RC(sl, p, R_NEXT), 0u);
         put(RC(sl, p, R_PREV), 0u);
       }
+      XPROF_CNT(PC_WAITERS, cnt);
       sort_slots(g.o_tmp, cnt, g.o_tw);
       // visited-skip set = vertices marked with this epoch
       uint32_t cur = ++epoch;
@@ -962,6 +1002,12 @@ struct Big {
 
   // GraphExecutor::handle(Add) (executor.rs:69-80) -> handle_add (mod.rs:213-275)
   __device__ __forceinline__ void x_add(uint32_t p, uint32_t sl) {
+    XPROF_T0();
+    XPROF_CNT(PC_XADD, 1);
+    x_add_(p, sl);
+    XPROF_ADD(PF_XADD);
+  }
+  __device__ __forceinline__ void x_add_(uint32_t p, uint32_t sl) {
     xp = p;
     xk = rl(pexec, p);
     nwl = 0;
@@ -977,6 +1023,7 @@ struct Big {
     bool keep = false;
     if (lid < vc && depj != d) keep = !contains_v(depj);
     if (!bal(keep)) {  // every dep executed: a singleton SCC
+      XPROF_CNT(PC_FAST, 1);
       put(RC(sl, p, R_PST), ps | PS_EXEC);
       hist_chain(1u);
       put(W(g.o_wl, nwl++), sl);
@@ -1005,8 +1052,11 @@ struct Big {
     xinfo = NONE;
   }
   __device__ __forceinline__ void send_p(uint32_t from, uint32_t to, uint32_t kind, uint32_t dot) {
+    XPROF_T0();
+    XPROF_CNT(PC_SEND, 1);
     const uint32_t d = msg_delay(rl(dpq, from * 8u + to));
     push_event(now + d, 0u, kind | (from << 4) | (to << 8), dot);
+    XPROF_ADD(PF_SEND);
   }
 
   // handle_send_to_proc / handle_submit_to_proc, then
@@ -1023,6 +1073,7 @@ struct Big {
         pend = false;
         frame_push();
         if (err) return;
+        XPROF_T0();
         switch (kind) {
           case M_SUBMIT: h_submit(p, w2); break;
           case M_COLLECT: h_mcollect(p, from, w2); break;
@@ -1032,6 +1083,7 @@ struct Big {
           case M_CONSENSUS_ACK: h_mconsensusack(p, from, w2); break;
           default: err = FX_ERR_INVALID_ARG;
         }
+        XPROF_ADD(PF_HANDLER);
         if (xinfo != NONE && !err) {  // to_executors (<= 1 per handler)
           const uint32_t sl = xinfo;
           xinfo = NONE;
@@ -1096,6 +1148,7 @@ struct Big {
         return;
       }
       case E_CLIENT: {  // Client::cmd_recv + cmd_send (simulation.rs:132-149)
+        XPROF_T0();
         const uint32_t c = arg;
         const uint32_t issued = rd(CL(c, 1));
         note(4, c + 1, 0, issued);
@@ -1115,18 +1168,25 @@ struct Big {
             }
           }
         }
+        XPROF_ADD(PF_CLIENT);
         return;
       }
-      case E_TICK:
+      case E_TICK: {
+        XPROF_T0();
         gc_tick(to);
         push_event(now + gc_ms, (1u << 6) | (to << 3), E_TICK | (to << 8), 0);
+        XPROF_ADD(PF_GC);
         return;
+      }
       case E_NOTIF:  // GraphExecutor::executed is None (executor/mod.rs:74-79)
         push_event(now + en_ms, 0u, E_NOTIF | (to << 8), 0);
         return;
-      case M_GC:
+      case M_GC: {
+        XPROF_T0();
         gc_deliver(to, from, gcv);
+        XPROF_ADD(PF_GC);
         return;
+      }
       default:
         note(3, to + 1, from + 1, ((uint64_t)kind << 32) | arg);
         run_handlers(to, from, kind, arg);
@@ -1255,7 +1315,15 @@ __global__ __launch_bounds__(64) void k_simx(ArgsX a) {
   const uint64_t max_events = a.max_events ? a.max_events : 0xFFFFFFFFull;
   while (!s.done && !s.err) {
     uint32_t hi = 0;
+#ifdef FX_SIM_PROFILE
+    const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#endif
     const uint32_t e = s.pop_event(hi);
+#ifdef FX_SIM_PROFILE
+    const uint64_t pt1 = __builtin_amdgcn_s_memtime();
+    s.prof[PF_POP] += pt1 - pt0;
+    s.prof[PC_EVENTS] += 1;
+#endif
     if (e == NONE) {
       s.err = FX_ERR_SIM_LATE;  // "there should be a new action"
       break;
@@ -1271,6 +1339,9 @@ __global__ __launch_bounds__(64) void k_simx(ArgsX a) {
     const uint32_t gcv = kind == M_GC && s.lid < n ? M[g.o_gp + e * n + s.lid] : 0u;
     s.free_event(e);
     s.run_event(kind, from, to, arg, gcv);
+#ifdef FX_SIM_PROFILE
+    s.prof[PF_EVENT] += __builtin_amdgcn_s_memtime() - pt1;
+#endif
     if (s.in_extra && s.now > s.final_ms) s.done = true;
     if (s.events >= max_events) s.err = FX_ERR_SIM_EVENTS;
   }
@@ -1295,6 +1366,9 @@ __global__ __launch_bounds__(64) void k_simx(ArgsX a) {
       st[FX_SIM_STAT_DEPS] = s.deps_total;
       st[FX_SIM_STAT_LAT_SUM] = s.lat_sum;
       st[FX_SIM_STAT_ERR_SITE] = s.err_site;
+#ifdef FX_SIM_PROFILE
+      for (uint32_t i = 0; i < 24; ++i) st[i] = s.prof[i];
+#endif
     }
   }
   for (uint32_t i = s.lid; i < HC_BINS + HD_BINS; i += 64) {

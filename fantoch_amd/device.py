@@ -88,6 +88,9 @@ def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096,
     release.fill_bytes(0xFF)  # rows a stream never reaches (an error) stay FX_RELEASE_NONE
     nexec = DeviceBuffer(S * 4)
     err = DeviceBuffer(S * 4)
+    # every driver writes every stream's count and status: a sentinel shows any it skipped
+    nexec.fill_bytes(0xAB)
+    err.fill_bytes(0xAB)
     inb = _lib.StreamBatch(bufs["dot"].ptr, bufs["hdr"].ptr, bufs["deps"].ptr,
                            lengths.ptr if lengths else None, S, steps, planes.dmax, planes.n)
     outb = _lib.OrderBatch(order.ptr, release.ptr, nexec.ptr, err.ptr)

@@ -54,8 +54,9 @@ class GraphExecutor:
             len(deps), int(time_ms)), "handle_add")
 
     # ---- partial replication (shard_count > 1, graph/mod.rs:82-406)
-    def handle_add_sharded(self, dot, rifl, keys, deps, shards, time_ms, read_only=False):
-        """handle(Add) / RequestReply::Info with each dep's shard bitmask."""
+    def handle_add_sharded(self, dot, rifl, keys, deps, shards, time_ms, read_only=False, cmd_shards=0):
+        """handle(Add) / RequestReply::Info with each dep's shard bitmask;
+        cmd_shards = the command's own shard set (0 = this shard only)."""
         keys = list(keys)
         karr = (ctypes.c_uint32 * max(len(keys), 1))(*keys)
         deps = list(deps)
@@ -63,7 +64,7 @@ class GraphExecutor:
         sarr = (ctypes.c_uint32 * max(len(deps), 1))(*[int(m) for m in shards])
         check(_lib.load().fx_graph_executor_handle_add_sharded(
             self._h, CDot(*dot), CRifl(*rifl), karr, len(keys), 1 if read_only else 0, darr, sarr,
-            len(deps), int(time_ms)), "handle_add_sharded")
+            len(deps), int(time_ms), int(cmd_shards)), "handle_add_sharded")
 
     def handle_executed(self, dots, time_ms):
         """RequestReply::Executed for each dot."""
@@ -218,8 +219,9 @@ class ExecutorClone:
     def cleanup(self):
         check(_lib.load().fx_graph_executor_cleanup(self._h), "cleanup")
 
-    def replies(self):
-        """Drains [(to shard, 'info' | 'executed', dot, [(dep, shards)])]."""
+    def replies(self, with_cmd_shards=False):
+        """Drains [(to shard, 'info' | 'executed', dot, [(dep, shards)])] (plus
+        each Info's command shard set when with_cmd_shards)."""
         out = []
         buf = (_lib.RequestReplyC * 256)()
         deps = (CDot * 8192)()
@@ -232,6 +234,7 @@ class ExecutorClone:
                 r = buf[i]
                 d = [((deps[r.first_dep + j].source, deps[r.first_dep + j].seq), sh[r.first_dep + j])
                      for j in range(r.ndeps)]
-                out.append((r.to_shard, "info" if r.kind else "executed", (r.dot.source, r.dot.seq), d))
+                row = (r.to_shard, "info" if r.kind else "executed", (r.dot.source, r.dot.seq), d)
+                out.append(row + (int(r.cmd_shards),) if with_cmd_shards else row)
             if got.value < 256:
                 return out

@@ -380,7 +380,11 @@ int fx_graph_executor_handle_add(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl
 int fx_graph_executor_handle_add_sharded(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl,
                                          const uint32_t* keys, uint32_t nkeys, uint32_t read_only,
                                          const fx_dot* deps, const uint32_t* dep_shards, uint32_t ndeps,
-                                         uint64_t now_ms);
+                                         uint64_t now_ms, uint64_t cmd_shards);
+/* cmd_shards: the shards the command has ops on (Command::replicated_by,
+ * command.rs:90-92) as a bitmask; 0 = this handle's shard only.  A Request for
+ * a pending dot from a shard that replicates it is the reference's panic
+ * (graph/mod.rs:308-316): FX_ERR_INVALID_ARG from handle_request / cleanup. */
 int fx_graph_executor_handle_executed(fx_graph_executor* ex, const fx_dot* dots, uint32_t n, uint64_t now_ms);
 int fx_graph_executor_requests(fx_graph_executor* ex, uint64_t* shards, fx_dot* dots, uint32_t cap,
                                uint32_t* n_out);
@@ -402,6 +406,7 @@ typedef struct fx_request_reply {
   fx_rifl rifl;       /* Info: the command's rifl */
   uint32_t ndeps;     /* Info: deps at deps[first_dep, first_dep + ndeps) */
   uint32_t first_dep;
+  uint64_t cmd_shards; /* Info: the command's shard set (cmd.shards(), as the reference ships the cmd) */
 } fx_request_reply;
 fx_graph_executor* fx_graph_executor_clone(fx_graph_executor* main);
 int fx_graph_executor_handle_executed_info(fx_graph_executor* ex, const fx_dot* dots, uint32_t n);

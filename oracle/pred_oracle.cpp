@@ -60,7 +60,8 @@ class PredecessorsGraph {  // mod.rs:28-384
 
   // mod.rs:104-152; false on the double-index panic (mod.rs:284-289)
   bool add(const Dot& dot, uint32_t rec, uint64_t clock, std::vector<Dot> deps) {
-    committed.add(dot.source, dot.sequence);
+    // assert!(self.committed_clock.add(..)) (mod.rs:123): a dot commits once
+    if (!committed.add(dot.source, dot.sequence)) return false;
     if (execute_at_commit) {
       execute(dot, rec);
       return true;

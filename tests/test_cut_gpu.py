@@ -21,14 +21,13 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("case", [
     dict(n=5, instances=8, cmds=400, window=8, cycle_pct=30, conflicts=(2, 50, 100)),
     dict(n=3, instances=16, cmds=300, window=6, cycle_pct=60, conflicts=(10, 100)),
-    # long SCC chains: segments over 256 steps send streams to the whole path
-    dict(n=7, instances=4, cmds=200, window=16, cycle_pct=60, conflicts=(100,), whole_ok=True),
+    # long SCC chains at 100 % conflicts: most streams still split
+    dict(n=7, instances=4, cmds=200, window=16, cycle_pct=60, conflicts=(100,)),
     dict(n=5, instances=8, cmds=200, window=0, cycle_pct=0, conflicts=(0, 100)),
     dict(n=2, instances=33, cmds=77, window=5, cycle_pct=40, conflicts=(50,)),
 ])
 def test_cut_matches_oracle(case):
     case = dict(case)
-    whole_ok = case.pop("whole_ok", False)
     p = fs.synth_params(seed=11, **case)
     planes = fs.synth_host(p)
     res = fd.run_batch(planes, cut=True, nbins_chain=64, nbins_delay=4096)
@@ -38,7 +37,7 @@ def test_cut_matches_oracle(case):
     assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
     st = res.cut_stats
     assert st.failed_streams == 0
-    assert whole_ok or (st.whole_streams == 0 and st.segments > planes.S)
+    assert st.whole_streams == 0 and st.segments > planes.S
 
 
 def test_cut_ragged_lengths():
@@ -94,3 +93,33 @@ def test_config4_single_huge_instance_cut():
     assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
     print("configs[4]: GPU cut driver %.3f s (incl. host<->device copies), oracle+compare %.3f s, "
           "%d segments, longest %d" % (t_gpu, t_cpu, res.cut_stats.segments, res.cut_stats.max_segment))
+
+
+def test_cut_every_stream_empty():
+    """All lengths 0: no segment at all; every stream still gets nexec = 0 and
+    FX_OK (the outputs start as a sentinel, device.run_batch)."""
+    p = fs.synth_params(seed=8, instances=4, n=3, cmds=20, window=4, cycle_pct=20, conflicts=(50,))
+    planes = fs.synth_host(p)
+    planes.lengths = np.zeros(planes.S, np.uint32)
+    res = fd.run_batch(planes, cut=True)
+    assert res.status == _lib.FX_OK
+    assert np.all(res.nexec == 0) and np.all(res.err == _lib.FX_OK)
+
+
+def test_cut_empty_stream_beside_unsplittable_only():
+    """One empty stream next to streams that all run whole (a dep that never
+    arrives): the empty one is still written."""
+    n = 3
+    streams = [
+        [((1, 1), [], 1), ((2, 1), [(3, 9)], 2)],  # (3, 9) never arrives: runs whole
+        [],
+        [((2, 1), [(1, 7)], 1), ((1, 1), [], 2)],  # (1, 7) never arrives
+    ]
+    planes = fs.pack_streams(streams, n)
+    res = fd.run_batch(planes, cut=True)
+    ref = fd.run_batch(planes)
+    assert res.status == _lib.FX_OK
+    assert np.array_equal(res.err, ref.err) and np.array_equal(res.nexec, ref.nexec)
+    assert res.nexec[1] == 0 and res.err[1] == _lib.FX_OK
+    assert res.cut_stats.whole_streams == 2
+    assert_parity(planes, res)

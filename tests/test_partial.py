@@ -73,3 +73,24 @@ def test_gpu_clone_serves_requests_like_oracle(seed):
     assert len(lo) == len(lg)
     for k, (a, b) in enumerate(zip(lo, lg)):
         assert a == b, k
+
+
+@pytest.mark.gpu
+def test_gpu_request_from_replicating_shard_is_an_error():
+    """process_requests panics when the requesting shard replicates the
+    pending command (graph/mod.rs:308-316, Command::replicated_by): here an
+    FX_ERR_INVALID_ARG; a request from a shard that does not replicate it gets
+    an Info carrying the command's shard set (the reference ships the cmd)."""
+    from fantoch_amd import _lib
+    from fantoch_amd.executor import GraphExecutor
+    ex = GraphExecutor(1, 0, 2, shard_count=3, monitor=False)
+    # (1, 1) waits on (3, 1), a command of shard 1: it stays pending
+    ex.handle_add_sharded((1, 1), (1, 1), [0], [(3, 1)], [0b010], 1, cmd_shards=0b101)
+    c = ex.clone()
+    c.handle_request(1, [(1, 1)])  # shard 1 does not replicate (1, 1)
+    rep = c.replies(with_cmd_shards=True)
+    assert [(r[0], r[1], r[2], r[4]) for r in rep] == [(1, "info", (1, 1), 0b101)]
+    with pytest.raises(_lib.FxError) as e:
+        c.handle_request(2, [(1, 1)])  # shard 2 replicates it
+    assert e.value.status == _lib.FX_ERR_INVALID_ARG
+    c.close()

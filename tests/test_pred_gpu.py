@@ -71,6 +71,11 @@ def test_execute_at_commit_and_errors():
     dup = [((1, 1), [(2, 1)], 0, (2, 1)), ((1, 1), [], 1, (3, 1))]
     planes, res = check([dup, P.SIMPLE], 2)
     assert res.err[0] == _lib.FX_ERR_DOUBLE_INDEX
+    # a dot committed again after it executed (pred/mod.rs:123 asserts the
+    # committed clock's add): an error, not a second execution
+    again = [((1, 1), [], 0, (1, 1)), ((2, 1), [(1, 1)], 1, (2, 1)), ((1, 1), [], 2, (3, 1))]
+    planes, res = check([again, P.SIMPLE], 2)
+    assert res.err[0] == _lib.FX_ERR_DOUBLE_INDEX and res.nexec[0] == 2
 
 
 def test_very_wide_deps():
