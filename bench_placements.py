@@ -41,6 +41,48 @@ def enumerate_placements(R, limit=None):
     return out
 
 
+def rank_range(P, rank, world):
+    """Rank r's contiguous share [r P / N, (r + 1) P / N) of the placements."""
+    return rank * P // world, (rank + 1) * P // world
+
+
+ROW_FIELDS = ["placement", "n", "f", "executed", "latency_sum", "client_cmds", "fast_paths", "slow_paths",
+              "status"]
+
+
+def placement_rows(torch, ids, allp, n, cmds, executed_len, stats, err):
+    """[len(ids), 9] int64 rows (ROW_FIELDS) of one launch (geometry n)."""
+    from fantoch_amd import _lib
+    N = len(ids)
+    dev = executed_len.device
+    st = stats.view(N, _lib.FX_SIM_STATS)
+    t = torch.tensor(ids, dtype=torch.int64, device=dev)
+    fs_ = torch.tensor([allp[g][1] for g in ids], dtype=torch.int64, device=dev)
+    return torch.stack([t, torch.full_like(t, n), fs_, executed_len.view(N, n).to(torch.int64).sum(1),
+                        st[:, _lib.FX_SIM_STAT_LAT_SUM], torch.full_like(t, n * cmds),
+                        st[:, _lib.FX_SIM_STAT_FAST:_lib.FX_SIM_STAT_FAST + n].sum(1),
+                        st[:, _lib.FX_SIM_STAT_SLOW:_lib.FX_SIM_STAT_SLOW + n].sum(1),
+                        err.to(torch.int64)], 1)
+
+
+def gather_rows(dist, world, rows):
+    """all_gather of per-rank row blocks of different sizes (padded to the
+    largest) -> every rank's rows, sorted by placement id."""
+    import torch
+    if world > 1:
+        dev = rows.device
+        cnt = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
+        counts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(counts, cnt)
+        mx = int(max(c.item() for c in counts))
+        pad = torch.full((mx, rows.shape[1]), -1, dtype=torch.int64, device=dev)
+        pad[:rows.shape[0]] = rows
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad)
+        rows = torch.cat([p[:int(c.item())] for p, c in zip(parts, counts)])
+    return rows[torch.argsort(rows[:, 0])] if rows.shape[0] else rows
+
+
 def main_placements(args):
     import torch
     import torch.distributed as dist
@@ -67,7 +109,7 @@ def main_placements(args):
     planet = S.Planet()
     allp = enumerate_placements(planet.R, args.placement_limit)
     P = len(allp)
-    lo, hi = rank * P // world, (rank + 1) * P // world
+    lo, hi = rank_range(P, rank, world)
     mine = list(range(lo, hi))
     stream = torch.cuda.current_stream(dev)
     hs = ctypes.c_void_p(stream.cuda_stream)
@@ -125,40 +167,21 @@ def main_placements(args):
     elapsed = time.perf_counter() - t0
 
     # per-placement rows: id, n, f, executed, latency sum, client commands, fast, slow, status
-    rows = []
-    for L in launches:
-        N, n = len(L["ids"]), L["n"]
-        st = L["stats"].view(N, _lib.FX_SIM_STATS)
-        ids = torch.tensor(L["ids"], dtype=torch.int64, device=dev)
-        fs_ = torch.tensor([allp[g][1] for g in L["ids"]], dtype=torch.int64, device=dev)
-        rows.append(torch.stack([ids, torch.full_like(ids, n), fs_,
-                                 L["executed_len"].view(N, n).to(torch.int64).sum(1),
-                                 st[:, _lib.FX_SIM_STAT_LAT_SUM], torch.full_like(ids, n * cmds),
-                                 st[:, _lib.FX_SIM_STAT_FAST:_lib.FX_SIM_STAT_FAST + n].sum(1),
-                                 st[:, _lib.FX_SIM_STAT_SLOW:_lib.FX_SIM_STAT_SLOW + n].sum(1),
-                                 L["err"].to(torch.int64)], 1))
-    rows = torch.cat(rows) if rows else torch.zeros((0, 9), dtype=torch.int64, device=dev)
+    rows = [placement_rows(torch, L["ids"], allp, L["n"], cmds, L["executed_len"], L["stats"], L["err"])
+            for L in launches]
+    rows = torch.cat(rows) if rows else torch.zeros((0, len(ROW_FIELDS)), dtype=torch.int64, device=dev)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        cnt = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
-        counts = [torch.zeros_like(cnt) for _ in range(world)]
-        dist.all_gather(counts, cnt)
-        mx = int(max(c.item() for c in counts))
-        pad = torch.full((mx, 9), -1, dtype=torch.int64, device=dev)
-        pad[:rows.shape[0]] = rows
-        parts = [torch.empty_like(pad) for _ in range(world)]
-        dist.all_gather(parts, pad)
-        rows = torch.cat([p[:int(c.item())] for p, c in zip(parts, counts)])
         for h in (lat_hist, chain, delay):
             dist.all_reduce(h)
+    rows = gather_rows(dist, world, rows)
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return None
     R = rows.cpu().numpy()
-    R = R[np.argsort(R[:, 0])]
     executed_all = int(R[:, 3].sum())
     value = executed_all * args.steps / elapsed
     best = {}

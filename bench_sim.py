@@ -40,21 +40,69 @@ def protocol_of(S, args, g):
     return (S.EPAXOS if args.protocol == "epaxos" else S.ATLAS), args.f
 
 
+def rate_list(args):
+    """Conflict rates, heaviest first (the instances of a rank are rate-major)."""
+    return sorted((int(c) for c in args.conflicts.split(",")), reverse=True)
+
+
+def global_spec(S, args, g, regs):
+    """Global instance g: rank g // P's instance g % P, P = seeds x rates,
+    rate-major (heaviest first), with its own C6 RNG stream (instance = g)."""
+    conflicts = rate_list(args)
+    per = args.seeds * len(conflicts)
+    c = conflicts[(g % per) // args.seeds]
+    proto, f = protocol_of(S, args, g)
+    return S.spec(proto, args.n, f, regs, regs, clients_per_region=args.clients_per_region,
+                  commands_per_client=args.cmds, conflict_rate=c, seed=args.seed, instance=g), c
+
+
 def local_specs(S, args, rank, planet):
-    """Rank r's instances: global ids [r P, (r + 1) P), P = seeds x rates,
-    heaviest conflict rate first; each with its own C6 RNG stream."""
-    conflicts = sorted((int(c) for c in args.conflicts.split(",")), reverse=True)
+    """Rank r's instances: the contiguous global range [r P, (r + 1) P)."""
+    conflicts = rate_list(args)
     regs = planet.ids(S.GCP5[:args.n])
     per = args.seeds * len(conflicts)
     specs, rates = [], []
-    for ci, c in enumerate(conflicts):
-        for k in range(args.seeds):
-            g = rank * per + ci * args.seeds + k
-            proto, f = protocol_of(S, args, g)
-            specs.append(S.spec(proto, args.n, f, regs, regs, clients_per_region=args.clients_per_region,
-                                commands_per_client=args.cmds, conflict_rate=c, seed=args.seed, instance=g))
-            rates.append(c)
+    for g in range(rank * per, (rank + 1) * per):
+        sp, c = global_spec(S, args, g, regs)
+        specs.append(sp)
+        rates.append(c)
     return specs, rates, conflicts
+
+
+ROW_FIELDS = ["instance", "conflict_pct", "executed", "fast_paths", "slow_paths", "status"]
+
+
+def instance_rows(torch, gid0, rates, executed_len, stats, err, n):
+    """[instances, 6] int64 rows (ROW_FIELDS) of one rank's batch: executed
+    summed over the n processes, Fast / Slow paths summed, the FX_* status."""
+    from fantoch_amd import _lib
+    N = len(rates)
+    dev = executed_len.device
+    st = stats.view(N, _lib.FX_SIM_STATS)
+    gid = torch.arange(N, dtype=torch.int64, device=dev) + gid0
+    return torch.stack([gid, torch.tensor(rates, dtype=torch.int64, device=dev),
+                        executed_len.view(N, n).to(torch.int64).sum(1),
+                        st[:, _lib.FX_SIM_STAT_FAST:_lib.FX_SIM_STAT_FAST + n].sum(1),
+                        st[:, _lib.FX_SIM_STAT_SLOW:_lib.FX_SIM_STAT_SLOW + n].sum(1),
+                        err.to(torch.int64)], 1)
+
+
+def allreduce_hists(dist, world, hists):
+    """The step's output: histograms summed over every rank's instances
+    (exact integers, so identical for any number of ranks; RCCL on GPUs)."""
+    if world > 1:
+        for h in hists:
+            dist.all_reduce(h)
+
+
+def gather_rows(dist, world, rows):
+    """One all_gather of the equal-sized per-rank row blocks -> global order."""
+    import torch
+    if world <= 1:
+        return rows
+    parts = [torch.empty_like(rows) for _ in range(world)]
+    dist.all_gather(parts, rows.contiguous())
+    return torch.cat(parts)
 
 
 def main_sim(args):
@@ -162,9 +210,7 @@ def main_sim(args):
         _lib.check(lib.fx_sim_run_tiered(ctypes.byref(batch), ctypes.byref(out), hs, ctypes.byref(reruns)),
                    "fx_sim_run_tiered")
         ev1.record(stream)
-        if world > 1:  # the step's output: histograms summed over every rank's instances (RCCL)
-            for h in (lat_hist, chain, delay):
-                dist.all_reduce(h)
+        allreduce_hists(dist, world, (lat_hist, chain, delay))
         ev1.synchronize()
         kernel_ms.append(ev0.elapsed_time(ev1))
     torch.cuda.synchronize(dev)
@@ -191,17 +237,8 @@ def main_sim(args):
                                                           float(deps_local), float(client_cmds_local))
 
     # per-instance rows (global id, conflict %, executed, fast, slow, status), one all_gather
-    gid = torch.arange(N, dtype=torch.int64, device=dev) + rank * N
-    rows = torch.stack([gid, torch.tensor(rates, dtype=torch.int64, device=dev),
-                        executed_len.view(N, n).to(torch.int64).sum(1),
-                        st[:, _lib.FX_SIM_STAT_FAST:_lib.FX_SIM_STAT_FAST + n].sum(1),
-                        st[:, _lib.FX_SIM_STAT_SLOW:_lib.FX_SIM_STAT_SLOW + n].sum(1),
-                        err.to(torch.int64)], 1)
-    if world > 1:
-        parts = [torch.empty_like(rows) for _ in range(world)]
-        dist.all_gather(parts, rows.contiguous())
-        rows = torch.cat(parts)
-    summary = {"fields": ["instance", "conflict_pct", "executed", "fast_paths", "slow_paths", "status"],
+    rows = gather_rows(dist, world, instance_rows(torch, rank * N, rates, executed_len, stats, err, n))
+    summary = {"fields": ROW_FIELDS,
                "instances": int(rows.shape[0]), "all_ok": bool((rows[:, 5] == 0).all().item()),
                "executed_matches": int(rows[:, 2].sum().item()) == int(executed_all)}
     fast_all, slow_all = int(rows[:, 3].sum().item()), int(rows[:, 4].sum().item())
