@@ -744,24 +744,29 @@ struct Big {
     if (rd(RC(sl, p, R_WAIT))) unlink(sl);
     const uint32_t c = rd(S(sl, SL_CLIENT));
     const uint32_t nk = (rd(S(sl, SL_CNT)) >> 16) & 3u;
-    if ((rd(CL(c, 0)) & 0xFFu) == p) {  // pending.wait_for registered this rifl at p
-      const uint32_t pend = rd(CL(c, 3));
-      if (pend < nk) {
-        err = FX_ERR_SIM_LATE;
-        return;
-      }
-      put(CL(c, 3), pend - nk);  // one ExecutorResult per key
-      if (pend == nk) {
-        if (rtop >= g.C + 64u) {
-          fail_cap(__LINE__);
-          return;
-        }
-        put(W(g.o_rdy, rtop++), c);
-      }
-    }
+    if ((rd(CL(c, 0)) & 0xFFu) == p) client_result(c, nk);  // pending.wait_for registered this rifl at p
+    if (err) return;
     const uint32_t masks = rd(S(sl, SL_MASKS));
     if (((masks >> 24) & 0xFFu) + 1u == n) put(S(sl, SL_DOT), 0u);  // executed everywhere: free the slot
     else put(S(sl, SL_MASKS), masks + (1u << 24));
+  }
+
+  // AggregatePending::add_executor_result (aggregate.rs:48-87): one
+  // ExecutorResult per key; the rifl is ready once all arrived
+  __device__ __forceinline__ void client_result(uint32_t c, uint32_t nk) {
+    const uint32_t pend = rd(CL(c, 3));
+    if (pend < nk) {
+      err = FX_ERR_SIM_LATE;
+      return;
+    }
+    put(CL(c, 3), pend - nk);
+    if (pend == nk) {
+      if (rtop >= g.C + 64u) {
+        fail_cap(__LINE__);
+        return;
+      }
+      put(W(g.o_rdy, rtop++), c);
+    }
   }
 
   // PendingIndex (index.rs:145-208): v waits on the dot in slot m
@@ -815,7 +820,11 @@ struct Big {
 
   // save_scc (mod.rs:488-523): the members W(o_tstk, base .. base + cnt)
   // (already in the executed clock) in ascending dot order; released dots
-  // pushed to the worklist
+  // pushed to the worklist.  Up to 64 members at a time, lane-parallel: each
+  // lane loads its member's fields at once, then the log, the ExecutionDelay
+  // samples, the worklist and the slots' execution counts are written in
+  // parallel; only waiter-list unlinks and the client results at the client's
+  // own process go one by one, in order.
   __device__ __forceinline__ void save_scc(uint32_t base, uint32_t cnt) {
     hist_chain(cnt);
     {
@@ -824,18 +833,70 @@ struct Big {
       XPROF_ADD(PF_SORT);
     }
     XPROF_T0();
-    for (uint32_t r = 0; r < cnt && !err; ++r) {
-      const uint32_t sl = rd(W(g.o_tl, r));
-      const uint32_t d = rd(S(sl, SL_DOT));
-      const uint32_t st = rd(RC(sl, xp, R_START));
-      if (nwl >= 2u * g.NS) {
-        fail_cap(__LINE__);
-        return;
+    if (nwl + cnt > 2u * g.NS) {
+      fail_cap(__LINE__);
+      return;
+    }
+    const uint32_t p = xp;
+    for (uint32_t r0 = 0; r0 < cnt && !err; r0 += 64) {
+      const uint32_t r = r0 + lid;
+      const bool act = r < cnt;
+      uint32_t sl = 0, d = 0, st = 0, wt = 0, c = 0, cw = 0, mk = 0;
+      if (act) {
+        sl = W(g.o_tl, r);
+        d = S(sl, SL_DOT);
+        st = RC(sl, p, R_START);
+        wt = RC(sl, p, R_WAIT);
+        c = S(sl, SL_CLIENT);
+        cw = S(sl, SL_CNT);
+        mk = S(sl, SL_MASKS);
       }
-      put(W(g.o_wl, nwl++), sl);
-      on_execute(sl, d, st);
+      const uint32_t cpr = act ? CL(c, 0) : 0u;
+      const uint32_t m = min(64u, cnt - r0);
+      if (act) {
+        if (A.executed && xk + lid < A.exec_cap) A.executed[((size_t)inst * n + p) * A.exec_cap + xk + lid] = d;
+        W(g.o_wl, nwl + lid) = sl;
+        if (A.delay_hist) {  // ExecutionDelay (graph/mod.rs:514-518)
+          const uint32_t bn = min(now - st, A.delay_bins - 1u);
+          if (bn < HD_BINS) atomicAdd(&lds[HC_BINS + bn], 1u);
+          else atomicAdd(&A.delay_hist[bn], 1ull);
+        }
+        if (((mk >> 24) & 0xFFu) + 1u == n) S(sl, SL_DOT) = 0u;  // executed everywhere: free the slot
+        else S(sl, SL_MASKS) = mk + (1u << 24);
+      }
+      xk += m;
+      nwl += m;
+      const uint64_t need = bal(act && (wt != 0 || (cpr & 0xFFu) == p));
+      for (uint64_t mm = need; mm && !err; mm &= mm - 1) {
+        const uint32_t j = ctz64(mm);
+        if (rl(wt, j)) unlink(rl(sl, j));
+        if ((rl(cpr, j) & 0xFFu) == p) client_result(rl(c, j), (rl(cw, j) >> 16) & 3u);
+      }
     }
     XPROF_ADD(PF_EMIT);
+  }
+
+  // the per-lane states of the top frame's deps, lanes [ci, cnd): the tag of
+  // the dep's slot and its record at xp (status, Tarjan id / low, mark).
+  // They stay valid until the search recurses (nothing else writes them).
+  __device__ __forceinline__ void dep_states(uint32_t drow, uint32_t ci, uint32_t cnd, uint32_t& ptag,
+                                             uint32_t& ppst, uint32_t& ptl, uint32_t& pmk) {
+    ptag = ppst = ptl = pmk = 0;
+    if (lid >= ci && lid < cnd && src_ok(drow)) {
+      const uint32_t sl = hslot(drow);
+      ptag = S(sl, SL_DOT);
+      ppst = RC(sl, xp, R_PST);
+      ptl = RC(sl, xp, R_TL);
+      pmk = RC(sl, xp, R_MARK);
+    }
+  }
+  // a vertex's dot, dep count and dep row (lane j = dep j), loaded together
+  __device__ __forceinline__ void frame_row(uint32_t sl, uint32_t& cdot, uint32_t& cnd, uint32_t& drow) {
+    const uint32_t t = S(sl, SL_DOT), cw = S(sl, SL_CNT);
+    drow = lid < g.vmax ? S(sl, g.sl_value + lid) : 0u;
+    cdot = uni(t);
+    cnd = (uni(cw) >> 8) & 0xFFu;
+    if (lid >= cnd) drow = 0;
   }
 
   // find_scc (mod.rs:409-486) + strong_connect (tarjan.rs:96-316) + finalize
@@ -854,16 +915,20 @@ struct Big {
     *saved = false;
     idc = 1;
     tsp = 0;
-    fsp = 0;
+    // DFS frames 0..63 in lanes: slot | next dep << 24, and the stack
+    // position of the frame's vertex; deeper frames in W(o_fv / o_fi)
+    uint32_t frs = 0, frt = 0;
+    const uint32_t mk0 = rd(RC(rsl, p, R_MARK));
     put(RC(rsl, p, R_TL), 1u | (1u << 16));
-    put(RC(rsl, p, R_MARK), rd(RC(rsl, p, R_MARK)) | 1u);
+    put(RC(rsl, p, R_MARK), mk0 | 1u);
     put(W(g.o_tstk, tsp++), rsl);
-    put(W(g.o_fv, fsp++), rsl);
-    // the top frame lives in registers: its slot, next dep, id, low, dot and
-    // dep row (lane j = dep j)
-    uint32_t cv = rsl, ci = 0, cid = 1, clow = 1, cdot = rd(S(rsl, SL_DOT));
-    uint32_t cnd = (rd(S(rsl, SL_CNT)) >> 8) & 0xFFu;
-    uint32_t drow = lid < cnd ? S(rsl, g.sl_value + lid) : 0u;
+    fsp = 1;
+    // the top frame in registers: slot, next dep, id, low, stack position,
+    // dot, dep count, dep row and the deps' prefetched states
+    uint32_t cv = rsl, ci = 0, cid = 1, clow = 1, ctp = 0, cdot = 0, cnd = 0, drow = 0;
+    frame_row(rsl, cdot, cnd, drow);
+    uint32_t ptag, ppst, ptl, pmk;
+    dep_states(drow, 0, cnd, ptag, ppst, ptl, pmk);
     uint32_t result = FOUND;
     for (uint32_t guard = 0; fsp && !err; ++guard) {
       if (guard > 64u * g.NS + 64u) {
@@ -871,40 +936,46 @@ struct Big {
         break;
       }
       if (ci < cnd) {
-        const uint32_t d = rl(drow, ci);
+        const uint32_t d = rl(drow, ci), tag = rl(ptag, ci), ps = rl(ppst, ci);
         ++ci;
         XPROF_CNT(PC_EDGES, 1);
-        if (d == cdot || !src_ok(d)) continue;  // self (tarjan.rs:128-130)
-        const uint32_t sl = hslot(d);
-        if (rd(S(sl, SL_DOT)) != d) continue;  // executed everywhere (tarjan.rs:131-145)
-        const uint32_t ps = rd(RC(sl, p, R_PST));
-        if (ps & PS_EXEC) continue;  // executed here
-        if (!(ps & PS_INGRAPH)) {    // missing (tarjan.rs:148-157, shard_count == 1)
+        // self (tarjan.rs:128-130); executed everywhere (its slot was freed)
+        // or here (tarjan.rs:131-145)
+        if (d == cdot || !src_ok(d) || tag != d || (ps & PS_EXEC)) continue;
+        if (!(ps & PS_INGRAPH)) {  // missing (tarjan.rs:148-157, shard_count == 1)
           *missing = d;
           result = MISSING;
           break;
         }
-        const uint32_t tw = rd(RC(sl, p, R_TL)), mk = rd(RC(sl, p, R_MARK));
+        const uint32_t tw = rl(ptl, ci - 1u), mk = rl(pmk, ci - 1u);
         if ((tw & 0xFFFFu) == 0) {  // recurse (tarjan.rs:172-214)
           XPROF_CNT(PC_RECURSE, 1);
-          put(W(g.o_fi, fsp - 1u), ci);
+          const uint32_t f = fsp - 1u;
+          if (f < 64u) {
+            lset(frs, f, cv | (ci << 24));
+            lset(frt, f, ctp);
+          } else {
+            put(W(g.o_fv, f), cv | (ci << 24));
+            put(W(g.o_fi, f), ctp);
+          }
           put(RC(cv, p, R_TL), cid | (clow << 16));
           ++idc;
           if (idc > 0xFFFFu || tsp >= g.NS || fsp >= g.NS) {
             fail_cap(__LINE__);
             break;
           }
+          const uint32_t sl = hslot(d);
           put(RC(sl, p, R_TL), idc | (idc << 16));
           put(RC(sl, p, R_MARK), mk | 1u);
+          ctp = tsp;
           put(W(g.o_tstk, tsp++), sl);
-          put(W(g.o_fv, fsp++), sl);
+          ++fsp;
           cv = sl;
           ci = 0;
           cid = idc;
           clow = idc;
-          cdot = d;
-          cnd = (rd(S(sl, SL_CNT)) >> 8) & 0xFFu;
-          drow = lid < cnd ? S(sl, g.sl_value + lid) : 0u;
+          frame_row(sl, cdot, cnd, drow);
+          dep_states(drow, 0, cnd, ptag, ppst, ptl, pmk);
         } else if (mk & 1u) {  // on the stack (tarjan.rs:215-225)
           clow = min(clow, tw & 0xFFFFu);
         }
@@ -912,92 +983,80 @@ struct Big {
       }
       // cv finished
       const uint32_t lowv = clow;
-      if (cid == lowv) {  // SCC root: pop the members (tarjan.rs:233-312)
-        uint32_t base = tsp;
-        while (base > 0) {
-          --base;
-          const uint32_t x = rd(W(g.o_tstk, base));
-          put(RC(x, p, R_MARK), rd(RC(x, p, R_MARK)) & ~1u);
-          put(RC(x, p, R_PST), rd(RC(x, p, R_PST)) | PS_EXEC);  // executed_clock.add (tarjan.rs:293)
-          if (x == cv) break;
+      if (cid == lowv) {  // SCC root: pop the members tstk[ctp, tsp) (tarjan.rs:233-312)
+        for (uint32_t i0 = ctp; i0 < tsp; i0 += 64) {
+          const uint32_t i = i0 + lid;
+          if (i < tsp) {
+            const uint32_t x = W(g.o_tstk, i);
+            const uint32_t mkx = RC(x, p, R_MARK), psx = RC(x, p, R_PST);
+            RC(x, p, R_MARK) = mkx & ~1u;
+            RC(x, p, R_PST) = psx | PS_EXEC;  // executed_clock.add (tarjan.rs:293)
+          }
         }
-        const uint32_t cnt = tsp - base;
-        save_scc(base, cnt);
-        tsp = base;
+        save_scc(ctp, tsp - ctp);
+        tsp = ctp;
         *saved = true;
         if (err) break;
       }
       --fsp;
       if (fsp) {  // resume the parent frame (tarjan.rs:211: low = min(low, dep low))
-        const uint32_t pp = rd(W(g.o_fv, fsp - 1u));
-        cv = pp;
-        ci = rd(W(g.o_fi, fsp - 1u));
-        const uint32_t tw = rd(RC(pp, p, R_TL));
-        cid = tw & 0xFFFFu;
-        clow = min(tw >> 16, lowv);
-        cdot = rd(S(pp, SL_DOT));
-        cnd = (rd(S(pp, SL_CNT)) >> 8) & 0xFFu;
-        drow = lid < cnd ? S(pp, g.sl_value + lid) : 0u;
+        const uint32_t f = fsp - 1u;
+        uint32_t pk, tp;
+        if (f < 64u) {
+          pk = rl(frs, f);
+          tp = rl(frt, f);
+        } else {
+          pk = rd(W(g.o_fv, f));
+          tp = rd(W(g.o_fi, f));
+        }
+        cv = pk & 0xFFFFFFu;
+        ci = pk >> 24;
+        ctp = tp;
+        const uint32_t tw = RC(cv, p, R_TL);
+        frame_row(cv, cdot, cnd, drow);
+        cid = uni(tw) & 0xFFFFu;
+        clow = min(uni(tw) >> 16, lowv);
+        dep_states(drow, ci, cnd, ptag, ppst, ptl, pmk);
       }
     }
     // finalize: ids of the vertices left on the stack; failed searches mark them visited
-    for (uint32_t k = 0; k < tsp; ++k) {
-      const uint32_t x = rd(W(g.o_tstk, k));
-      put(RC(x, p, R_TL), 0u);
-      if (mark_epoch && result == MISSING) put(RC(x, p, R_MARK), (rd(RC(x, p, R_MARK)) & 1u) | (mark_epoch << 1));
+    const bool markit = mark_epoch && result == MISSING;
+    for (uint32_t i0 = 0; i0 < tsp; i0 += 64) {
+      const uint32_t i = i0 + lid;
+      if (i < tsp) {
+        const uint32_t x = W(g.o_tstk, i);
+        RC(x, p, R_TL) = 0u;
+        if (markit) RC(x, p, R_MARK) = (RC(x, p, R_MARK) & 1u) | (mark_epoch << 1);
+      }
     }
     tsp = 0;
     return result;
   }
 
-  // check_pending (mod.rs:556-587) + try_pending (589-642): LIFO over the
-  // released dots; each one's waiters in ascending dot order (C2)
-  __device__ __forceinline__ void check_pending() {
-    XPROF_T0();
-    check_pending_();
-    XPROF_ADD(PF_CHECK);
-  }
-  __device__ __forceinline__ void check_pending_() {
+  // PendingIndex::remove (index.rs:204-207) of the released dot in slot x:
+  // unregisters its waiters and sorts them ascending (C2) into W(o_tw, ..)
+  __device__ __forceinline__ uint32_t take_waiters(uint32_t x) {
     const uint32_t p = xp;
-    while (nwl && !err) {
-      const uint32_t x = rd(W(g.o_wl, --nwl));
-      uint32_t v = rd(RC(x, p, R_HEAD));
-      if (!v) continue;
-      put(RC(x, p, R_HEAD), 0u);
-      // PendingIndex::remove: collect (and unregister) every waiter
-      uint32_t cnt = 0;
-      while (v) {
-        const uint32_t sl = v - 1u;
-        if (cnt >= g.NS) {
-          fail_cap(__LINE__);
-          return;
-        }
-        put(W(g.o_tmp, cnt++), sl);
-        v = rd(RC(sl, p, R_NEXT));
-        put(RC(sl, p, R_WAIT), 0u);
-        put(RC(sl, p, R_NEXT), 0u);
-        put(RC(sl, p, R_PREV), 0u);
+    uint32_t v = rd(RC(x, p, R_HEAD));
+    if (!v) return 0;
+    put(RC(x, p, R_HEAD), 0u);
+    uint32_t cnt = 0;
+    while (v) {
+      const uint32_t sl = v - 1u;
+      if (cnt >= g.NS) {
+        fail_cap(__LINE__);
+        return 0;
       }
-      XPROF_CNT(PC_WAITERS, cnt);
-      sort_slots(g.o_tmp, cnt, g.o_tw);
-      // visited-skip set = vertices marked with this epoch
-      uint32_t cur = ++epoch;
-      for (uint32_t k = 0; k < cnt && !err; ++k) {
-        const uint32_t wsl = rd(W(g.o_tw, k));
-        if (rd(RC(wsl, p, R_PST)) & PS_EXEC) continue;  // no longer pending (NotPending)
-        if ((rd(RC(wsl, p, R_MARK)) >> 1) == cur) continue;  // visited by a failed search
-        uint32_t missing = 0;
-        bool saved = false;
-        const uint32_t r = find_scc(wsl, &missing, cur, &saved);
-        if (err) return;
-        if (r == FOUND) {
-          cur = ++epoch;  // visited.clear()
-        } else {
-          index_pending(wsl, missing);
-          if (saved) cur = ++epoch;
-        }
-      }
+      const uint32_t nx = rd(RC(sl, p, R_NEXT));
+      put(W(g.o_tmp, cnt++), sl);
+      put(RC(sl, p, R_WAIT), 0u);
+      put(RC(sl, p, R_NEXT), 0u);
+      put(RC(sl, p, R_PREV), 0u);
+      v = nx;
     }
+    XPROF_CNT(PC_WAITERS, cnt);
+    sort_slots(g.o_tmp, cnt, g.o_tw);
+    return cnt;
   }
 
   // GraphExecutor::handle(Add) (executor.rs:69-80) -> handle_add (mod.rs:213-275)
@@ -1007,6 +1066,11 @@ struct Big {
     x_add_(p, sl);
     XPROF_ADD(PF_XADD);
   }
+  // The searches of one handle_add: the new vertex's first find, then
+  // check_pending (mod.rs:556-587) LIFO over the released dots and
+  // try_pending (589-642) over each one's waiters in ascending dot order (C2),
+  // skipping the ones a failed search of this round visited.  One loop, one
+  // find_scc call site.
   __device__ __forceinline__ void x_add_(uint32_t p, uint32_t sl) {
     xp = p;
     xk = rl(pexec, p);
@@ -1022,7 +1086,8 @@ struct Big {
     const uint32_t depj = lid < vc ? S(sl, g.sl_value + lid) : 0u;
     bool keep = false;
     if (lid < vc && depj != d) keep = !contains_v(depj);
-    if (!bal(keep)) {  // every dep executed: a singleton SCC
+    bool first = bal(keep) != 0;
+    if (!first) {  // every dep executed: a singleton SCC
       XPROF_CNT(PC_FAST, 1);
       put(RC(sl, p, R_PST), ps | PS_EXEC);
       hist_chain(1u);
@@ -1031,12 +1096,62 @@ struct Big {
     } else {
       put(RC(sl, p, R_PST), ps | PS_INGRAPH);
       put(RC(sl, p, R_START), now);  // Vertex::start_time_ms (tarjan.rs:332-348)
+    }
+    XPROF_T0();
+    uint32_t wk = 0, wcnt = 0, cur = 0;  // the waiter list being tried
+    uint32_t wps = 0, wmk = 0, wbase = NONE;  // lanes: states of waiters [wbase, wbase + 64)
+    while (!err) {
+      uint32_t root, mark = 0;
+      if (first) {
+        root = sl;
+        first = false;
+      } else {
+        // the next waiter still pending and not visited in this round
+        root = NONE;
+        while (wk < wcnt) {
+          if (wbase == NONE || wk >= wbase + 64u) {
+            wbase = wk;
+            wps = wmk = 0;
+            if (wbase + lid < wcnt) {
+              const uint32_t w = W(g.o_tw, wbase + lid);
+              wps = RC(w, p, R_PST);
+              wmk = RC(w, p, R_MARK);
+            }
+          }
+          const uint64_t ok = bal(lid >= wk - wbase && wbase + lid < wcnt && !(wps & PS_EXEC) &&
+                                  (wmk >> 1) != cur);
+          if (!ok) {
+            wk = wbase + 64u;
+            continue;
+          }
+          const uint32_t j = ctz64(ok);
+          root = rd(W(g.o_tw, wbase + j));
+          wk = wbase + j + 1u;
+          break;
+        }
+        if (root == NONE) {  // this list is done: the next released dot with waiters
+          if (!nwl) break;
+          wcnt = take_waiters(rd(W(g.o_wl, --nwl)));
+          wk = 0;
+          wbase = NONE;
+          cur = ++epoch;  // try_pending's visited set starts empty
+          continue;
+        }
+        mark = cur;
+      }
       uint32_t missing = 0;
       bool saved = false;
-      const uint32_t r = find_scc(sl, &missing, 0, &saved);
-      if (r == MISSING && !err) index_pending(sl, missing);  // index_pending (mod.rs:525-554)
+      const uint32_t r = find_scc(root, &missing, mark, &saved);
+      if (err) break;
+      if (r == MISSING) index_pending(root, missing);  // index_pending (mod.rs:525-554)
+      if (mark && (r == FOUND || saved)) {
+        cur = ++epoch;  // visited.clear()
+        wbase = NONE;   // marks and states changed: reload the waiters' states
+      } else if (mark) {
+        wbase = NONE;
+      }
     }
-    if (!err) check_pending();
+    XPROF_ADD(PF_CHECK);
     lset(pexec, p, xk);
   }
 
@@ -1195,7 +1310,7 @@ struct Big {
 };
 
 template <uint32_t NG>
-__global__ __launch_bounds__(64) void k_simx(ArgsX a) {
+__global__ __launch_bounds__(64, 3) void k_simx(ArgsX a) {
   __shared__ uint32_t smem[LDS_WORDS];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
