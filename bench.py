@@ -44,7 +44,8 @@ LAYOUT = {0: "16 lanes per stream", 1: "one lane per stream", 2: "one lane per s
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["sim", "dense-sim", "executor", "huge", "dense", "placements", "pred"],
+    ap.add_argument("--mode", choices=["sim", "dense-sim", "executor", "huge", "dense", "placements", "pred",
+                                       "handle"],
                     default="sim",
                     help="sim: the batched simulator (BASELINE configs[1], the headline); "
                          "dense-sim: the simulator on BASELINE configs[3] (64 clients/region, 100%% "
@@ -132,6 +133,9 @@ def main():
     if args.mode == "dense":
         from bench_huge import main_dense
         return main_dense(args)
+    if args.mode == "handle":
+        from bench_handle import main_handle
+        return main_handle(args)
     if args.mode == "pred":
         from bench_pred import main_pred
         return main_pred(args)
