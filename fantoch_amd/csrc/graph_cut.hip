@@ -126,9 +126,37 @@ struct WaveMax {
   }
 };
 
-__global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad) {
+// With few streams (configs[4]: 5), per-stream maxima from thousands of
+// blocks would all hit the same few addresses: the atomics serialise at L2.
+// Then the block's waves combine in LDS and the block writes its S partial
+// maxima (part[block][S]), reduced per stream by k_part_max.
+constexpr uint32_t SMALL_S = 64;
+
+// out[s] = max(out[s], max over blocks b of part[b][s]); one block per stream
+__global__ void k_part_max(const uint32_t* part, uint32_t blocks, uint32_t S, uint32_t* out) {
+  const uint32_t s = blockIdx.x;
+  uint32_t m = 0;
+  for (uint32_t b = threadIdx.x; b < blocks; b += blockDim.x) m = max(m, part[(size_t)b * S + s]);
+  for (uint32_t off = 32; off; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+  __shared__ uint32_t sh[BT / 64];
+  if ((threadIdx.x & 63u) == 0) sh[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t i = 1; i < blockDim.x / 64; ++i) m = max(m, sh[i]);
+    out[s] = max(out[s], max(m, sh[0]));
+  }
+}
+
+__global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad, uint32_t* part) {
   const uint64_t total = (uint64_t)in.S * in.steps;
   WaveMax acc;
+  __shared__ uint32_t lm[SMALL_S];
+  const bool small = part != nullptr;
+  if (small) {
+    if (threadIdx.x < SMALL_S) lm[threadIdx.x] = 0;
+    __syncthreads();
+  }
+  uint32_t* out = small ? lm : maxseq;
   // wave-uniform trip count (the reduction needs every lane active)
   for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x; b0 < total; b0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t t = b0 + threadIdx.x;
@@ -142,9 +170,15 @@ __global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad) {
       if (src < 1 || src > in.n || FX_HDR_KIND(in.hdr[at]) != FX_KIND_ADD) bad[s] = 1;
       sq = FX_DOT_SEQ(d);
     }
-    acc.add(maxseq, s, sq);
+    acc.add(out, s, sq);
   }
-  acc.flush_block(maxseq);
+  if (small) {
+    acc.flush(lm);
+    __syncthreads();
+    if (threadIdx.x < in.S) part[(size_t)blockIdx.x * in.S + threadIdx.x] = lm[threadIdx.x];
+  } else {
+    acc.flush_block(maxseq);
+  }
 }
 
 __global__ void k_pos(In in, const uint64_t* base, const uint32_t* maxseq, uint32_t* pos, uint32_t* bad) {
@@ -285,8 +319,15 @@ __global__ void k_segs(In in, const uint8_t* flag, uint32_t nch, const uint32_t*
 
 // segment starts and lengths; longest segment per stream
 __global__ void k_seglen(uint64_t nseg, const uint64_t* segbase, const uint32_t* seg_end, const uint32_t* seg_stream,
-                         uint32_t* seg_start, uint32_t* smax) {
+                         uint32_t* seg_start, uint32_t* smax, uint32_t S, uint32_t* part) {
   WaveMax acc;
+  __shared__ uint32_t lm[SMALL_S];
+  const bool small = part != nullptr;
+  if (small) {
+    if (threadIdx.x < SMALL_S) lm[threadIdx.x] = 0;
+    __syncthreads();
+  }
+  uint32_t* out = small ? lm : smax;
   for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x; b0 < nseg; b0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t k = b0 + threadIdx.x;
     const bool valid = k < nseg;
@@ -297,9 +338,15 @@ __global__ void k_seglen(uint64_t nseg, const uint64_t* segbase, const uint32_t*
       seg_start[k] = a;
       len = seg_end[k] - a + 1u;
     }
-    acc.add(smax, s, len);
+    acc.add(out, s, len);
   }
-  acc.flush_block(smax);
+  if (small) {
+    acc.flush(lm);
+    __syncthreads();
+    if (threadIdx.x < S) part[(size_t)blockIdx.x * S + threadIdx.x] = lm[threadIdx.x];
+  } else {
+    acc.flush_block(smax);
+  }
 }
 
 struct Seg {
@@ -435,7 +482,11 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
   uint32_t* maxseq = db.alloc<uint32_t>(S, 0);
   uint32_t* bad = db.alloc<uint32_t>(S, 0);
   if (!maxseq || !bad) return FX_ERR_HIP;
-  hipLaunchKernelGGL(k_maxseq, dim3(grid_for_max(work)), dim3(BT), 0, hs, in, maxseq, bad);
+  const uint32_t gmax = grid_for_max(work);
+  uint32_t* part = S <= SMALL_S ? db.alloc<uint32_t>((size_t)gmax * S) : nullptr;
+  if (S <= SMALL_S && !part) return FX_ERR_HIP;
+  hipLaunchKernelGGL(k_maxseq, dim3(gmax), dim3(BT), 0, hs, in, maxseq, bad, part);
+  if (part) hipLaunchKernelGGL(k_part_max, dim3(S), dim3(BT), 0, hs, part, gmax, S, maxseq);
   std::vector<uint32_t> h_maxseq(S), h_bad(S);
   (void)hipMemcpyAsync(h_maxseq.data(), maxseq, (size_t)S * 4, hipMemcpyDeviceToHost, hs);
   if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
@@ -486,7 +537,14 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
   if (!segbase || !seg_of || !seg_end || !seg_stream || !seg_start || !smax) return FX_ERR_HIP;
   (void)hipMemcpyAsync(segbase, h_segbase.data(), (size_t)S * 8, hipMemcpyHostToDevice, hs);
   hipLaunchKernelGGL(k_segs, dim3(nch * S), dim3(BT), 0, hs, in, flag, nch, ccnt, segbase, seg_of, seg_end, seg_stream);
-  if (NS) hipLaunchKernelGGL(k_seglen, dim3(grid_for_max(NS)), dim3(BT), 0, hs, NS, segbase, seg_end, seg_stream, seg_start, smax);
+  if (NS) {
+    const uint32_t gs = grid_for_max(NS);
+    uint32_t* spart = S <= SMALL_S ? db.alloc<uint32_t>((size_t)gs * S) : nullptr;
+    if (S <= SMALL_S && !spart) return FX_ERR_HIP;
+    hipLaunchKernelGGL(k_seglen, dim3(gs), dim3(BT), 0, hs, NS, segbase, seg_end, seg_stream, seg_start, smax, S,
+                       spart);
+    if (spart) hipLaunchKernelGGL(k_part_max, dim3(S), dim3(BT), 0, hs, spart, gs, S, smax);
+  }
   std::vector<uint32_t> h_smax(S);
   (void)hipMemcpyAsync(h_smax.data(), smax, (size_t)S * 4, hipMemcpyDeviceToHost, hs);
   if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;

@@ -81,11 +81,14 @@ enum : uint32_t { SL_DOT = 0, SL_CLIENT = 1, SL_IDX = 2, SL_KEYS = 3, SL_CNT = 4
 // SL_QUORUM: the MCollect's quorum mask (8) | its size << 8
 // per-(slot, process) record words
 enum : uint32_t { R_PST = 0, R_START = 1, R_WAIT = 2, R_TL = 3, R_MARK = 4, R_NEXT = 5, R_PREV = 6,
-                  R_HEAD = 7 };
+                  R_HEAD = 7, R_CMISS = 8, R_CEPOCH = 9, RW = 16 };
 // R_TL:   Tarjan id (16) | low (16) << 16
 // R_MARK: on the Tarjan stack | visited epoch << 1 (try_pending's skip rule)
 // R_WAIT / R_NEXT / R_PREV / R_HEAD: slot + 1 (0 = none) — the PendingIndex
 //         entry of a waited-on dot is a doubly linked list through its waiters
+// R_CMISS / R_CEPOCH: the missing dep the last search rooted at this vertex
+//         stopped at, and the process's execution epoch then (0 = none); see
+//         x_add_ for why a still-valid one stands in for a whole search
 
 struct GeoX {  // launch-uniform geometry (words)
   uint32_t n, C, K, Q, qlog, NS, R, ncli_keys;
@@ -170,7 +173,7 @@ enum : uint32_t { FOUND = 0, MISSING = 1 };
 enum : uint32_t { PF_POP = 0, PF_EVENT = 1, PF_XADD = 2, PF_FIND = 3, PF_CHECK = 4, PF_SORT = 5, PF_EMIT = 6,
                   PF_HANDLER = 7, PF_SEND = 8, PF_GC = 9, PF_CLIENT = 10,
                   PC_EDGES = 16, PC_RECURSE = 17, PC_XADD = 18, PC_FIND = 19, PC_WAITERS = 20, PC_FAST = 21,
-                  PC_EVENTS = 22, PC_SEND = 23 };
+                  PC_EVENTS = 22, PC_SEND = 23, PC_CACHE = 11 };
 
 // NG: registers of group minima per lane (message pool <= 4096 NG entries)
 template <uint32_t NG>
@@ -205,6 +208,8 @@ struct Big {
   // lane p: proposal seq, Fast / Slow (and their read-only shares), executed
   // count, Stable, quorums (fast | write << 8 | majority << 16), GC reporters
   uint32_t pseq = 0, pfast = 0, pslow = 0, pfr = 0, psr = 0, pexec = 0, pstab = 0, pq = 0, prep = 0;
+  // lane p: executions so far at p, in SCCs (the epoch of the search-result cache)
+  uint32_t pxe = 0;
   // lane 8 p + s: p's committed frontier of source s + 1 (GC track), its
   // previous stable frontier, and the link delay p -> s
   uint32_t gcf = 0, gps = 0, dpq = 0;
@@ -213,7 +218,7 @@ struct Big {
   uint32_t frw = 0, frd = 0, frb = 0;
   uint32_t nfrm = 0, xinfo = NONE, rtop = 0;
   // executor (the process being run)
-  uint32_t xp = 0, xk = 0, epoch = 0, nwl = 0, idc = 0, tsp = 0, fsp = 0;
+  uint32_t xp = 0, xk = 0, xe = 0, epoch = 0, nwl = 0, idc = 0, tsp = 0, fsp = 0;
 #ifdef FX_SIM_PROFILE
   uint64_t prof[24] = {};
 #endif
@@ -221,7 +226,7 @@ struct Big {
   // ------------------------------------------------------------ arena views
   __device__ __forceinline__ uint32_t& S(uint32_t sl, uint32_t w) { return M[g.o_slot + sl * g.SW + w]; }
   __device__ __forceinline__ uint32_t& RC(uint32_t sl, uint32_t p, uint32_t w) {
-    return M[g.o_rec + (sl * g.n + p) * 8u + w];
+    return M[g.o_rec + (sl * g.n + p) * RW + w];
   }
   __device__ __forceinline__ uint32_t& CL(uint32_t c, uint32_t w) { return M[g.o_cl + c * 8u + w]; }
   __device__ __forceinline__ uint32_t& KD(uint32_t p, uint32_t key, uint32_t w) {
@@ -492,7 +497,7 @@ struct Big {
       else if (i >= SL_COLLECT && i < SL_COLLECT + nd) v = dv;
       S(sl, i) = v;
     }
-    for (uint32_t i = lid; i < g.n * 8u; i += 64) M[g.o_rec + sl * g.n * 8u + i] = 0;
+    for (uint32_t i = lid; i < g.n * RW; i += 64) M[g.o_rec + sl * g.n * RW + i] = 0;
     if (A.dot_client && s <= A.exec_cap && lid == 0)
       A.dot_client[((size_t)inst * n + p) * A.exec_cap + s - 1u] = c + 1u;
     act_send(M_COLLECT, dot, (1u << n) - 1u);
@@ -827,6 +832,7 @@ struct Big {
   // own process go one by one, in order.
   __device__ __forceinline__ void save_scc(uint32_t base, uint32_t cnt) {
     hist_chain(cnt);
+    ++xe;  // the graph lost vertices: every cached search result of xp is stale
     {
       XPROF_T0();
       sort_slots(g.o_tstk + base, cnt, g.o_tl);
@@ -1074,6 +1080,7 @@ struct Big {
   __device__ __forceinline__ void x_add_(uint32_t p, uint32_t sl) {
     xp = p;
     xk = rl(pexec, p);
+    xe = rl(pxe, p);
     nwl = 0;
     const uint32_t d = rd(S(sl, SL_DOT));
     const uint32_t ps = rd(RC(sl, p, R_PST));
@@ -1090,12 +1097,40 @@ struct Big {
     if (!first) {  // every dep executed: a singleton SCC
       XPROF_CNT(PC_FAST, 1);
       put(RC(sl, p, R_PST), ps | PS_EXEC);
+      ++xe;
       hist_chain(1u);
       put(W(g.o_wl, nwl++), sl);
       on_execute(sl, d, now);
     } else {
       put(RC(sl, p, R_PST), ps | PS_INGRAPH);
       put(RC(sl, p, R_START), now);  // Vertex::start_time_ms (tarjan.rs:332-348)
+      // The first search from the new vertex v enters its first dep u that is
+      // neither v nor executed (deps ascend, C1).  If u is pending and the last
+      // search rooted at u stopped at missing dep m with no execution at p
+      // since, and m is still missing and is not v, this search stops at m
+      // too, having found no SCC: u's walk meets the same deps in the same
+      // states up to m (a vertex that was pending then is still pending; one
+      // that was missing then would have stopped that search, so only m can
+      // have arrived; v itself is reachable only through a dep that was
+      // missing then).  So v just waits on m (index_pending) — no walk; and
+      // v's own result is the same cache entry.
+      const uint32_t j0 = ctz64(bal(keep));
+      const uint32_t u = rl(depj, j0), usl = hslot(u);
+      const uint32_t ut = S(usl, SL_DOT), ups = RC(usl, p, R_PST), ucm = RC(usl, p, R_CMISS),
+                     uce = RC(usl, p, R_CEPOCH);
+      const uint32_t cm = uni(ucm);
+      if (uni(ut) == u && (uni(ups) & (PS_INGRAPH | PS_EXEC)) == PS_INGRAPH && cm && cm != d &&
+          uni(uce) == xe && src_ok(cm)) {
+        const uint32_t msl = hslot(cm);
+        const uint32_t mt = S(msl, SL_DOT), mps = RC(msl, p, R_PST);
+        if (uni(mt) == cm && !(uni(mps) & (PS_INGRAPH | PS_EXEC))) {
+          XPROF_CNT(PC_CACHE, 1);
+          index_pending(sl, cm);
+          put(RC(sl, p, R_CMISS), cm);
+          put(RC(sl, p, R_CEPOCH), xe);
+          first = false;
+        }
+      }
     }
     XPROF_T0();
     uint32_t wk = 0, wcnt = 0, cur = 0;  // the waiter list being tried
@@ -1143,7 +1178,13 @@ struct Big {
       bool saved = false;
       const uint32_t r = find_scc(root, &missing, mark, &saved);
       if (err) break;
-      if (r == MISSING) index_pending(root, missing);  // index_pending (mod.rs:525-554)
+      if (r == MISSING) {
+        index_pending(root, missing);  // index_pending (mod.rs:525-554)
+        if (!saved) {  // a fresh search from root now stops at `missing`
+          put(RC(root, p, R_CMISS), missing);
+          put(RC(root, p, R_CEPOCH), xe);
+        }
+      }
       if (mark && (r == FOUND || saved)) {
         cur = ++epoch;  // visited.clear()
         wbase = NONE;   // marks and states changed: reload the waiters' states
@@ -1153,6 +1194,7 @@ struct Big {
     }
     XPROF_ADD(PF_CHECK);
     lset(pexec, p, xk);
+    lset(pxe, p, xe);
   }
 
   // =========================================== send_to_processes_and_executors
@@ -1550,7 +1592,7 @@ bool simx_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t dots, simx::Ge
     o += (words + 15u) & ~15ull;  // 64-byte aligned tables
   };
   take(g.o_slot, (uint64_t)g.NS * g.SW);
-  take(g.o_rec, (uint64_t)g.NS * n * 8u);
+  take(g.o_rec, (uint64_t)g.NS * n * RW);
   take(g.o_kd, (uint64_t)n * g.ncli_keys * 2u);
   take(g.o_cl, (uint64_t)C * 8u);
   take(g.o_kh, R);

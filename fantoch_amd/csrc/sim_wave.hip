@@ -396,6 +396,59 @@ struct Sim {
     ++seq;
   }
 
+  // the sends of one ToSend action to the targets in `mask` (p excluded), in
+  // ascending target order (C4), as one lane-parallel step: lane q builds the
+  // message to q with the insertion seq and the pool entry the one-by-one
+  // loop would give it (seq + rank, the rank-th pop of the free stack) and
+  // appends it to link (p, q); the link lanes then take their new list words
+  // and heads from the target lanes
+  __device__ __forceinline__ void send_batch(uint32_t p, uint32_t mask, uint32_t kind, uint32_t w2) {
+    PROF_T0();
+    send_batch_(p, mask, kind, w2);
+    PROF_ADD(3);
+  }
+  __device__ __forceinline__ void send_batch_(uint32_t p, uint32_t mask, uint32_t kind, uint32_t w2) {
+    const uint32_t k = pop32(mask);
+    if (k == 0) return;
+    if (nfree < k) {
+      fail_cap(__LINE__);
+      return;
+    }
+    const bool tq = lid < 8u && ((mask >> lid) & 1u);
+    const uint32_t r = pop32(mask & (lid < 8u ? (1u << lid) - 1u : 0u));
+    const uint32_t t = now + gather(dpq, (p * 8u + lid) & 63u);  // lane q: now + d(p, q)
+    if (bal(tq && t >= (1u << 28))) {
+      err = FX_ERR_TIME_RANGE;
+      return;
+    }
+    const uint32_t base = p * (g.n - 1u);
+    const uint32_t rh = gather(rhv, (base + (lid < p ? lid : lid - 1u)) & 63u);  // lane q: link (p, q)'s list
+    const uint32_t head = rh & 0xFFFFu;
+    uint32_t e = 0;
+    if (tq) {
+      e = lds[g.off_free + nfree - 1u - r];
+      uint4* m = reinterpret_cast<uint4*>(&lds[g.off_pool + e * 4u]);
+      *m = make_uint4(t | (kind << 28), seq + r, w2, LNIL);
+      if (head != LNIL) msg(rh >> 16, 3) = e;  // after the tail
+    }
+    const uint32_t nrh = head == LNIL ? (e | (e << 16)) : (head | (e << 16));
+    // lane base + i = link (p, q(i)) takes lane q(i)'s values
+    const uint32_t i = lid - base;
+    const bool ll = lid >= base && i < g.n - 1u;
+    const uint32_t q = (ll ? (i < p ? i : i + 1u) : 0u) & 63u;
+    const uint32_t v_nrh = gather(nrh, q), v_t = gather(t, q), v_new = gather(head == LNIL ? 1u : 0u, q);
+    const uint32_t v_sq = seq + gather(r, q);
+    if (ll && ((mask >> q) & 1u)) {
+      rhv = v_nrh;
+      if (v_new) {  // the link was empty: the message is its head (P links are lanes < 64)
+        ht[0] = v_t;
+        hs[0] = v_sq;
+      }
+    }
+    nfree -= k;
+    seq += k;
+  }
+
   // -------------------------------------------------------------- trace
   __device__ __forceinline__ void note(uint64_t kind, uint64_t a, uint64_t b, uint64_t c) {
     PROF_T0();
@@ -1184,22 +1237,20 @@ struct Sim {
       const uint32_t w = rl(frw, fi);
       if (w & 3u) {  // ToSend: targets ascending (C4), self recurses in place
         const uint32_t tgt = (w >> 8) & 0xFFu, k2 = (w >> 2) & 15u, dot = rl(frd, fi);
-        uint32_t nx = (w >> 16) & 15u;
-        while (nx < n) {
-          const uint32_t to = nx++;
-          if (!((tgt >> to) & 1u)) continue;
-          if (to == p) {
-            lset(frw, fi, (w & ~(15u << 16)) | (nx << 16));
-            from = p;
-            kind = k2;
-            w2 = dot;
-            pend = true;
-            break;
-          }
-          send_p(p, to, k2, dot);
-          if (err) return;
+        const uint32_t nx = (w >> 16) & 15u;
+        // the targets before the self-delivery (or all of them) in one batch
+        const bool self = ((tgt >> p) & 1u) && p >= nx;
+        const uint32_t hi = self ? p : n;
+        send_batch(p, tgt & ((1u << hi) - 1u) & ~((1u << nx) - 1u) & ~(1u << p), k2, dot);
+        if (err) return;
+        if (self) {
+          lset(frw, fi, (w & ~(15u << 16)) | ((p + 1u) << 16));
+          from = p;
+          kind = k2;
+          w2 = dot;
+          pend = true;
+          continue;
         }
-        if (pend) continue;
       }
       // ready results -> schedule_to_client (runner.rs:434-440)
       const uint32_t nr = (w >> 20) & 31u;

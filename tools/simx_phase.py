@@ -27,8 +27,8 @@ specs = [S.spec(S.ATLAS if i % 2 == 0 else S.EPAXOS, 5, 1 if i % 2 == 0 else 2, 
 res = S.run(specs, pl, lat_cap=0)
 st = res.stats.astype(np.float64)
 names = ["pop", "event (all)", "x_add", "find_scc", "check_pending", "sort", "emit", "handlers", "send",
-         "gc", "client"]
-counts = {16: "dfs edges", 17: "dfs recursions", 18: "x_add calls", 19: "find_scc calls", 20: "waiters",
+         "gc", "client"]  # slot 11 is a count (cached first finds)
+counts = {11: "cached first finds", 16: "dfs edges", 17: "dfs recursions", 18: "x_add calls", 19: "find_scc calls", 20: "waiters",
           21: "fast-path adds", 22: "events", 23: "sends"}
 ev = st[:, 22].sum()
 tot = st[:, 0].sum() + st[:, 1].sum()
