@@ -334,7 +334,7 @@ def main_sim(args):
 def sim_key(args):
     return "sim_%s_n%d_f%d_s%d_c%s_m%d_seed%d%s" % (
         args.protocol, args.n, args.f, args.seeds, args.conflicts.replace(",", "-"), args.cmds, args.seed,
-        "" if args.clients_per_region == 1 else "_k%d" % args.clients_per_region)
+        "" if (args.clients_per_region or 1) == 1 else "_k%d" % args.clients_per_region)
 
 
 def cpu_baseline_sim(args, specs, rates, executed, executed_len, st, lat_hist, n, exec_cap, planet):
