@@ -327,12 +327,12 @@ struct Sim {
     const uint32_t w = uni(S(sl, SL_PST + (p >> 2)));
     const uint32_t sh = (p & 3u) * 8u;
     const uint32_t nw = (w & ~(0xFFu << sh)) | ((v & 0xFFu) << sh);
-    if (lid == 0) S(sl, SL_PST + (p >> 2)) = nw;
+    S(sl, SL_PST + (p >> 2)) = nw;
   }
-  // store a uniform value from lane 0 (every lane computed the same)
-  __device__ __forceinline__ void put(uint32_t& dst, uint32_t v) {
-    if (lid == 0) dst = v;
-  }
+  // store a uniform value to an LDS word: every lane computed the same value
+  // and stores it (one ds_write; no exec-mask save / restore around a
+  // lane-0-only store, which costs scalar issue slots — the kernel's bound)
+  __device__ __forceinline__ void put(uint32_t& dst, uint32_t v) { dst = v; }
   // set lane `lane` of a lane table
   __device__ __forceinline__ void lset(uint32_t& reg, uint32_t lane, uint32_t v) {
     if (lid == lane) reg = v;
