@@ -122,7 +122,10 @@ def main_sim(args):
         if args.protocol == "epaxos" and args.f == 2:
             args.protocol = "both"
         if args.seeds == 4096:
-            args.seeds = 2048
+            # one resident wavefront per instance: k_simx runs 3 waves per SIMD
+            # (164 VGPRs), 12 per CU x 256 CUs = 3,072 (4,096 adds a second,
+            # one-third-occupied round: 99 -> 72 M cmds/s)
+            args.seeds = 3072
         if args.cmds is None:
             args.cmds = 50
     if args.clients_per_region is None:

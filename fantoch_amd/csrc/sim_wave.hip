@@ -70,6 +70,8 @@ constexpr uint32_t HL_LOG = FX_SIM_HL_LOG, HL_SLOTS = 1u << HL_LOG;  // client-l
 constexpr uint32_t HMAX = 2;             // link heads per lane (links <= 128; a template parameter)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t LNIL = 0xFFFFu;  // end of a link's message list
+// per-process tables packed in one VGPR (lane PT_x + p)
+constexpr uint32_t PT_SEQ = 0, PT_FAST = 8, PT_SLOW = 16, PT_EXEC = 24, PT_OCC = 32, PT_WAIT = 48;
 
 // FX_SIM_PROFILE builds (make prof): shader-clock cycles per event phase in
 // the stats rows (slots 0-15 cycles, 16-23 counts) instead of the counters
@@ -176,7 +178,6 @@ template <uint32_t HM, uint32_t DS, uint32_t NX = NMAX>
 struct Sim {
   // ---------------------------------------------------------------- context
   uint32_t lid;
-  uint64_t lbit;
   SimArgs A;
   Geo g;
   uint32_t* lds;
@@ -207,12 +208,18 @@ struct Sim {
   // index reads them with v_readlane instead of an LDS round trip):
   // lane p: proposal seq, Fast / Slow counters, executed count, the
   // executor's occupancy and waiting masks, fast | write quorum << 8
-  uint32_t pseq = 0, pfast = 0, pslow = 0, pexec = 0, pocc0 = 0, pocc1 = 0, pwm0 = 0, pwm1 = 0, pq = 0;
+  // lane 8 k + p of `pt`: table k of process p (proposal seq, Fast, Slow,
+  // executed count, the executor's occupancy and waiting masks, two words
+  // each) — eight small tables in one VGPR; lane p of `pq`: fast | write quorum << 8
+  uint32_t pt = 0, pq = 0;
   // lane c: process | region << 8, commands issued, start time, results pending
-  uint32_t cpr = 0, ciss = 0, cst = 0, cpend = 0;
-  // link delays (runner.rs:575-595): lane 8 p + q for p -> q; lane c for
-  // client c -> its process (dcs) and back (dcr)
-  uint32_t dpq = 0, dcs = 0, dcr = 0;
+  // lane c / 32 + c of `ca`, `cb`, `cd` (C <= 32): process | region << 8 /
+  // commands issued; start time / results pending; the client -> process
+  // delay / the process -> client delay
+  uint32_t ca = 0, cb = 0, cd = 0;
+  // link delays (runner.rs:575-595): lane 8 p + q for p -> q (the client
+  // links' delays are in cd)
+  uint32_t dpq = 0;
   // handler frame stack, frame fi in lane fi: action (0 none, 1 ToSend) |
   // kind << 2 | targets << 8 | next target << 16 | ready results << 20; dot
   uint32_t frw = 0, frd = 0;
@@ -432,17 +439,18 @@ struct Sim {
       if (head != LNIL) msg(rh >> 16, 3) = e;  // after the tail
     }
     const uint32_t nrh = head == LNIL ? (e | (e << 16)) : (head | (e << 16));
-    // lane base + i = link (p, q(i)) takes lane q(i)'s values
+    // lane base + i = link (p, q(i)) takes lane q(i)'s values: the new list
+    // word, and time (28 bits) | rank << 28 | link was empty << 31 in one word
+    const uint32_t tw = t | (r << 28) | (head == LNIL ? 1u << 31 : 0u);
     const uint32_t i = lid - base;
     const bool ll = lid >= base && i < g.n - 1u;
     const uint32_t q = (ll ? (i < p ? i : i + 1u) : 0u) & 63u;
-    const uint32_t v_nrh = gather(nrh, q), v_t = gather(t, q), v_new = gather(head == LNIL ? 1u : 0u, q);
-    const uint32_t v_sq = seq + gather(r, q);
+    const uint32_t v_nrh = gather(nrh, q), v_tw = gather(tw, q);
     if (ll && ((mask >> q) & 1u)) {
       rhv = v_nrh;
-      if (v_new) {  // the link was empty: the message is its head (P links are lanes < 64)
-        ht[0] = v_t;
-        hs[0] = v_sq;
+      if (v_tw >> 31) {  // the link was empty: the message is its head (P links are lanes < 64)
+        ht[0] = v_tw & 0x0FFFFFFFu;
+        hs[0] = seq + ((v_tw >> 28) & 7u);
       }
     }
     nfree -= k;
@@ -533,13 +541,13 @@ struct Sim {
 
   // Protocol::submit (atlas.rs:210-249, epaxos.rs:199-221)
   __device__ __forceinline__ void h_submit(uint32_t p, uint32_t c) {
-    const uint32_t s = rl(pseq, p) + 1u;
-    lset(pseq, p, s);
+    const uint32_t s = rl(pt, PT_SEQ + p) + 1u;
+    lset(pt, PT_SEQ + p, s);
     if (s > FX_SEQ_MASK) { err = FX_ERR_DOT_RANGE; return; }
     const uint32_t dot = FX_PACK_DOT(p + 1, s);
     const uint32_t sl = slot_alloc();
     if (sl == NONE) { fail_cap(__LINE__); return; }
-    const uint32_t idx = rl(ciss, c) - 1u;
+    const uint32_t idx = rl(ca, 32u + c) - 1u;
     uint32_t nk = 0;
     const uint32_t keys = gen_keys(c + 1, idx, nk);
     // fresh slot
@@ -637,10 +645,7 @@ struct Sim {
     if (first) S(sl, g.sl_value + rank) = v;
     const uint32_t c0 = uni(S(sl, SL_CNT));
     put(S(sl, SL_CNT), (c0 & ~0xFFu) | nu | (fast ? 0u : (1u << 16)));  // slow: proposer ballot set
-    if (lid == p) {
-      if (fast) ++pfast;
-      else ++pslow;
-    }
+    if (lid == (fast ? PT_FAST : PT_SLOW) + p) ++pt;
     if (fast) {
       act_send(M_COMMIT, dot, (1u << n) - 1u);
     } else {
@@ -856,7 +861,11 @@ struct Sim {
   }
 
   // ===================================================== GraphExecutor
-  __device__ __forceinline__ bool mine(uint64_t m) const { return (m & lbit) != 0; }
+  // lane bit of a wave-uniform 64-bit mask (no per-lane 64-bit lane mask kept live)
+  __device__ __forceinline__ bool mine(uint64_t m) const {
+    const uint32_t half = lid < 32u ? (uint32_t)m : (uint32_t)(m >> 32);
+    return (half >> (lid & 31u)) & 1u;
+  }
   __device__ __forceinline__ uint32_t vcount_of(uint32_t d) { return uni(S(slot_find(d), SL_CNT)) & 0xFFu; }
   __device__ __forceinline__ uint32_t value_at(uint32_t d, uint32_t j) { return uni(S(slot_find(d), g.sl_value + j)); }
 
@@ -868,21 +877,22 @@ struct Sim {
     stl = 0;
     sfr = 0;
     epoch = 1;
-    occ = (uint64_t)rl(pocc0, p) | ((uint64_t)rl(pocc1, p) << 32);
-    wmask = (uint64_t)rl(pwm0, p) | ((uint64_t)rl(pwm1, p) << 32);
-    xk = rl(pexec, p);
+    occ = (uint64_t)rl(pt, PT_OCC + p) | ((uint64_t)rl(pt, PT_OCC + 8u + p) << 32);
+    wmask = (uint64_t)rl(pt, PT_WAIT + p) | ((uint64_t)rl(pt, PT_WAIT + 8u + p) << 32);
+    xk = rl(pt, PT_EXEC + p);
     tmask = 0;
     phase = PH_IDLE;
   }
   __device__ __forceinline__ void x_store() {
     const uint32_t p = xp;
     rput(xdot, p, sdot); rput(xrec, p, srec); rput(xwait, p, swait);
-    if (lid == p) {
-      pocc0 = (uint32_t)occ;
-      pocc1 = (uint32_t)(occ >> 32);
-      pwm0 = (uint32_t)wmask;
-      pwm1 = (uint32_t)(wmask >> 32);
-      pexec = xk;
+    if ((lid & 7u) == p) {
+      const uint32_t k = lid >> 3;
+      if (k == PT_OCC / 8u) pt = (uint32_t)occ;
+      else if (k == PT_OCC / 8u + 1u) pt = (uint32_t)(occ >> 32);
+      else if (k == PT_WAIT / 8u) pt = (uint32_t)wmask;
+      else if (k == PT_WAIT / 8u + 1u) pt = (uint32_t)(wmask >> 32);
+      else if (k == PT_EXEC / 8u) pt = xk;
     }
   }
 
@@ -948,10 +958,10 @@ struct Sim {
     if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
     const uint32_t c = uni(S(sl, SL_CLIENT));
     const uint32_t nk = (uni(S(sl, SL_CNT)) >> 20) & 3u;
-    if ((rl(cpr, c) & 0xFFu) == p) {  // pending.wait_for registered this rifl at p
-      const uint32_t pend = rl(cpend, c);
+    if ((rl(ca, c) & 0xFFu) == p) {  // pending.wait_for registered this rifl at p
+      const uint32_t pend = rl(cb, 32u + c);
       if (pend < nk) { err = FX_ERR_SIM_LATE; return; }
-      lset(cpend, c, pend - nk);  // one ExecutorResult per key
+      lset(cb, 32u + c, pend - nk);  // one ExecutorResult per key
       if (pend == nk) {
         const uint32_t fi = nfrm - 1;
         const uint32_t w = rl(frw, fi);
@@ -1256,7 +1266,7 @@ struct Sim {
       const uint32_t nr = (w >> 20) & 31u;
       for (uint32_t r = 0; r < nr; ++r) {
         const uint32_t c = uni(FRR(fi, r));
-        schedule_timer(link_r(c), rl(dcr, c));
+        schedule_timer(link_r(c), rl(cd, 32u + c));
       }
       --nfrm;
     }
@@ -1265,13 +1275,11 @@ struct Sim {
   // ======================================================= event loop
   // Client::cmd_send: next command of client c (0-based) -> SubmitToProc
   __device__ __forceinline__ bool client_send(uint32_t c) {
-    const uint32_t issued = rl(ciss, c);
+    const uint32_t issued = rl(ca, 32u + c);
     if (issued >= cmds) return false;
-    if (lid == c) {
-      ciss = issued + 1u;
-      cst = now;  // Pending::start
-    }
-    schedule_timer(link_s(c), rl(dcs, c));
+    lset(ca, 32u + c, issued + 1u);
+    lset(cb, c, now);  // Pending::start
+    schedule_timer(link_s(c), rl(cd, c));
     return true;
   }
 
@@ -1304,9 +1312,9 @@ struct Sim {
     if (x < g.C) {  // S(c): SubmitToProc
       const uint32_t c = x;
       head_set(link, NONE, NONE);
-      const uint32_t p = rl(cpr, c) & 0xFFu;
-      note(2, p + 1, c + 1, rl(ciss, c));
-      lset(cpend, c, g.K);  // AggregatePending::wait_for: key_count results
+      const uint32_t p = rl(ca, c) & 0xFFu;
+      note(2, p + 1, c + 1, rl(ca, 32u + c));
+      lset(cb, 32u + c, g.K);  // AggregatePending::wait_for: key_count results
       run_handlers(p, p, M_SUBMIT, c);
       return;
     }
@@ -1315,11 +1323,11 @@ struct Sim {
     {  // R(c): SendToClient -> Client::cmd_recv + cmd_send (simulation.rs:132-149)
       const uint32_t c = x;
       head_set(link, NONE, NONE);
-      const uint32_t issued = rl(ciss, c);
+      const uint32_t issued = rl(ca, 32u + c);
       note(4, c + 1, 0, issued);
-      const uint32_t lat = now - rl(cst, c);  // latency.as_millis()
+      const uint32_t lat = now - rl(cb, c);  // latency.as_millis()
       lat_sum += lat;
-      const uint32_t region = rl(cpr, c) >> 8;
+      const uint32_t region = rl(ca, c) >> 8;
       if (lid == 0) {
         if (A.latency_log && issued - 1u < A.lat_cap)
           A.latency_log[((size_t)inst * g.C + c) * A.lat_cap + issued - 1u] = lat;
@@ -1386,7 +1394,6 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
 #pragma unroll
   for (uint32_t k = 0; k < DS; ++k) s.sdv[k] = 0;
   s.lid = threadIdx.x;
-  s.lbit = 1ull << s.lid;
   s.A = a;
   s.g = a.g;
   s.lds = smem;
@@ -1462,10 +1469,10 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
       }
       for (uint32_t i = 0; i < sp.clients_per_region; ++i, ++c) {
         if (s.lid == c) {
-          s.cpr = best | (rc << 8);
-          s.dcs = a.ping[rc * RP + sp.process_regions[best]] / 2u;
-          s.dcr = a.ping[sp.process_regions[best] * RP + rc] / 2u;
+          s.ca = best | (rc << 8);
+          s.cd = a.ping[rc * RP + sp.process_regions[best]] / 2u;
         }
+        if (s.lid == 32u + c) s.cd = a.ping[sp.process_regions[best] * RP + rc] / 2u;
       }
     }
   }
@@ -1524,13 +1531,15 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
   }
   // ----------------------------------------------------------- outputs
   __builtin_amdgcn_s_barrier();
-  if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = s.pexec;
+  const uint32_t o_exec = gather(s.pt, (PT_EXEC + s.lid) & 63u), o_fast = gather(s.pt, (PT_FAST + s.lid) & 63u),
+                 o_slow = gather(s.pt, (PT_SLOW + s.lid) & 63u);
+  if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = o_exec;
   if (a.stats) {
     unsigned long long* st = a.stats + (size_t)inst * FX_SIM_STATS;
     if (s.lid < NMAX) {
       const bool v = s.lid < n;
-      st[FX_SIM_STAT_FAST + s.lid] = v ? s.pfast : 0u;
-      st[FX_SIM_STAT_SLOW + s.lid] = v ? s.pslow : 0u;
+      st[FX_SIM_STAT_FAST + s.lid] = v ? o_fast : 0u;
+      st[FX_SIM_STAT_SLOW + s.lid] = v ? o_slow : 0u;
       st[FX_SIM_STAT_STABLE + s.lid] = 0u;
       st[FX_SIM_STAT_FAST_READS + s.lid] = 0u;  // no read-only commands on this kernel
       st[FX_SIM_STAT_SLOW_READS + s.lid] = 0u;
