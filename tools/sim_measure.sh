@@ -35,6 +35,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $M/huge_trace -o run --out
 timeout -k 10 600 python3 bench.py --mode placements --cmds 100 --steps 1 --warmup 0 > $M/placements.log 2>&1 \
   || { echo "placements rc=$?"; tail -20 $M/placements.log; exit 1; }
 tail -1 $M/placements.log | cut -c1-300
+timeout -k 10 400 python3 bench.py --mode dense-sim > $M/dense_sim.log 2>&1 || { echo "dense-sim rc=$?"; tail -20 $M/dense_sim.log; exit 1; }
+tail -1 $M/dense_sim.log | cut -c1-300
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $M/dense_sim_trace -o run --output-format csv -- \
+  python3 bench.py --mode dense-sim --no-cpu-baseline > $M/dense_sim_trace.log 2>&1 || { echo "dense-sim trace rc=$?"; exit 1; }
 timeout -k 10 300 python3 bench.py --mode dense > $M/dense.log 2>&1 || { echo "dense rc=$?"; tail -20 $M/dense.log; exit 1; }
 tail -1 $M/dense.log | cut -c1-300
 timeout -k 10 300 python3 bench.py --mode pred > $M/pred.log 2>&1 || { echo "pred rc=$?"; tail -20 $M/pred.log; exit 1; }
