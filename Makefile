@@ -17,8 +17,15 @@ HDRS := include/fantoch_amd.h include/fantoch_amd.hpp fantoch_amd/csrc/fx_synth.
 
 all: $(LIB) $(ORACLE) $(CPPTEST)
 
-$(LIB): $(SRCS) $(HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+# one object per source (make -j compiles them in parallel), then one link
+OBJDIR := fantoch_amd/build/obj
+OBJS := $(patsubst fantoch_amd/csrc/%,$(OBJDIR)/%.o,$(SRCS))
+$(OBJDIR)/%.o: fantoch_amd/csrc/% $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
 
 # phase-cycle profile build of the simulator (tools/sim_phase.py; FX_LIB=...)
 PROF_LIB := fantoch_amd/build_prof/libfantoch_amd.so
@@ -26,6 +33,15 @@ prof: $(PROF_LIB)
 $(PROF_LIB): $(SRCS) $(HDRS)
 	@mkdir -p fantoch_amd/build_prof
 	$(HIPCC) $(HIPFLAGS) -DFX_SIM_PROFILE -shared -o $@ $(SRCS)
+
+# measurement-only variants of the library (A/B and ablations, FX_LIB=...):
+# make variant V=name D="-DFOO=1" rebuilds sim_wave.hip with the extra flags
+# and links it with the other objects into fantoch_amd/build_$(V)/
+variant: $(OBJS)
+	@mkdir -p fantoch_amd/build_$(V)
+	$(HIPCC) $(HIPFLAGS) $(D) -c -o fantoch_amd/build_$(V)/sim_wave.o fantoch_amd/csrc/sim_wave.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o fantoch_amd/build_$(V)/libfantoch_amd.so \
+	  $(filter-out $(OBJDIR)/sim_wave.hip.o,$(OBJS)) fantoch_amd/build_$(V)/sim_wave.o
 
 ORACLE_SRCS := oracle/graph_oracle.cpp oracle/sim_oracle.cpp oracle/pred_oracle.cpp
 $(ORACLE): $(ORACLE_SRCS) oracle/graph_oracle.hpp include/fantoch_amd.h

@@ -77,6 +77,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-baseline-seconds", type=float, default=None,
                     help="CPU work budget of the cpu_baseline sample (sim default 15, executor 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--generic", action="store_true",
+                    help="simulator: the run-time-geometry kernel build even for a compiled-in geometry (A/B)")
     ap.add_argument("--placement-conflict", type=int, default=2,
                     help="placements mode (BASELINE configs[2]): conflict rate of every placement")
     ap.add_argument("--placement-limit", type=int, default=None,

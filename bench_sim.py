@@ -170,7 +170,8 @@ def main_sim(args):
     delay = torch.zeros(DELAY_BINS, dtype=torch.int64, device=dev)
     stats = torch.zeros(N * _lib.FX_SIM_STATS, dtype=torch.int64, device=dev)
     err = torch.zeros(N, dtype=torch.int32, device=dev)
-    batch = _lib.SimBatch(spec_dev.data_ptr(), ctypes.addressof(host), N, 0, ping.data_ptr(),
+    sim_flags = _lib.FX_SIM_FLAG_GENERIC if getattr(args, "generic", False) else 0
+    batch = _lib.SimBatch(spec_dev.data_ptr(), ctypes.addressof(host), N, sim_flags, ping.data_ptr(),
                           rank_m.data_ptr(), planet.R, S.Planet.STRIDE, exec_cap, 0, 0,
                           args.ring_entries, args.dot_slots, 0)
     out = _lib.SimOutput(executed.data_ptr(), executed_len.data_ptr(), None, lat_hist.data_ptr(),

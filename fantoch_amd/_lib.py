@@ -34,6 +34,7 @@ FX_PROTOCOL_EPAXOS = 1
 FX_PROTOCOL_BASIC = 2
 FX_SIM_FLAG_EXEC_NOTIFICATIONS = 1
 FX_SIM_FLAG_LARGE = 2
+FX_SIM_FLAG_GENERIC = 4
 FX_SIM_STAT_FAST, FX_SIM_STAT_SLOW, FX_SIM_STAT_STABLE = 0, 8, 16
 FX_SIM_STAT_EVENTS, FX_SIM_STAT_END_MS, FX_SIM_STAT_TRACE, FX_SIM_STAT_SEQ = 24, 25, 26, 27
 FX_SIM_STAT_DEPS = 28

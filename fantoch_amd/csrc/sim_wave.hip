@@ -44,6 +44,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstring>
 #include <vector>
 
 #include "fantoch_amd.h"
@@ -61,12 +63,8 @@ constexpr uint32_t VMAX = 16;            // deps of a committed value (per-launc
 // last max-distance + interval, the change log the moves of the last interval
 constexpr uint32_t FMAX = 12;            // frame stack depth
 constexpr uint32_t RDMAX = 16;           // ready results per frame
-constexpr uint32_t HC_BINS = 64;         // ChainSize bins counted per instance in LDS
-constexpr uint32_t HD_BINS = 256;        // ExecutionDelay bins counted per instance in LDS
-#ifndef FX_SIM_HL_LOG
-#define FX_SIM_HL_LOG 6  // 64 entries: with them the configs[1] geometry fits 16 instances per CU
-#endif
-constexpr uint32_t HL_LOG = FX_SIM_HL_LOG, HL_SLOTS = 1u << HL_LOG;  // client-latency cache entries per instance
+constexpr uint32_t HC_BINS = 64;         // ChainSize values counted per instance in lanes
+constexpr uint32_t HD_BINS = 256;        // ExecutionDelay values counted per instance in LDS
 constexpr uint32_t HMAX = 2;             // link heads per lane (links <= 128; a template parameter)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t LNIL = 0xFFFFu;  // end of a link's message list
@@ -103,8 +101,105 @@ constexpr uint32_t SL_CLIENT = 1,  // word 0 spare (the slot's dot lives in lane
 struct Geo {  // launch-uniform geometry
   uint32_t n, C, K, W, R, L, NP, ncli_keys, rt, rc;
   uint32_t amax, vmax, sl_value, sl_ack, slotw;  // dot-slot layout (MCollectAck deps <= 2K, value <= K(n+1))
-  uint32_t off_pool, off_free, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_frame, off_wl, off_hist, off_lat,
-      words;
+  uint32_t off_pool, off_free, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_frame, off_wl, off_hist, words;
+};
+
+__host__ __device__ constexpr uint32_t cmin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__host__ __device__ constexpr uint32_t cmax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+// the launch geometry of n processes, C clients, K keys per command and a
+// conflict pool of `pool` keys; ring / wslots = 0: the defaults.  constexpr:
+// the fixed-geometry kernels (GeoCT) fold it into immediates
+__host__ __device__ constexpr bool geo_make(uint32_t n, uint32_t C, uint32_t K, uint32_t pool, uint32_t ring,
+                                            uint32_t wslots, Geo& g) {
+  if (n < 2 || n > NMAX) return false;
+  if (C < 1 || C > CMAX) return false;
+  g.n = n;
+  g.C = C;
+  g.K = K;
+  // table sizes: small by default (LDS decides how many instances share a CU);
+  // fx_sim_run_tiered reruns the instances that outgrow them with 256 dots
+  const uint32_t cpr = (C + n - 1) / n;  // clients per process region
+  // live dots per instance: 8 per client, at most 64; 32 for n > 5 with one
+  // client per region (configs[2]'s n = 7: 12.4 KB instead of 15.4 KB, 13
+  // instances per CU instead of 10, the same reruns; 24 reran more, 16 lost 4x)
+  g.W = wslots ? wslots : (n > 5 && C <= 8 ? 32u : cmin(64u, 8u * C));
+  if (g.W > 256u) return false;
+  // messages in flight per instance: 16 per process and client; at least 192
+  // for n > 5, where a lagging far replica overflowed the smaller pool often
+  // enough (reruns at 4x) that the larger table wins despite fewer instances
+  // per CU (configs[2] sweep)
+  g.R = ring ? ring : cmin(4096u, cmax(16u * n * cpr, n > 5 ? 192u : 0u));
+  if (g.R > 65534u) return false;
+  g.NP = n * (n - 1);
+  g.L = g.NP + n + 2 * C;
+  if (g.L > 64 * HMAX) return false;
+  g.ncli_keys = pool + C + 1;
+  // an MCollectAck carries the coordinator's deps plus the replica's latest
+  // write per key (<= 2K); a committed value is their union over the fast
+  // quorum (<= K (n + 1): the coordinator's past plus one latest per member)
+  g.amax = 2 * g.K;
+  g.vmax = cmin(VMAX, g.K * (n + 1));
+  g.sl_value = SL_COLLECT + g.K;
+  g.sl_ack = g.sl_value + g.vmax;
+  g.slotw = g.sl_ack + n * g.amax;
+  if (n * g.amax > 64 || g.slotw > 64) return false;
+  uint32_t o = 0;
+  // messages in flight: one pool per instance, a FIFO list per process link
+  g.off_pool = o; o += g.R * 4;
+  g.off_free = o; o += g.R;
+  // GC logs: 4 / 2 entries per client per region (commits of one source
+  // arrive about once per client round trip), 32 / 16 in the rerun geometry
+  g.rt = 4;
+  while (g.rt < 4 * cpr && g.rt < 64) g.rt <<= 1;
+  if (g.W > 64u) g.rt = cmax(g.rt, 32u);
+  g.rc = g.rt / 2;
+  g.off_gct = o; o += n * n * g.rt * 2;
+  g.off_gcc = o; o += n * n * g.rc * 2;
+  g.off_gcr = o; o += n * n * 4;
+  g.off_slot = o; o += g.W * g.slotw;
+  g.off_kd = o; o += n * g.ncli_keys;
+  g.off_frame = o; o += FMAX * RDMAX;
+  g.off_wl = o; o += 72;
+  g.off_hist = o; o += HD_BINS;
+  g.words = (o + 3) & ~3u;
+  return true;
+}
+__host__ __device__ constexpr Geo geo_fixed(uint32_t n, uint32_t C) {
+  Geo g{};
+  geo_make(n, C, 1, 1, 0, 0, g);
+  return g;
+}
+
+// Geometry policy of a kernel build.  GeoRT: the launch's geometry arrives in
+// the kernel arguments (any batch the all-on-chip kernel takes).  GeoCT: one
+// BASELINE geometry (protocol, n, f, one client per region, one key per
+// command, a one-key conflict pool, default tables) compiled in, so table
+// offsets, link arithmetic and quorum sizes are immediates and their scalar
+// registers and instructions go away (the kernel is bound by scalar issue).
+// xp_lanes: the executors' slot tables.  0: one 64-lane table per process
+// (xdot / xrec / xwait[NX]), swapped into the working registers for each Add.
+// > 0: ONE table whose lanes are split between the processes, xp_lanes each
+// (process p owns lanes [p xp_lanes, (p + 1) xp_lanes)), so an Add works on
+// the table in place: no swap, and occupancy / waiting masks are ballots of
+// the lanes (a slot is occupied iff its dot is non-zero, waiting iff its
+// waited-on dot is).  A process that needs more pending slots fails with
+// FX_ERR_SIM_CAPACITY and fx_sim_run_tiered reruns the instance on the
+// run-time build's larger tables.
+struct GeoRT {
+  static constexpr bool fixed = false;
+  static constexpr uint32_t proto = 0xFFu, fc = 0xFFu, xp_lanes = 0;
+  Geo g;
+};
+template <uint32_t PR, uint32_t N, uint32_t F, uint32_t CC>
+struct GeoCT {
+  static constexpr bool fixed = true;
+#ifdef FX_XSWAP
+  static constexpr uint32_t proto = PR, fc = F, xp_lanes = 0;
+#else
+  static constexpr uint32_t proto = PR, fc = F, xp_lanes = 64u / N;
+#endif
+  static constexpr Geo g = geo_fixed(N, CC);
 };
 
 struct SimArgs {
@@ -127,6 +222,25 @@ struct SimArgs {
   unsigned long long* stats;
   uint32_t* err;
 };
+
+// The kernel's arguments, read where a rarely taken path needs them through
+// the kernarg segment (scalar loads, scalar-cache hits) instead of being held
+// in scalar registers for the whole run: the simulator is short of SGPRs, and
+// every spilled one costs a v_readlane / v_writelane pair on the hot path.
+// The empty asm makes the pointer opaque so the loads are not hoisted.
+typedef __attribute__((address_space(4))) const SimArgs KSimArgs;
+__device__ __forceinline__ KSimArgs* kargs() {
+  KSimArgs* p = (KSimArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+// a copy of a uniform value the compiler must treat as per-lane: arithmetic
+// on it runs on the (mostly idle) vector unit instead of the scalar unit
+__device__ __forceinline__ uint32_t vdiv(uint32_t x) {
+  uint32_t r;
+  asm("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t src) {
@@ -174,30 +288,56 @@ __device__ __forceinline__ uint32_t tmk(uint32_t id, uint32_t low, uint32_t ep) 
 constexpr uint32_t EPOCH_MAX = 0xFFFFu;
 
 // NX: processes the executor slot tables are sized for (n <= NX)
-template <uint32_t HM, uint32_t DS, uint32_t NX = NMAX>
-struct Sim {
+template <uint32_t HM, uint32_t DS, uint32_t NX, class GP>
+struct Sim : GP {
+  using GP::g;
   // ---------------------------------------------------------------- context
   uint32_t lid;
-  SimArgs A;
-  Geo g;
   uint32_t* lds;
-  uint32_t inst;
-  uint64_t seed, rng_inst;
-  uint32_t protocol, n, f, synod_f, fq, wq, gc_ms, en_ms, cmds, conflict, pool, extra;
-  bool has_extra;
+  uint32_t protocol, n, f, synod_f, fq, wq;
+  // Per-instance parameters and rarely changed values in lanes of one VGPR
+  // (lane P_*), read with v_readlane where they are used: kept in scalar
+  // registers for the whole run they pushed hot values into spill slots.
+  enum : uint32_t { P_SEED = 0, P_RNG = 2, P_GC = 4, P_EN = 5, P_CMDS = 6, P_CONFLICT = 7, P_POOL = 8, P_EXTRA = 9,
+                    P_HAS_EXTRA = 10, P_FINAL = 11, P_CDONE = 12, P_ERRSITE = 13, P_INST = 14 };
+  uint32_t pv = 0;
+  // one v_readlane at each use (volatile: not hoisted into a scalar register
+  // for the whole loop); it reads the lane whatever the exec mask, so it is
+  // also right inside lane-divergent code
+  __device__ __forceinline__ uint32_t prm(uint32_t k) const {
+    uint32_t r;
+    // s_nop: the hazard recognizer does not see the asm's SGPR write (a VALU
+    // write read by a VMEM / lane-select operand needs wait states)
+    asm volatile("v_readlane_b32 %0, %1, %2\n\ts_nop 4" : "=s"(r) : "v"(pv), "i"(k));
+    return r;
+  }
+  __device__ __forceinline__ uint64_t prm64(uint32_t k) const {
+    return (uint64_t)prm(k) | ((uint64_t)prm(k + 1) << 32);
+  }
+  __device__ __forceinline__ void prm_set(uint32_t k, uint32_t x) {
+    if (lid == k) pv = x;
+  }
   uint32_t C;
   uint32_t err = 0;
-  uint32_t err_site = 0;  // source line of the first capacity failure (diagnostics)
+  // source line of the first capacity failure (diagnostics): lane P_ERRSITE
   __device__ __forceinline__ void fail_cap(uint32_t line) {
-    if (!err) err_site = line;
+    if (!err) prm_set(P_ERRSITE, line);
     err = FX_ERR_SIM_CAPACITY;
   }
   uint32_t now = 0;       // ms
   uint32_t seq = 0;       // insertion counter (C3)
-  uint64_t events = 0, trace = 0, deps_total = 0, lat_sum = 0;
-  uint32_t clients_done = 0;
+  uint32_t events = 0;  // <= max_events < 2^32
+  // per-lane (vector-unit) bookkeeping, every lane holds the same value: the
+  // action trace hash, deps and latency sums
+  uint64_t trace, deps_total, lat_sum;
+  // histogram samples counted per instance: ChainSize value v < 64 in lane v
+  // of hcv, ExecutionDelay value v < 256 in LDS word v of the instance's
+  // table, client latencies in a direct-mapped cache keyed by (region,
+  // latency): lane h holds key + 1 (hlk) and its count (hlc); everything else
+  // goes to the global bins directly; the bins are clamped when the counts are
+  // flushed (exact)
+  uint32_t hcv = 0, hlk = 0, hlc = 0;
   bool done = false, in_extra = false;
-  uint32_t final_ms = 0;
 
   // link heads owned by this lane: time, seq (time NONE = empty)
   uint32_t ht[HM], hs[HM];
@@ -236,6 +376,8 @@ struct Sim {
   // DFS frames only live during one handle_add
   uint32_t sdot, srec, swait, stl, sfr;
   uint64_t occ, wmask, tmask;
+  static constexpr uint32_t XPL = GP::xp_lanes;
+  uint64_t pmask = ~0ull;  // lanes of the running process's slots
   uint32_t xk, epoch, nwl, phase, root, idc, nfr, missing, fv, fdi, fnc, in_try, emitted, xp;
 #ifdef FX_SIM_PROFILE
   uint64_t prof[24] = {};
@@ -292,38 +434,42 @@ struct Sim {
   // histograms once at the end: one global atomic per sample made every
   // executed command a device-scope atomic on the same few bins.
   __device__ __forceinline__ void hist_chain(uint32_t v) {
-    if (!A.chain_hist) return;
-    const uint32_t b = min(v, A.chain_bins - 1u);
-    if (lid == 0) {
-      if (b < HC_BINS) atomicAdd(&lds[g.off_hist + b], 1u);
-      else atomicAdd(&A.chain_hist[b], 1ull);
+    if (v < HC_BINS) {
+      hcv += lid == v ? 1u : 0u;
+    } else if (lid == 0) {
+      KSimArgs* k = kargs();
+      if (k->chain_hist) atomicAdd(&k->chain_hist[min(v, k->chain_bins - 1u)], 1ull);
     }
   }
   // client latency samples: a direct-mapped per-instance cache of (region,
   // bin) -> count (a region's latencies take few distinct values); a sample
   // whose entry is taken by another bin goes to the global bin directly
   __device__ __forceinline__ void hist_lat(uint32_t region, uint32_t lat) {
-    if (!A.lat_hist) return;
-    const uint32_t key = region * A.lat_bins + min(lat, A.lat_bins - 1u);
-    const uint32_t h = (key * 2654435761u) >> (32 - HL_LOG);
-    const uint32_t k = uni(lds[g.off_lat + h]);
-    if (lid == 0) {
-      if (k == key + 1u) {
-        atomicAdd(&lds[g.off_lat + HL_SLOTS + h], 1u);
-      } else if (k == 0) {
-        lds[g.off_lat + h] = key + 1u;
-        lds[g.off_lat + HL_SLOTS + h] = 1u;
-      } else {
-        atomicAdd(&A.lat_hist[key], 1ull);
+    const uint32_t key = (region << 24) | min(lat, 0xFFFFFFu);
+    const uint32_t h = (key * 2654435761u) >> 26;
+    const uint32_t k = rl(hlk, h);
+    if (k == key + 1u || k == 0) {
+      if (lid == h) {
+        hlk = key + 1u;
+        ++hlc;
       }
+    } else {
+      flush_lat(key, 1u);
+    }
+  }
+  __device__ __forceinline__ void flush_lat(uint32_t key, uint32_t cnt) {
+    if (lid == 0) {
+      KSimArgs* k = kargs();
+      const uint32_t lat = key & 0xFFFFFFu, bins = k->lat_bins;
+      if (k->lat_hist) atomicAdd(&k->lat_hist[(key >> 24) * bins + min(lat, bins - 1u)], (unsigned long long)cnt);
     }
   }
   __device__ __forceinline__ void hist_delay(uint32_t v) {
-    if (!A.delay_hist) return;
-    const uint32_t b = min(v, A.delay_bins - 1u);
-    if (lid == 0) {
-      if (b < HD_BINS) atomicAdd(&lds[g.off_hist + HC_BINS + b], 1u);
-      else atomicAdd(&A.delay_hist[b], 1ull);
+    if (v < HD_BINS) {
+      if (lid == 0) atomicAdd(&lds[g.off_hist + v], 1u);
+    } else if (lid == 0) {
+      KSimArgs* k = kargs();
+      if (k->delay_hist) atomicAdd(&k->delay_hist[min(v, k->delay_bins - 1u)], 1ull);
     }
   }
 
@@ -472,6 +618,8 @@ struct Sim {
   // Workload::gen_cmd (workload.rs:142-197) keys of command idx of client c
   // (1-based id), canonical C6/C7/C11: packed key0 | key1 << 16, count
   __device__ __forceinline__ uint32_t gen_keys(uint32_t cid, uint32_t idx, uint32_t& nk) {
+    const uint64_t seed = prm64(P_SEED), rng_inst = prm64(P_RNG);
+    const uint32_t conflict_ = prm(P_CONFLICT), pool = prm(P_POOL);
     uint32_t k0 = 0xFFFFu, k1 = 0xFFFFu;
     nk = 0;
     for (uint32_t draw = 0; nk < g.K && draw < 65536u; ++draw) {  // gen_unique_keys draws until distinct
@@ -489,11 +637,9 @@ struct Sim {
     if (nk == 2 && k1 < k0) { const uint32_t t = k0; k0 = k1; k1 = t; }  // C11
     return k0 | (k1 << 16);
   }
-  uint32_t conflict_;
 
   // ------------------------------------------------------- frame stack
   uint32_t nfrm = 0;  // frames in use
-  uint32_t cur_p = 0; // process of the current frame chain (0-based)
   uint32_t xinfo = 0; // execution info pushed by the current handler (dot, 0 = none)
 
   __device__ __forceinline__ void act_send(uint32_t kind, uint32_t dot, uint32_t tgt) {
@@ -671,7 +817,7 @@ struct Sim {
     // Forward(MCommitDot) to self: it only moves the GC track's committed
     // clock (gc/clock.rs:43-48), which nothing but the GC evaluation reads,
     // so it is applied in place
-    if (gc_ms) h_mcommitdot(p, dot);
+    if (prm(P_GC)) h_mcommitdot(p, dot);
   }
 
   // atlas.rs:477-524 / epaxos.rs:430-477
@@ -725,6 +871,9 @@ struct Sim {
 
   // MCommitDot: add_to_clock (gc/clock.rs:43-48)
   __device__ __forceinline__ void h_mcommitdot(uint32_t p, uint32_t dot) {
+#ifdef FX_ABL_GC
+    return;
+#endif
     const uint32_t si = (dot >> FX_SEQ_BITS) - 1u, sq = dot & FX_SEQ_MASK;
     bool bad = false;
     if (lid == p * 8u + si && sq > gf) {
@@ -739,6 +888,7 @@ struct Sim {
         const uint32_t ones = __builtin_ctz(~win);
         gf = gf + 1 + ones;
         gw = win >> ones;
+        const uint32_t gc_ms = prm(P_GC);
         if (gc_ms) {
           const uint32_t kt = now ? (now - 1u) / gc_ms : 0u;  // ticks strictly before now
           if (gnt == 0 || kt != glk) {
@@ -797,6 +947,7 @@ struct Sim {
   // first GC action after time x: its time, and (ticks first, then
   // deliveries by (from, to)) the delivery it is, or NONE for a tick
   __device__ __forceinline__ uint32_t gc_next_after(uint32_t x, uint32_t& pair) {
+    const uint32_t gc_ms = prm(P_GC);
     const uint32_t tick = (x / gc_ms + 1u) * gc_ms;
     uint32_t tv = NONE;
     const uint32_t p = lid >> 3, q = lid & 7u;
@@ -819,6 +970,7 @@ struct Sim {
   // before time tc, plus the delivery `pair` (8 from + to) at tc if the run
   // stopped on it
   __device__ __forceinline__ void gc_finish(uint32_t tc, uint32_t pair, unsigned long long* st) {
+    const uint32_t gc_ms = prm(P_GC);
     if (gc_lane(lid >> 3)) {
       uint32_t* r = gcr(lid >> 3, lid & 7u);
       r[0] = gf;
@@ -871,20 +1023,34 @@ struct Sim {
 
   __device__ __forceinline__ void x_load(uint32_t p) {
     xp = p;
-    sdot = rsel(xdot, p); srec = rsel(xrec, p); swait = rsel(xwait, p);
+    // the search state is written before it is read in every Add; fixing it
+    // here makes its values dead between Adds (no scalar registers held
+    // across the event loop)
+    root = idc = nfr = missing = fv = fdi = fnc = in_try = emitted = nwl = 0;
     // Tarjan ids are reset at the end of every search (finalize) and the
     // visited marks only matter inside one try_pending: a fresh epoch per call
     stl = 0;
     sfr = 0;
     epoch = 1;
-    occ = (uint64_t)rl(pt, PT_OCC + p) | ((uint64_t)rl(pt, PT_OCC + 8u + p) << 32);
-    wmask = (uint64_t)rl(pt, PT_WAIT + p) | ((uint64_t)rl(pt, PT_WAIT + 8u + p) << 32);
+    if constexpr (XPL != 0) {
+      pmask = ((1ull << XPL) - 1ull) << (p * XPL);
+      occ = bal(sdot != 0u) & pmask;
+      wmask = bal(swait != 0u) & pmask;
+    } else {
+      sdot = rsel(xdot, p); srec = rsel(xrec, p); swait = rsel(xwait, p);
+      occ = (uint64_t)rl(pt, PT_OCC + p) | ((uint64_t)rl(pt, PT_OCC + 8u + p) << 32);
+      wmask = (uint64_t)rl(pt, PT_WAIT + p) | ((uint64_t)rl(pt, PT_WAIT + 8u + p) << 32);
+    }
     xk = rl(pt, PT_EXEC + p);
     tmask = 0;
     phase = PH_IDLE;
   }
   __device__ __forceinline__ void x_store() {
     const uint32_t p = xp;
+    if constexpr (XPL != 0) {
+      lset(pt, PT_EXEC + p, xk);
+      return;
+    }
     rput(xdot, p, sdot); rput(xrec, p, srec); rput(xwait, p, swait);
     if ((lid & 7u) == p) {
       const uint32_t k = lid >> 3;
@@ -949,8 +1115,10 @@ struct Sim {
   // AggregatePending (runner.rs:406-424), executor metrics, execution log
   __device__ __forceinline__ void on_execute(uint32_t d, uint32_t start) {
     const uint32_t p = xp;
-    if (xk < A.exec_cap && A.executed && lid == 0)
-      A.executed[((size_t)inst * n + p) * A.exec_cap + xk] = d;
+    if (lid == 0) {
+      KSimArgs* k = kargs();
+      if (xk < k->exec_cap && k->executed) k->executed[((size_t)prm(P_INST) * n + p) * k->exec_cap + xk] = d;
+    }
     ++xk;
     const uint32_t delay = now - start;  // ExecutionDelay (graph/mod.rs:514-518)
     hist_delay(delay);
@@ -986,7 +1154,7 @@ struct Sim {
   }
 
   __device__ __forceinline__ int insert_vertex(uint32_t d) {
-    const uint64_t fre = ~occ;
+    const uint64_t fre = ~occ & pmask;
     if (!fre) { fail_cap(__LINE__); return -1; }
     const uint32_t sl = ctz64(fre);
     if (lid == sl) {
@@ -1035,6 +1203,12 @@ struct Sim {
       if (err) return;
     }
     nwl += cnt;
+    if constexpr (XPL != 0) {
+      if (mem) {  // the slots are free again
+        sdot = 0;
+        swait = 0;
+      }
+    }
     occ &= ~mm;
     wmask &= ~mm;
     tmask &= ~mm;
@@ -1134,6 +1308,9 @@ struct Sim {
     const uint64_t t = bal(mine(wmask) && swait == x);
     if (!t) return;
     wmask &= ~t;
+    if constexpr (XPL != 0) {
+      if (mine(t)) swait = 0;
+    }
     tmask = t;
     new_epoch();
     phase = PH_TRY;
@@ -1276,7 +1453,7 @@ struct Sim {
   // Client::cmd_send: next command of client c (0-based) -> SubmitToProc
   __device__ __forceinline__ bool client_send(uint32_t c) {
     const uint32_t issued = rl(ca, 32u + c);
-    if (issued >= cmds) return false;
+    if (issued >= prm(P_CMDS)) return false;
     lset(ca, 32u + c, issued + 1u);
     lset(cb, c, now);  // Pending::start
     schedule_timer(link_s(c), rl(cd, c));
@@ -1305,7 +1482,7 @@ struct Sim {
     }
     uint32_t x = link - g.NP;
     if (x < g.n) {  // E(p): executed notification (a no-op for the GraphExecutor)
-      schedule_timer(link_e(x), en_ms);
+      schedule_timer(link_e(x), prm(P_EN));
       return;
     }
     x -= g.n;
@@ -1329,15 +1506,17 @@ struct Sim {
       lat_sum += lat;
       const uint32_t region = rl(ca, c) >> 8;
       if (lid == 0) {
-        if (A.latency_log && issued - 1u < A.lat_cap)
-          A.latency_log[((size_t)inst * g.C + c) * A.lat_cap + issued - 1u] = lat;
+        KSimArgs* k = kargs();
+        if (k->latency_log && issued - 1u < k->lat_cap)
+          k->latency_log[((size_t)prm(P_INST) * g.C + c) * k->lat_cap + issued - 1u] = lat;
       }
       hist_lat(region, lat);
       if (!client_send(c)) {
-        ++clients_done;
-        if (clients_done == g.C) {
-          if (has_extra) {
-            final_ms = now + extra;
+        const uint32_t cdone = prm(P_CDONE) + 1u;
+        prm_set(P_CDONE, cdone);
+        if (cdone == g.C) {
+          if (prm(P_HAS_EXTRA)) {
+            prm_set(P_FINAL, now + prm(P_EXTRA));
             in_extra = true;
           } else {
             done = true;
@@ -1385,33 +1564,44 @@ struct Sim {
 // lets 16 instances share a CU (the default configs[1] geometry: 10.0 KB at
 // n = 5 — 4 waves issue more of the scalar unit's slots than 3 even with a few
 // spilled registers, +14 %), 3 otherwise, 2 for the 256-slot dot tables
-template <uint32_t HM, uint32_t DS, uint32_t WPS, uint32_t NX>
+template <uint32_t HM, uint32_t DS, uint32_t WPS, uint32_t NX, class GP = GeoRT>
 __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
-  Sim<HM, DS, NX> s;
+  Sim<HM, DS, NX, GP> s;
 #pragma unroll
   for (uint32_t k = 0; k < DS; ++k) s.sdv[k] = 0;
   s.lid = threadIdx.x;
-  s.A = a;
-  s.g = a.g;
+  s.trace = ((uint64_t)vdiv(0) << 32) | vdiv(0);
+  s.deps_total = s.trace;
+  s.lat_sum = s.trace;
+  if constexpr (!GP::fixed) s.g = a.g;
   s.lds = smem;
-  s.inst = inst;
   const fx_sim_spec& sp = a.specs[inst];
-  s.seed = sp.seed;
-  s.rng_inst = sp.instance;
-  s.protocol = sp.protocol;
-  s.n = a.g.n;
-  s.f = sp.f;
-  s.C = a.g.C;
-  s.gc_ms = sp.gc_interval_ms;
-  s.en_ms = sp.executed_notification_ms;
-  s.cmds = sp.commands_per_client;
-  s.conflict_ = sp.conflict_rate;
-  s.pool = sp.pool_size;
-  s.has_extra = sp.extra_sim_time_ms >= 0;
-  s.extra = s.has_extra ? (uint32_t)sp.extra_sim_time_ms : 0u;
+  s.protocol = GP::fixed ? GP::proto : sp.protocol;
+  s.n = s.g.n;
+  s.f = GP::fixed ? GP::fc : sp.f;
+  s.C = s.g.C;
+  const bool has_extra = sp.extra_sim_time_ms >= 0;
+  {
+    const uint32_t l = s.lid;
+    uint32_t v = 0;
+    v = l == Sim<HM, DS, NX, GP>::P_SEED ? (uint32_t)sp.seed : v;
+    v = l == Sim<HM, DS, NX, GP>::P_SEED + 1 ? (uint32_t)(sp.seed >> 32) : v;
+    v = l == Sim<HM, DS, NX, GP>::P_RNG ? (uint32_t)sp.instance : v;
+    v = l == Sim<HM, DS, NX, GP>::P_RNG + 1 ? (uint32_t)(sp.instance >> 32) : v;
+    v = l == Sim<HM, DS, NX, GP>::P_GC ? sp.gc_interval_ms : v;
+    v = l == Sim<HM, DS, NX, GP>::P_EN ? sp.executed_notification_ms : v;
+    v = l == Sim<HM, DS, NX, GP>::P_CMDS ? sp.commands_per_client : v;
+    v = l == Sim<HM, DS, NX, GP>::P_CONFLICT ? sp.conflict_rate : v;
+    v = l == Sim<HM, DS, NX, GP>::P_POOL ? sp.pool_size : v;
+    v = l == Sim<HM, DS, NX, GP>::P_EXTRA ? (has_extra ? (uint32_t)sp.extra_sim_time_ms : 0u) : v;
+    v = l == Sim<HM, DS, NX, GP>::P_HAS_EXTRA ? (has_extra ? 1u : 0u) : v;
+    v = l == Sim<HM, DS, NX, GP>::P_INST ? inst : v;
+    s.pv = v;
+  }
+  const uint32_t gc_ms = sp.gc_interval_ms, en_ms = sp.executed_notification_ms;
   const uint32_t n = s.n;
   if (s.protocol == FX_PROTOCOL_ATLAS) {
     s.fq = n / 2 + s.f;
@@ -1424,14 +1614,15 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
     s.synod_f = fe;  // EPaxos::allowed_faults
   }
   // ---------------------------------------------------------------- init
-  for (uint32_t i = s.lid; i < a.g.words; i += 64) smem[i] = 0;
-  for (uint32_t i = s.lid; i < a.g.R; i += 64) smem[a.g.off_free + i] = a.g.R - 1u - i;  // free stack
-  s.nfree = a.g.R;
+  for (uint32_t i = s.lid; i < s.g.words; i += 64) smem[i] = 0;
+  for (uint32_t i = s.lid; i < s.g.R; i += 64) smem[s.g.off_free + i] = s.g.R - 1u - i;  // free stack
+  s.nfree = s.g.R;
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (uint32_t k = 0; k < HM; ++k) s.ht[k] = s.hs[k] = NONE;
 #pragma unroll
   for (uint32_t k = 0; k < NX; ++k) s.xdot[k] = s.xrec[k] = s.xwait[k] = 0;
+  s.sdot = s.srec = s.swait = 0;
   const uint32_t RP = a.RP;
   // process regions, quorums (BaseProcess::discover over
   // sort_processes_by_distance, base.rs:62-154, util.rs:153-185)
@@ -1480,17 +1671,17 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
   // periodic events (runner.rs:179-187), then clients (run(), C5 ascending)
   // (the periodic GC events are evaluated in gc_finish; their insertion
   // seqs only shift the numbering, C3)
-  const bool sim_en = a.sim_exec_notif || s.has_extra;
+  const bool sim_en = a.sim_exec_notif || has_extra;
   for (uint32_t p = 0; p < n; ++p) {
-    if (sim_en) s.schedule_timer(s.link_e(p), s.en_ms);
+    if (sim_en) s.schedule_timer(s.link_e(p), en_ms);
     else ++s.seq;  // keep the insertion numbering of the reference
   }
   for (uint32_t c = 0; c < s.C; ++c) {
     s.client_send(c);
-    if (s.cmds == 0) s.err = FX_ERR_INVALID_ARG;
+    if (sp.commands_per_client == 0) s.err = FX_ERR_INVALID_ARG;
   }
   // ------------------------------------------------------------ loop
-  const uint64_t max_events = a.max_events ? a.max_events : 0xFFFFFFFFull;
+  const uint32_t max_events = a.max_events ? a.max_events : 0xFFFFFFFFu;
   uint32_t gc_pair = NONE;
   while (!s.done && !s.err) {
     uint32_t t = 0;
@@ -1510,11 +1701,11 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
       s.err = FX_ERR_TIME_RANGE;
       break;
     }
-    if (s.in_extra && t > s.final_ms && s.gc_ms) {
+    if (s.in_extra && t > s.prm(s.P_FINAL) && gc_ms) {
       // the run stops at the first action after final_ms: a GC action
       // before t (C3: at t, t's other actions go first) ends it instead
       uint32_t pair = NONE;
-      const uint32_t tg = s.gc_next_after(s.final_ms, pair);
+      const uint32_t tg = s.gc_next_after(s.prm(s.P_FINAL), pair);
       if (tg < t) {
         s.now = tg;
         gc_pair = pair;
@@ -1526,7 +1717,7 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
 #ifdef FX_SIM_PROFILE
     s.prof[1] += __builtin_amdgcn_s_memtime() - pt1;
 #endif
-    if (s.in_extra && s.now > s.final_ms) s.done = true;
+    if (s.in_extra && s.now > s.prm(s.P_FINAL)) s.done = true;
     if (s.events >= max_events) s.err = FX_ERR_SIM_EVENTS;
   }
   // ----------------------------------------------------------- outputs
@@ -1544,7 +1735,7 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
       st[FX_SIM_STAT_FAST_READS + s.lid] = 0u;  // no read-only commands on this kernel
       st[FX_SIM_STAT_SLOW_READS + s.lid] = 0u;
     }
-    if (s.gc_ms && !s.err) s.gc_finish(s.now, gc_pair, st);
+    if (gc_ms && !s.err) s.gc_finish(s.now, gc_pair, st);
     if (s.lid == 0) {
       st[FX_SIM_STAT_EVENTS] = s.events;
 #ifdef FX_SIM_PROFILE
@@ -1555,23 +1746,19 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
       st[FX_SIM_STAT_SEQ] = s.seq;
       st[FX_SIM_STAT_DEPS] = s.deps_total;
       st[FX_SIM_STAT_LAT_SUM] = s.lat_sum;
-      st[FX_SIM_STAT_ERR_SITE] = s.err_site;
+      st[FX_SIM_STAT_ERR_SITE] = s.prm(s.P_ERRSITE);
     }
   }
-  // the instance's cached histogram bins (exact: a sample either went here or
-  // straight to the global bin)
-  for (uint32_t i = s.lid; i < HC_BINS + HD_BINS; i += 64) {
-    const uint32_t c = smem[a.g.off_hist + i];
-    if (!c) continue;
-    if (i < HC_BINS) {
-      if (a.chain_hist) atomicAdd(&a.chain_hist[i], (unsigned long long)c);
-    } else if (a.delay_hist) {
-      atomicAdd(&a.delay_hist[i - HC_BINS], (unsigned long long)c);
-    }
+  // the instance's histogram counts held in lanes (exact: a sample either
+  // went there or straight to its global bin), clamped into the bins here
+  if (s.hcv && a.chain_hist) atomicAdd(&a.chain_hist[min(s.lid, a.chain_bins - 1u)], (unsigned long long)s.hcv);
+  for (uint32_t i = s.lid; i < HD_BINS; i += 64) {
+    const uint32_t c = smem[s.g.off_hist + i];
+    if (c && a.delay_hist) atomicAdd(&a.delay_hist[min(i, a.delay_bins - 1u)], (unsigned long long)c);
   }
-  for (uint32_t i = s.lid; i < HL_SLOTS; i += 64) {
-    const uint32_t k = smem[a.g.off_lat + i];
-    if (k && a.lat_hist) atomicAdd(&a.lat_hist[k - 1u], (unsigned long long)smem[a.g.off_lat + HL_SLOTS + i]);
+  if (s.hlk && a.lat_hist) {
+    const uint32_t key = s.hlk - 1u, lat = key & 0xFFFFFFu;
+    atomicAdd(&a.lat_hist[(key >> 24) * a.lat_bins + min(lat, a.lat_bins - 1u)], (unsigned long long)s.hlc);
   }
   if (s.lid == 0) a.err[inst] = s.err;
 }
@@ -1585,62 +1772,24 @@ size_t simx_arena_bytes(const fx_sim_spec& sp, uint32_t ring, uint32_t dots);
 bool simx_table_sizes(const fx_sim_spec& sp, uint32_t ring, uint32_t dots, uint32_t* R, uint32_t* NS);
 int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs);
 
+// the fixed-geometry builds: BASELINE configs[1] (EPaxos n = 5 f = 2, one
+// client in each of the 5 process regions) and configs[0] (Atlas n = 3 f = 1)
+using GeoC1 = GeoCT<FX_PROTOCOL_EPAXOS, 5, 2, 5>;
+#ifdef FX_XSWAP
+constexpr uint32_t XNX = 5;
+#else
+constexpr uint32_t XNX = 1;
+#endif
+using GeoC0 = GeoCT<FX_PROTOCOL_ATLAS, 3, 1, 3>;
+template <class GP>
+static bool geo_is(const Geo& g, const fx_sim_spec& s0) {
+  const Geo c = GP::g;
+  return s0.protocol == GP::proto && s0.f == GP::fc && std::memcmp(&g, &c, sizeof(Geo)) == 0;
+}
+
 static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, Geo& g) {
-  const uint32_t n = sp.n;
-  if (n < 2 || n > NMAX) return false;
-  const uint32_t C = sp.clients_per_region * sp.num_client_regions;
-  if (C < 1 || C > CMAX) return false;
-  g.n = n;
-  g.C = C;
-  g.K = sp.keys_per_command;
-  // table sizes: small by default (LDS decides how many instances share a CU);
-  // fx_sim_run_tiered reruns the instances that outgrow them with 256 dots
-  const uint32_t cpr = (C + n - 1) / n;  // clients per process region
-  // live dots per instance: 8 per client, at most 64; 32 for n > 5 with one
-  // client per region (configs[2]'s n = 7: 12.4 KB instead of 15.4 KB, 13
-  // instances per CU instead of 10, the same reruns; 24 reran more, 16 lost 4x)
-  g.W = wslots ? wslots : (n > 5 && C <= 8 ? 32u : std::min<uint32_t>(64u, 8u * C));
-  if (g.W > 256u) return false;
-  // messages in flight per instance: 16 per process and client; at least 192
-  // for n > 5, where a lagging far replica overflowed the smaller pool often
-  // enough (reruns at 4x) that the larger table wins despite fewer instances
-  // per CU (configs[2] sweep)
-  g.R = ring ? ring : std::min<uint32_t>(4096u, std::max<uint32_t>(16u * n * cpr, n > 5 ? 192u : 0u));
-  if (g.R > 65534u) return false;
-  g.NP = n * (n - 1);
-  g.L = g.NP + n + 2 * C;
-  if (g.L > 64 * HMAX) return false;
-  g.ncli_keys = sp.pool_size + C + 1;
-  // an MCollectAck carries the coordinator's deps plus the replica's latest
-  // write per key (<= 2K); a committed value is their union over the fast
-  // quorum (<= K (n + 1): the coordinator's past plus one latest per member)
-  g.amax = 2 * g.K;
-  g.vmax = std::min<uint32_t>(VMAX, g.K * (n + 1));
-  g.sl_value = SL_COLLECT + g.K;
-  g.sl_ack = g.sl_value + g.vmax;
-  g.slotw = g.sl_ack + n * g.amax;
-  if (n * g.amax > 64 || g.slotw > 64) return false;
-  uint32_t o = 0;
-  // messages in flight: one pool per instance, a FIFO list per process link
-  g.off_pool = o; o += g.R * 4;
-  g.off_free = o; o += g.R;
-  // GC logs: 4 / 2 entries per client per region (commits of one source
-  // arrive about once per client round trip), 32 / 16 in the rerun geometry
-  g.rt = 4;
-  while (g.rt < 4 * cpr && g.rt < 64) g.rt <<= 1;
-  if (g.W > 64u) g.rt = std::max<uint32_t>(g.rt, 32u);
-  g.rc = g.rt / 2;
-  g.off_gct = o; o += n * n * g.rt * 2;
-  g.off_gcc = o; o += n * n * g.rc * 2;
-  g.off_gcr = o; o += n * n * 4;
-  g.off_slot = o; o += g.W * g.slotw;
-  g.off_kd = o; o += n * g.ncli_keys;
-  g.off_frame = o; o += FMAX * RDMAX;
-  g.off_wl = o; o += 72;
-  g.off_hist = o; o += HC_BINS + HD_BINS;
-  g.off_lat = o; o += 2 * HL_SLOTS;
-  g.words = (o + 3) & ~3u;
-  return true;
+  return geo_make(sp.n, sp.clients_per_region * sp.num_client_regions, sp.keys_per_command, sp.pool_size, ring,
+                  wslots, g);
 }
 
 }  // namespace fx
@@ -1676,9 +1825,12 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   const fx_sim_spec& s0 = b->host_specs[0];
   // the all-on-chip kernel unless the batch needs the large-instance one
   bool large = (b->flags & FX_SIM_FLAG_LARGE) != 0 || W > 256;
+  // one protocol and f over the batch: a fixed-geometry build may take it
+  bool one_pf = true;
   // every instance of a launch shares the geometry (protocol, n, clients, keys)
   for (uint32_t i = 0; i < b->instances; ++i) {
     const fx_sim_spec& s = b->host_specs[i];
+    if (s.protocol != s0.protocol || s.f != s0.f) one_pf = false;
     if (s.protocol != FX_PROTOCOL_ATLAS && s.protocol != FX_PROTOCOL_EPAXOS) return FX_ERR_UNSUPPORTED;
     if (s.n != s0.n || s.clients_per_region != s0.clients_per_region ||
         s.num_client_regions != s0.num_client_regions || s.keys_per_command != s0.keys_per_command ||
@@ -1733,6 +1885,10 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
     (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 1, 3, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 4, 2, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 4, 2, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, XNX, GeoC1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, 1, GeoC0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     configured = true;
   }
   // link heads per lane: one when every link fits a lane
@@ -1740,7 +1896,13 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   const dim3 grid(b->instances), block(64);
   hipStream_t hs = (hipStream_t)hip_stream;
   const bool four = lds <= 160u * 1024u / 16u;  // 16 instances per CU: 4 waves per SIMD
-  if (a.g.W <= 64) {
+  // the BASELINE geometries compiled in (same results as the run-time build)
+  const bool fixed_ok = one_pf && !(b->flags & FX_SIM_FLAG_GENERIC) && a.g.L <= 64 && four;
+  if (fixed_ok && geo_is<GeoC1>(a.g, s0)) {
+    hipLaunchKernelGGL((sim::k_sim<1, 1, 4, XNX, GeoC1>), grid, block, lds, hs, a);
+  } else if (fixed_ok && geo_is<GeoC0>(a.g, s0)) {
+    hipLaunchKernelGGL((sim::k_sim<1, 1, 4, 1, GeoC0>), grid, block, lds, hs, a);
+  } else if (a.g.W <= 64) {
     // n <= 5 (configs[0], configs[1], half of configs[2]): executor tables
     // for 5 processes, 9 VGPRs fewer under the 4-wave budget
     if (a.g.L <= 64 && four && a.g.n <= 5) hipLaunchKernelGGL((sim::k_sim<1, 1, 4, 5>), grid, block, lds, hs, a);
@@ -1751,7 +1913,12 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
     if (a.g.L <= 64) hipLaunchKernelGGL((sim::k_sim<1, 4, 2, NMAX>), grid, block, lds, hs, a);
     else hipLaunchKernelGGL((sim::k_sim<2, 4, 2, NMAX>), grid, block, lds, hs, a);
   }
-  return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "fx_sim_run: launch failed: %s\n", hipGetErrorString(e));
+    return FX_ERR_HIP;
+  }
+  return FX_OK;
 }
 
 // ------------------------------------------------------ escalation driver

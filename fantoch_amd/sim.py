@@ -216,9 +216,11 @@ class Result:
 
 def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bins=256,
         delay_bins=8192, ring_entries=0, dot_slots=0, max_events=0, flags=0, stream=None,
-        large=False):
+        large=False, generic=False):
     """Simulates every instance of `specs` on the GPU; returns a Result.
-    large=True forces the large-instance kernel (FX_SIM_FLAG_LARGE)."""
+    large=True forces the large-instance kernel (FX_SIM_FLAG_LARGE);
+    generic=True the run-time-geometry build of the all-on-chip kernel even
+    for a compiled-in geometry (FX_SIM_FLAG_GENERIC)."""
     lib = _lib.load()
     planet = planet or Planet()
     N = len(specs)
@@ -233,6 +235,8 @@ def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bi
         max_events = min(0xFFFFFFFF, 4000 * C * cmds + 10_000_000)
     if large:
         flags |= _lib.FX_SIM_FLAG_LARGE
+    if generic:
+        flags |= _lib.FX_SIM_FLAG_GENERIC
     host = (_lib.SimSpec * N)(*specs)
     dspec = DeviceBuffer(ctypes.sizeof(host))
     check(lib.fx_dev_h2d(dspec.ptr, ctypes.addressof(host), ctypes.sizeof(host), stream), "h2d")

@@ -501,6 +501,9 @@ typedef struct fx_sim_spec {
                                              (GraphExecutor::executed is None; they matter
                                              only for where a run with extra time stops) */
 #define FX_SIM_FLAG_LARGE 2u              /* run the large-instance kernel */
+#define FX_SIM_FLAG_GENERIC 4u            /* the all-on-chip kernel built for run-time geometry even
+                                             when the batch has one of the geometries compiled in
+                                             (BASELINE configs[0]-[2]; same results, for A/B tests) */
 typedef struct fx_sim_batch {
   const fx_sim_spec* specs;        /* [instances] device copy                          */
   const fx_sim_spec* host_specs;   /* [instances] host copy (validation, geometry)     */
