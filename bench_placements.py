@@ -134,7 +134,9 @@ def main_placements(args):
         executed_len = torch.zeros(N * n, dtype=torch.int32, device=dev)
         stats = torch.zeros(N * _lib.FX_SIM_STATS, dtype=torch.int64, device=dev)
         err = torch.zeros(N, dtype=torch.int32, device=dev)
-        batch = _lib.SimBatch(spec_dev.data_ptr(), ctypes.addressof(host), N, 0, ping.data_ptr(), rank_m.data_ptr(),
+        sim_flags = _lib.FX_SIM_FLAG_GENERIC if getattr(args, "generic", False) else 0
+        batch = _lib.SimBatch(spec_dev.data_ptr(), ctypes.addressof(host), N, sim_flags, ping.data_ptr(),
+                              rank_m.data_ptr(),
                               planet.R, S.Planet.STRIDE, 0, 0, 0, args.ring_entries, args.dot_slots, 0)
         out = _lib.SimOutput(None, executed_len.data_ptr(), None, lat_hist.data_ptr(), chain.data_ptr(),
                              delay.data_ptr(), stats.data_ptr(), err.data_ptr(), LAT_BINS, CHAIN_BINS, DELAY_BINS, 0)

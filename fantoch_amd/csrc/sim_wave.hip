@@ -186,9 +186,10 @@ __host__ __device__ constexpr Geo geo_fixed(uint32_t n, uint32_t C) {
 // waited-on dot is).  A process that needs more pending slots fails with
 // FX_ERR_SIM_CAPACITY and fx_sim_run_tiered reruns the instance on the
 // run-time build's larger tables.
+constexpr uint32_t FANY = 0xFFu;  // f: per instance
 struct GeoRT {
   static constexpr bool fixed = false;
-  static constexpr uint32_t proto = 0xFFu, fc = 0xFFu, xp_lanes = 0;
+  static constexpr uint32_t proto = 0xFFu, fc = FANY, xp_lanes = 0;
   Geo g;
 };
 template <uint32_t PR, uint32_t N, uint32_t F, uint32_t CC>
@@ -1581,7 +1582,7 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
   const fx_sim_spec& sp = a.specs[inst];
   s.protocol = GP::fixed ? GP::proto : sp.protocol;
   s.n = s.g.n;
-  s.f = GP::fixed ? GP::fc : sp.f;
+  s.f = GP::fc != FANY ? GP::fc : sp.f;
   s.C = s.g.C;
   const bool has_extra = sp.extra_sim_time_ms >= 0;
   {
@@ -1781,10 +1782,14 @@ constexpr uint32_t XNX = 5;
 constexpr uint32_t XNX = 1;
 #endif
 using GeoC0 = GeoCT<FX_PROTOCOL_ATLAS, 3, 1, 3>;
+// configs[2]: Atlas over region subsets, one client per region, f = 1 and 2
+// in one batch (f per instance)
+using GeoC2a = GeoCT<FX_PROTOCOL_ATLAS, 5, FANY, 5>;
+using GeoC2b = GeoCT<FX_PROTOCOL_ATLAS, 7, FANY, 7>;
 template <class GP>
 static bool geo_is(const Geo& g, const fx_sim_spec& s0) {
   const Geo c = GP::g;
-  return s0.protocol == GP::proto && s0.f == GP::fc && std::memcmp(&g, &c, sizeof(Geo)) == 0;
+  return s0.protocol == GP::proto && (GP::fc == FANY || s0.f == GP::fc) && std::memcmp(&g, &c, sizeof(Geo)) == 0;
 }
 
 static bool sim_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t wslots, Geo& g) {
@@ -1826,11 +1831,12 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   // the all-on-chip kernel unless the batch needs the large-instance one
   bool large = (b->flags & FX_SIM_FLAG_LARGE) != 0 || W > 256;
   // one protocol and f over the batch: a fixed-geometry build may take it
-  bool one_pf = true;
+  bool one_p = true, one_f = true;
   // every instance of a launch shares the geometry (protocol, n, clients, keys)
   for (uint32_t i = 0; i < b->instances; ++i) {
     const fx_sim_spec& s = b->host_specs[i];
-    if (s.protocol != s0.protocol || s.f != s0.f) one_pf = false;
+    if (s.protocol != s0.protocol) one_p = false;
+    if (s.f != s0.f) one_f = false;
     if (s.protocol != FX_PROTOCOL_ATLAS && s.protocol != FX_PROTOCOL_EPAXOS) return FX_ERR_UNSUPPORTED;
     if (s.n != s0.n || s.clients_per_region != s0.clients_per_region ||
         s.num_client_regions != s0.num_client_regions || s.keys_per_command != s0.keys_per_command ||
@@ -1887,6 +1893,10 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
     (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 4, 2, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, XNX, GeoC1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, 1, GeoC2a>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 3, 1, GeoC2b>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, 1, GeoC0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     configured = true;
@@ -1897,11 +1907,15 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   hipStream_t hs = (hipStream_t)hip_stream;
   const bool four = lds <= 160u * 1024u / 16u;  // 16 instances per CU: 4 waves per SIMD
   // the BASELINE geometries compiled in (same results as the run-time build)
-  const bool fixed_ok = one_pf && !(b->flags & FX_SIM_FLAG_GENERIC) && a.g.L <= 64 && four;
-  if (fixed_ok && geo_is<GeoC1>(a.g, s0)) {
+  const bool fixed_ok = one_p && !(b->flags & FX_SIM_FLAG_GENERIC) && a.g.L <= 64;
+  if (fixed_ok && one_f && four && geo_is<GeoC1>(a.g, s0)) {
     hipLaunchKernelGGL((sim::k_sim<1, 1, 4, XNX, GeoC1>), grid, block, lds, hs, a);
-  } else if (fixed_ok && geo_is<GeoC0>(a.g, s0)) {
+  } else if (fixed_ok && one_f && four && geo_is<GeoC0>(a.g, s0)) {
     hipLaunchKernelGGL((sim::k_sim<1, 1, 4, 1, GeoC0>), grid, block, lds, hs, a);
+  } else if (fixed_ok && four && geo_is<GeoC2a>(a.g, s0)) {
+    hipLaunchKernelGGL((sim::k_sim<1, 1, 4, 1, GeoC2a>), grid, block, lds, hs, a);
+  } else if (fixed_ok && !four && geo_is<GeoC2b>(a.g, s0)) {
+    hipLaunchKernelGGL((sim::k_sim<1, 1, 3, 1, GeoC2b>), grid, block, lds, hs, a);
   } else if (a.g.W <= 64) {
     // n <= 5 (configs[0], configs[1], half of configs[2]): executor tables
     // for 5 processes, 9 VGPRs fewer under the 4-wave budget

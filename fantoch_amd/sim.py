@@ -216,11 +216,12 @@ class Result:
 
 def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bins=256,
         delay_bins=8192, ring_entries=0, dot_slots=0, max_events=0, flags=0, stream=None,
-        large=False, generic=False):
+        large=False, generic=False, tiered=True):
     """Simulates every instance of `specs` on the GPU; returns a Result.
     large=True forces the large-instance kernel (FX_SIM_FLAG_LARGE);
     generic=True the run-time-geometry build of the all-on-chip kernel even
-    for a compiled-in geometry (FX_SIM_FLAG_GENERIC)."""
+    for a compiled-in geometry (FX_SIM_FLAG_GENERIC); tiered=False: one
+    fx_sim_run, instances that outgrow the tables keep FX_ERR_SIM_CAPACITY."""
     lib = _lib.load()
     planet = planet or Planet()
     N = len(specs)
@@ -257,8 +258,11 @@ def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bi
                        out["chain"].ptr, out["delay"].ptr, out["stats"].ptr, out["err"].ptr,
                        lat_bins, chain_bins, delay_bins, 0, out["dot_client"].ptr)
     reruns = ctypes.c_uint32()
-    check(lib.fx_sim_run_tiered(ctypes.byref(b), ctypes.byref(o), stream, ctypes.byref(reruns)),
-          "fx_sim_run_tiered")
+    if tiered:
+        check(lib.fx_sim_run_tiered(ctypes.byref(b), ctypes.byref(o), stream, ctypes.byref(reruns)),
+              "fx_sim_run_tiered")
+    else:
+        check(lib.fx_sim_run(ctypes.byref(b), ctypes.byref(o), stream), "fx_sim_run")
     check(lib.fx_dev_synchronize(stream), "fx_sim_run sync")
     d = lambda k, dt, cnt: out[k].download(dt, cnt, stream)
     res = Result(specs, d("executed", np.uint32, N * s0.n * exec_cap),
