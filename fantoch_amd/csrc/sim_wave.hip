@@ -872,6 +872,7 @@ struct Sim : GP {
 
   // MCommitDot: add_to_clock (gc/clock.rs:43-48)
   __device__ __forceinline__ void h_mcommitdot(uint32_t p, uint32_t dot) {
+    const uint32_t gc_ms = prm(P_GC);
 #ifdef FX_ABL_GC
     return;
 #endif
@@ -889,7 +890,6 @@ struct Sim : GP {
         const uint32_t ones = __builtin_ctz(~win);
         gf = gf + 1 + ones;
         gw = win >> ones;
-        const uint32_t gc_ms = prm(P_GC);
         if (gc_ms) {
           const uint32_t kt = now ? (now - 1u) / gc_ms : 0u;  // ticks strictly before now
           if (gnt == 0 || kt != glk) {
@@ -1116,9 +1116,13 @@ struct Sim : GP {
   // AggregatePending (runner.rs:406-424), executor metrics, execution log
   __device__ __forceinline__ void on_execute(uint32_t d, uint32_t start) {
     const uint32_t p = xp;
+    // lane reads (prm, rl) only outside lane-divergent code: a VGPR the
+    // compiler reloads or copies under a partial exec mask holds garbage in the
+    // inactive lanes
+    const uint32_t inst = prm(P_INST);
     if (lid == 0) {
       KSimArgs* k = kargs();
-      if (xk < k->exec_cap && k->executed) k->executed[((size_t)prm(P_INST) * n + p) * k->exec_cap + xk] = d;
+      if (xk < k->exec_cap && k->executed) k->executed[((size_t)inst * n + p) * k->exec_cap + xk] = d;
     }
     ++xk;
     const uint32_t delay = now - start;  // ExecutionDelay (graph/mod.rs:514-518)
@@ -1506,10 +1510,11 @@ struct Sim : GP {
       const uint32_t lat = now - rl(cb, c);  // latency.as_millis()
       lat_sum += lat;
       const uint32_t region = rl(ca, c) >> 8;
+      const uint32_t inst = prm(P_INST);
       if (lid == 0) {
         KSimArgs* k = kargs();
         if (k->latency_log && issued - 1u < k->lat_cap)
-          k->latency_log[((size_t)prm(P_INST) * g.C + c) * k->lat_cap + issued - 1u] = lat;
+          k->latency_log[((size_t)inst * g.C + c) * k->lat_cap + issued - 1u] = lat;
       }
       hist_lat(region, lat);
       if (!client_send(c)) {
@@ -1737,6 +1742,7 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
       st[FX_SIM_STAT_SLOW_READS + s.lid] = 0u;
     }
     if (gc_ms && !s.err) s.gc_finish(s.now, gc_pair, st);
+    const uint32_t err_site = s.prm(s.P_ERRSITE);
     if (s.lid == 0) {
       st[FX_SIM_STAT_EVENTS] = s.events;
 #ifdef FX_SIM_PROFILE
@@ -1747,7 +1753,7 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
       st[FX_SIM_STAT_SEQ] = s.seq;
       st[FX_SIM_STAT_DEPS] = s.deps_total;
       st[FX_SIM_STAT_LAT_SUM] = s.lat_sum;
-      st[FX_SIM_STAT_ERR_SITE] = s.prm(s.P_ERRSITE);
+      st[FX_SIM_STAT_ERR_SITE] = err_site;
     }
   }
   // the instance's histogram counts held in lanes (exact: a sample either
