@@ -62,9 +62,9 @@ constexpr uint32_t VMAX = 16;            // deps of a committed value (per-launc
 // tick log needs one entry per GC interval in which the frontier moved over the
 // last max-distance + interval, the change log the moves of the last interval
 constexpr uint32_t FMAX = 12;            // frame stack depth
-constexpr uint32_t RDMAX = 16;           // ready results per frame
+constexpr uint32_t RDMAX = 16;           // ready results per frame (at most one per client: min(16, C))
 constexpr uint32_t HC_BINS = 64;         // ChainSize values counted per instance in lanes
-constexpr uint32_t HD_BINS = 256;        // ExecutionDelay values counted per instance in LDS
+constexpr uint32_t HD_BINS = 224;        // ExecutionDelay values counted per instance in LDS (p95 of configs[1]: 198 ms)
 constexpr uint32_t HMAX = 2;             // link heads per lane (links <= 128; a template parameter)
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint32_t LNIL = 0xFFFFu;  // end of a link's message list
@@ -90,16 +90,16 @@ enum : uint32_t { PH_IDLE = 0, PH_DFS = 1, PH_TRY = 2, PH_CHECK = 3 };
 
 // dot-table slot (u32 words): fixed header, then (per-launch sizes, Geo)
 // collect deps [K] | value [vmax] | ack deps [n][amax]
-constexpr uint32_t SL_CLIENT = 1,  // word 0 spare (the slot's dot lives in lane `slot`, sdv)
-    SL_IDX = 2, SL_KEYS = 3, SL_PST = 4,  // 4,5: per-process state bytes
-    SL_MASKS = 6, SL_CNT = 7, SL_COLLECT = 8;
+constexpr uint32_t SL_CLIENT = 0,  // (the slot's dot lives in lane `slot`, sdv)
+    SL_IDX = 1, SL_KEYS = 2, SL_PST = 3,  // 3,4: per-process state bytes
+    SL_MASKS = 5, SL_CNT = 6, SL_COLLECT = 7;
 // per-process state byte: status(2) | buffered commit(1) | accepted(1) | buffered-from(4)
 // SL_MASKS: participants(8) | proposer accepts(8) | committed count(8) | executed count(8)
 // SL_CNT:   value count(8) | collect count(8) | proposer ballot set(1) << 16 | nkeys << 20
 
 
 struct Geo {  // launch-uniform geometry
-  uint32_t n, C, K, W, R, L, NP, ncli_keys, rt, rc;
+  uint32_t n, C, K, W, R, L, NP, ncli_keys, rt, rc, rdm;
   uint32_t amax, vmax, sl_value, sl_ack, slotw;  // dot-slot layout (MCollectAck deps <= 2K, value <= K(n+1))
   uint32_t off_pool, off_free, off_gct, off_gcc, off_gcr, off_slot, off_kd, off_frame, off_wl, off_hist, words;
 };
@@ -156,11 +156,17 @@ __host__ __device__ constexpr bool geo_make(uint32_t n, uint32_t C, uint32_t K, 
   g.rc = g.rt / 2;
   g.off_gct = o; o += n * n * g.rt * 2;
   g.off_gcc = o; o += n * n * g.rc * 2;
-  g.off_gcr = o; o += n * n * 4;
+  // the final GC summaries (gc_finish, after the run) reuse the message pool
+  if (g.R >= n * n) {
+    g.off_gcr = g.off_pool;
+  } else {
+    g.off_gcr = o; o += n * n * 4;
+  }
   g.off_slot = o; o += g.W * g.slotw;
   g.off_kd = o; o += n * g.ncli_keys;
-  g.off_frame = o; o += FMAX * RDMAX;
-  g.off_wl = o; o += 72;
+  g.rdm = cmin(RDMAX, C);  // a client's command completes once per frame at most
+  g.off_frame = o; o += FMAX * g.rdm;
+  g.off_wl = o; o += 68;  // released dots: nwl + cnt <= 65
   g.off_hist = o; o += HD_BINS;
   g.words = (o + 3) & ~3u;
   return true;
@@ -428,7 +434,7 @@ struct Sim : GP {
   // take consecutive seqs in ascending target order) and the next tick index
   // link (p, q) delivers
   __device__ __forceinline__ uint32_t& kd(uint32_t p, uint32_t key) { return lds[g.off_kd + p * g.ncli_keys + key]; }
-  __device__ __forceinline__ uint32_t& FRR(uint32_t fi, uint32_t r) { return lds[g.off_frame + fi * RDMAX + r]; }
+  __device__ __forceinline__ uint32_t& FRR(uint32_t fi, uint32_t r) { return lds[g.off_frame + fi * g.rdm + r]; }
   __device__ __forceinline__ uint32_t& wl(uint32_t i) { return lds[g.off_wl + i]; }
   // Histogram samples are counted per instance in LDS (ChainSize bins
   // [0, HC_BINS), ExecutionDelay bins [0, HD_BINS)) and added to the global
@@ -1139,7 +1145,7 @@ struct Sim : GP {
         const uint32_t fi = nfrm - 1;
         const uint32_t w = rl(frw, fi);
         const uint32_t nr = (w >> 20) & 31u;
-        if (nr >= RDMAX) { fail_cap(__LINE__); return; }
+        if (nr >= g.rdm) { fail_cap(__LINE__); return; }
         put(FRR(fi, nr), c);
         lset(frw, fi, w + (1u << 20));
       }
@@ -1899,6 +1905,10 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
     (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 4, 2, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, XNX, GeoC1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 5, XNX, GeoC1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 5, 1, GeoC2a>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, 1, GeoC2a>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 3, 1, GeoC2b>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1914,7 +1924,18 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   const bool four = lds <= 160u * 1024u / 16u;  // 16 instances per CU: 4 waves per SIMD
   // the BASELINE geometries compiled in (same results as the run-time build)
   const bool fixed_ok = one_p && !(b->flags & FX_SIM_FLAG_GENERIC) && a.g.L <= 64;
-  if (fixed_ok && one_f && four && geo_is<GeoC1>(a.g, s0)) {
+  // 20 instances per CU: 5 waves per SIMD (the compiled-in configs[1] / [2]
+  // n = 5 geometry is 8,192 B)
+#ifdef FX_SIM_NO_WPS5
+  const bool five = false;
+#else
+  const bool five = lds <= 160u * 1024u / 20u;
+#endif
+  if (fixed_ok && one_f && five && geo_is<GeoC1>(a.g, s0)) {
+    hipLaunchKernelGGL((sim::k_sim<1, 1, 5, XNX, GeoC1>), grid, block, lds, hs, a);
+  } else if (fixed_ok && five && geo_is<GeoC2a>(a.g, s0)) {
+    hipLaunchKernelGGL((sim::k_sim<1, 1, 5, 1, GeoC2a>), grid, block, lds, hs, a);
+  } else if (fixed_ok && one_f && four && geo_is<GeoC1>(a.g, s0)) {
     hipLaunchKernelGGL((sim::k_sim<1, 1, 4, XNX, GeoC1>), grid, block, lds, hs, a);
   } else if (fixed_ok && one_f && four && geo_is<GeoC0>(a.g, s0)) {
     hipLaunchKernelGGL((sim::k_sim<1, 1, 4, 1, GeoC0>), grid, block, lds, hs, a);
