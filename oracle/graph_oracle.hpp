@@ -16,6 +16,11 @@
 #include <vector>
 
 
+// census hooks for tools/dense_census.cpp (no-ops in every other build)
+#ifndef ORACLE_CENSUS
+#define ORACLE_CENSUS(x)
+#endif
+
 namespace oracle {
 
 // fantoch/src/id.rs:21-27 — Id<ProcessId>{source, sequence}, derived Ord.
@@ -193,6 +198,7 @@ struct DependencyGraph {
     } else {
       fr = strong_connect(first_find, dot, v, scc_count, missing_deps_count, result_missing);
     }
+    ORACLE_CENSUS(search(first_find, (int)fr, scc_count, stack.size(), dot, result_missing.first));
     total_scc_count += scc_count;
     // save new SCCs (mod.rs:438-444)
     std::vector<std::set<Dot>> found;
@@ -238,6 +244,7 @@ struct DependencyGraph {
   // missing dep and keeps going (tarjan.rs:148-166).
   FinderResult strong_connect(bool first_find, const Dot& dot, Vertex* vertex, size_t& scc_count,
                               size_t& missing_deps_count, std::pair<Dot, uint32_t>& missing_out) {
+    ORACLE_CENSUS(recursion(first_find));
     finder_id += 1;
     vertex->id = finder_id;
     vertex->low = finder_id;
@@ -246,6 +253,7 @@ struct DependencyGraph {
 
     for (size_t i = 0; i < vertex->deps.size(); ++i) {
       Dot dep_dot = vertex->deps[i];
+      ORACLE_CENSUS(edge(first_find));
       // ignore self or already executed (tarjan.rs:128-145)
       if (dep_dot == dot || executed_clock.contains(dep_dot.source, dep_dot.sequence)) continue;
       Vertex* dep_vertex = find(dep_dot);
@@ -357,7 +365,7 @@ struct DependencyGraph {
                    uint64_t time_ms) {
     std::set<Dot> visited;
     for (const Dot& d : pending) {
-      if (visited.count(d)) continue;
+      if (visited.count(d)) { ORACLE_CENSUS(skip()); continue; }
       std::vector<Dot> new_dots;
       std::set<Dot> new_visited;
       std::set<std::pair<Dot, uint32_t>> missing;
