@@ -35,36 +35,51 @@ enum : uint32_t { FOUND = 0, MISSING = 1, NOT_PENDING = 2 };
 
 constexpr uint32_t PW = 64;  // partial replication: parents a vertex may wait on at once
 
+// The LDS tables are packed (PK) so that five streams share a CU: u16 vertex
+// lists (free list, Tarjan stack, waiter lists, index slots), one word per DFS
+// frame, a vertex's dep count beside its arrival index, and its Tarjan id,
+// on-stack bit and visited epoch in one word.  The HBM tables keep one u32
+// per field (16,384 vertices do not fit the packed fields).
+constexpr uint32_t PK_REC_BITS = 26;                       // arrival index | ndeps << 26
+constexpr uint32_t PK_ID_MASK = 0x3FFu, PK_ONSTACK = 0x400u;  // vmark: id | on-stack | epoch << 11
+constexpr uint32_t PK_EPOCH_SHIFT = 11, PK_EPOCH_MAX = (1u << 21) - 4096u;
+
 struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-bit clock windows
-  uint32_t P, Q, WB, n, D;
-  uint32_t vdot, vrec, vnd, vdeps, vwait, vid, vlow, vmark, vfree, tstk, fv, fi, wl, tl, tmp, hidx, front, bits, sc, words;
+  uint32_t P, Q, WB, n, D, wlcap;
+  bool pk;
+  uint32_t vdot, vrec, vnd, vdeps, vwait, vid, vlow, vmark, vce, vfree, tstk, fv, fi, wl, tl, tmp, hidx, front, bits, sc, words;
   // partial replication only (0 words otherwise): per-vertex parent lists
   // (count + PW dots), per-frame missing-dep counts, the collected missing deps
   uint32_t vwn, vwl, fm, ml;
   __host__ __device__ void make(uint32_t P_, uint32_t Q_, uint32_t WB_, uint32_t n_, uint32_t D_,
-                                bool partial = false) {
+                                bool partial = false, bool packed = false) {
     P = P_;
     Q = Q_;
     WB = WB_;
     n = n_;
     D = D_;
+    pk = packed;
     uint32_t o = 0;
+    const uint32_t h = packed ? P / 2 : P;  // a u16 list of P entries
     vdot = o; o += P;
     vrec = o; o += P;
-    vnd = o; o += P;      // deps of the vertex (copied from the planes at index time:
-    vdeps = o; o += P * D;  // the DFS then never waits on HBM)
+    vnd = o; o += packed ? 0 : P;
+    vdeps = o; o += P * D;  // deps of the vertex (copied from the planes at index time:
+                            // the DFS then never waits on HBM)
     vwait = o; o += P;
-    vid = o; o += P;
-    vlow = o; o += P;
+    vid = o; o += packed ? 0 : P;
+    vlow = o; o += packed ? 0 : P;  // per DFS frame: low of the frame's vertex
     vmark = o; o += P;
-    vfree = o; o += P;
-    tstk = o; o += P;
-    fv = o; o += P;
-    fi = o; o += P;
-    wl = o; o += 2 * P;
-    tl = o; o += P;
-    tmp = o; o += P;
-    hidx = o; o += n * Q;
+    vce = o; o += P;  // search-result cache: executions when the vertex's last search failed
+    vfree = o; o += h;
+    tstk = o; o += h;
+    fv = o; o += P;                 // packed: vertex | next dep << 10 | low << 15
+    fi = o; o += packed ? 0 : P;
+    wlcap = packed ? P : 2 * P;     // released dots of one handle_add: at most the vertices present
+    wl = o; o += wlcap;
+    tl = o; o += h;
+    tmp = o; o += h;
+    hidx = o; o += packed ? n * Q / 2 : n * Q;
     front = o; o += 8;
     bits = o; o += n * WB;
     sc = o; o += 4;  // saved scalars of a resumable (HBM) stream: nfree, nexec, epoch
@@ -76,6 +91,7 @@ struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-
   }
 };
 
+template <bool PK>
 struct W {
   KArgs a;
   Lay L;
@@ -88,11 +104,88 @@ struct W {
   uint32_t nml = 0;      // missing deps collected by a first search (partial)
 
   __device__ __forceinline__ uint32_t& at(uint32_t base, uint32_t i) { return m[base + i]; }
+  // a uniform store: every lane writes the same word (LDS: no exec-mask
+  // save / restore around it; HBM: lane 0)
   __device__ __forceinline__ void put(uint32_t base, uint32_t i, uint32_t v) {
-    if (lid == 0) m[base + i] = v;
+    if (PK || lid == 0) m[base + i] = v;
   }
   __device__ __forceinline__ uint32_t rd(uint32_t base, uint32_t i) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)m[base + i]);
+  }
+  // vertex lists: u16 entries when packed
+  __device__ __forceinline__ uint32_t lget(uint32_t base, uint32_t i) {
+    if constexpr (PK) return ((const uint16_t*)(m + base))[i];
+    else return m[base + i];
+  }
+  __device__ __forceinline__ void lset(uint32_t base, uint32_t i, uint32_t v) {
+    if constexpr (PK) ((uint16_t*)(m + base))[i] = (uint16_t)v;
+    else m[base + i] = v;
+  }
+  __device__ __forceinline__ uint32_t lrd(uint32_t base, uint32_t i) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)lget(base, i));
+  }
+  __device__ __forceinline__ void lput(uint32_t base, uint32_t i, uint32_t v) {
+    if (PK || lid == 0) lset(base, i, v);
+  }
+  // vertex fields
+  __device__ __forceinline__ uint32_t rec_of(uint32_t w) { return PK ? w & ((1u << PK_REC_BITS) - 1u) : w; }
+  __device__ __forceinline__ uint32_t nd_of(uint32_t v) {
+    if constexpr (PK) return rd(L.vrec, v) >> PK_REC_BITS;
+    else return rd(L.vnd, v);
+  }
+  // the Tarjan word of v: id (0 = unvisited) and on-stack bit, plus the
+  // visited epoch (packed: one word; HBM: id and mark words)
+  __device__ __forceinline__ uint32_t epoch_of(uint32_t mk) { return PK ? mk >> PK_EPOCH_SHIFT : mk >> 1; }
+  __device__ __forceinline__ bool onstack_of(uint32_t mk) { return PK ? (mk & PK_ONSTACK) != 0 : (mk & 1u) != 0; }
+  __device__ __forceinline__ uint32_t rd_mark(uint32_t v) { return rd(L.vmark, v); }
+  __device__ __forceinline__ uint32_t rd_id(uint32_t v, uint32_t mk) {
+    if constexpr (PK) return mk & PK_ID_MASK;
+    else return rd(L.vid, v);
+  }
+  // v enters the search with id `id` (on the stack)
+  __device__ __forceinline__ void visit(uint32_t v, uint32_t mk, uint32_t id) {
+    if constexpr (PK) {
+      put(L.vmark, v, (mk & ~PK_ID_MASK) | id | PK_ONSTACK);
+    } else {
+      put(L.vid, v, id);
+      put(L.vmark, v, mk | 1u);
+    }
+  }
+  __device__ __forceinline__ void pop_stack(uint32_t x) {
+    if constexpr (PK) put(L.vmark, x, rd(L.vmark, x) & ~PK_ONSTACK);
+    else put(L.vmark, x, rd(L.vmark, x) & ~1u);
+  }
+  // finalize: id reset; a failed search marks the vertex visited in `ep`
+  __device__ __forceinline__ void unvisit(uint32_t x, uint32_t ep) {
+    if constexpr (PK) {
+      const uint32_t mk = rd(L.vmark, x);
+      put(L.vmark, x, ep ? (mk & PK_ONSTACK) | (ep << PK_EPOCH_SHIFT) : mk & ~PK_ID_MASK);
+    } else {
+      put(L.vid, x, 0);
+      if (ep) put(L.vmark, x, (rd(L.vmark, x) & 1u) | (ep << 1));
+    }
+  }
+  // DFS frame f: its vertex, next dep and low (packed: one word)
+  __device__ __forceinline__ void frame_save(uint32_t f, uint32_t v, uint32_t i, uint32_t low) {
+    if constexpr (PK) {
+      put(L.fv, f, v | (i << 10) | (low << 15));
+    } else {
+      put(L.fv, f, v);
+      put(L.fi, f, i);
+      put(L.vlow, f, low);
+    }
+  }
+  __device__ __forceinline__ void frame_load(uint32_t f, uint32_t& v, uint32_t& i, uint32_t& low) {
+    if constexpr (PK) {
+      const uint32_t w = rd(L.fv, f);
+      v = w & 0x3FFu;
+      i = (w >> 10) & 31u;
+      low = w >> 15;
+    } else {
+      v = rd(L.fv, f);
+      i = rd(L.fi, f);
+      low = rd(L.vlow, f);
+    }
   }
   // record fields of arrival r
   __device__ __forceinline__ size_t ix(uint32_t r) const { return fx_index(r, s, a.steps); }
@@ -104,16 +197,6 @@ struct W {
   // and kept in step by clock_add, so the per-edge check reads no LDS word
   // unless the seq is above the frontier
   uint32_t frv = 0;
-  __device__ __forceinline__ bool contains(uint32_t d) {
-    const uint32_t src = FX_DOT_SRC(d), sq = FX_DOT_SEQ(d);
-    if (src < 1 || src > L.n) return false;
-    const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)frv, (int)(src - 1));
-    if (sq <= f) return true;
-    const uint32_t off = sq - f - 1;
-    if (off >= L.WB * 32u) return false;
-    const uint32_t b = sq & (L.WB * 32u - 1u);
-    return (rd(L.bits, (src - 1) * L.WB + (b >> 5)) >> (b & 31u)) & 1u;
-  }
   __device__ __forceinline__ void clock_add(uint32_t d) {
     const uint32_t src = FX_DOT_SRC(d), sq = FX_DOT_SEQ(d);
     if (src < 1 || src > L.n) { err = FX_ERR_DOT_RANGE; return; }
@@ -135,20 +218,38 @@ struct W {
     if (lid == src - 1) frv = f;
   }
 
+  // executed_clock.contains(d), frontiers read from the table
+  __device__ __forceinline__ bool contains(uint32_t d) {
+    const uint32_t src = FX_DOT_SRC(d), sq = FX_DOT_SEQ(d);
+    if (src < 1 || src > L.n) return false;
+    const uint32_t f = rd(L.front, src - 1);
+    if (sq <= f) return true;
+    if (sq - f - 1 >= L.WB * 32u) return false;
+    const uint32_t b = sq & (L.WB * 32u - 1u);
+    return (rd(L.bits, (src - 1) * L.WB + (b >> 5)) >> (b & 31u)) & 1u;
+  }
+
   // ------------------------------------------------------- vertex index
+  // HBM: an index word is (vertex + 1) | seq / Q << 16, so it names its dot
+  // without a read of the vertex table.  Packed: a u16 (vertex + 1), and the
+  // vertex's dot is compared (read in the same round trip as its Tarjan word).
   __device__ __forceinline__ uint32_t hslot(uint32_t d) const {
     return (FX_DOT_SRC(d) - 1) * L.Q + (FX_DOT_SEQ(d) & (L.Q - 1u));
   }
-  // an index word is (vertex + 1) | seq / Q << 16: it names its dot without
-  // a read of the vertex table (the slot gives the source and seq mod Q)
   __device__ __forceinline__ uint32_t htag(uint32_t d) const {
     return (FX_DOT_SEQ(d) >> __builtin_ctz(L.Q)) << 16;
+  }
+  __device__ __forceinline__ uint32_t hword(uint32_t v, uint32_t d) const { return PK ? v + 1u : (v + 1) | htag(d); }
+  // the vertex an index word names for dot d (NONE if none); `vd` = that vertex's dot (packed only)
+  __device__ __forceinline__ uint32_t hmatch(uint32_t hw, uint32_t d, uint32_t vd) const {
+    if constexpr (PK) return (hw != 0 && vd == d) ? hw - 1u : NONE;
+    else return ((hw & 0xFFFFu) != 0 && (hw & 0xFFFF0000u) == htag(d)) ? (hw & 0xFFFFu) - 1u : NONE;
   }
   __device__ __forceinline__ uint32_t find(uint32_t d) {
     const uint32_t src = FX_DOT_SRC(d);
     if (src < 1 || src > L.n) return NONE;
-    const uint32_t w = rd(L.hidx, hslot(d));
-    return ((w & 0xFFFFu) != 0 && (w & 0xFFFF0000u) == htag(d)) ? (w & 0xFFFFu) - 1u : NONE;
+    const uint32_t w = lrd(L.hidx, hslot(d));
+    return hmatch(w, d, PK && w ? rd(L.vdot, (w & 0xFFFFu) - 1u) : 0u);
   }
 
   // ------------------------------------------------------- emission
@@ -158,16 +259,16 @@ struct W {
     for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
       const uint32_t i = i0 + lid;
       if (i < cnt) {
-        const uint32_t v = at(L.tstk, base + i), d = at(L.vdot, v);
+        const uint32_t v = lget(L.tstk, base + i), d = at(L.vdot, v);
         uint32_t r = 0;
-        for (uint32_t k = 0; k < cnt; ++k) r += at(L.vdot, at(L.tstk, base + k)) < d ? 1u : 0u;
-        at(L.tmp, r) = v;
+        for (uint32_t k = 0; k < cnt; ++k) r += at(L.vdot, lget(L.tstk, base + k)) < d ? 1u : 0u;
+        lset(L.tmp, r, v);
       }
     }
     __syncthreads();
     for (uint32_t r = 0; r < cnt; ++r) {
-      const uint32_t v = rd(L.tmp, r);
-      const uint32_t d = rd(L.vdot, v), rec = rd(L.vrec, v);
+      const uint32_t v = lrd(L.tmp, r);
+      const uint32_t d = rd(L.vdot, v), rec = rec_of(rd(L.vrec, v));
       if (nexec >= a.steps) { err = FX_ERR_ORDER_OVERFLOW; return; }
       if (lid == 0) {
         a.order[ix(nexec)] = rec | (r == 0 ? FX_ORDER_SCC_START : 0u);
@@ -175,12 +276,12 @@ struct W {
       }
       ++nexec;
       // remove from the index, free the slot; push to the released list
-      put(L.hidx, hslot(d), 0u);
+      lput(L.hidx, hslot(d), 0u);
       put(L.vdot, v, 0u);
       put(L.vwait, v, 0u);
       if (partial) put(L.vwn, v, 0u);
-      put(L.vfree, nfree++, v);
-      if (nwl >= 2 * L.P) { err = FX_ERR_CAPACITY; return; }
+      lput(L.vfree, nfree++, v);
+      if (nwl >= L.wlcap) { err = FX_ERR_CAPACITY; return; }
       put(L.wl, nwl++, d);
     }
   }
@@ -202,18 +303,15 @@ struct W {
     fsp = 0;
     nml = 0;
     frv = lid < L.n ? at(L.front, lid) : 0u;
-    put(L.vid, root, 1);
-    put(L.vlow, root, 1);
-    put(L.vmark, root, rd(L.vmark, root) | 1u);
-    put(L.tstk, tsp++, root);
-    put(L.fv, fsp, root);
+    visit(root, rd_mark(root), 1);
+    lput(L.tstk, tsp++, root);
     if (partial) put(L.fm, fsp, 0);
     ++fsp;
     // the top frame lives in registers: its vertex, next dep, id, low, dot,
     // dep count and dep row (lane j = dep j); a frame's position and low go
-    // to the tables only when it recurses, and come back when it resumes
+    // to the frame table only when it recurses, and come back when it resumes
     uint32_t cv = root, ci = 0, cid = 1, clow = 1, cdot = root_dot;
-    uint32_t cnd = rd(L.vnd, root);
+    uint32_t cnd = nd_of(root);
     uint32_t drow = lid < cnd ? at(L.vdeps, root * L.D + lid) : 0u;
     uint32_t result = FOUND;
     while (fsp && !err) {
@@ -226,12 +324,17 @@ struct W {
         const bool inr = src >= 1 && src <= L.n;
         const uint32_t si = inr ? src - 1 : 0u;
         const uint32_t bb = sq & (L.WB * 32u - 1u);
-        const uint32_t hw = rd(L.hidx, si * L.Q + (sq & (L.Q - 1u)));
+        const uint32_t hw = lrd(L.hidx, si * L.Q + (sq & (L.Q - 1u)));
         const uint32_t bw = rd(L.bits, si * L.WB + (bb >> 5));
         const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)frv, (int)si);
         const bool executed = inr && (sq <= f || (sq - f - 1u < L.WB * 32u && ((bw >> (bb & 31u)) & 1u)));
         if (d == cdot || executed) continue;  // self or executed (tarjan.rs:128-145)
-        const uint32_t w = (inr && (hw & 0xFFFFu) != 0 && (hw & 0xFFFF0000u) == htag(d)) ? (hw & 0xFFFFu) - 1u : NONE;
+        // the named vertex's Tarjan word (and, packed, its dot) in one round trip
+        const uint32_t hv = inr ? (hw & 0xFFFFu) : 0u;
+        const uint32_t hx = hv ? hv - 1u : 0u;
+        const uint32_t mkw = rd(L.vmark, hx);
+        const uint32_t aux = PK ? rd(L.vdot, hx) : rd(L.vid, hx);  // packed: its dot; HBM: its id
+        const uint32_t w = inr ? hmatch(hw, d, aux) : NONE;
         if (w == NONE) {
           if (collect) {  // partial replication, first search (tarjan.rs:158-166)
             bool seen = false;
@@ -247,15 +350,12 @@ struct W {
           result = MISSING;
           break;
         }
-        const uint32_t idw = rd(L.vid, w), mkw = rd(L.vmark, w);  // both reads in flight at once
+        const uint32_t idw = PK ? mkw & PK_ID_MASK : aux;
         if (idw == 0) {  // recurse
-          put(L.fi, fsp - 1, ci);
-          put(L.vlow, cv, clow);
+          frame_save(fsp - 1, cv, ci, clow);
           ++idc;
-          put(L.vid, w, idc);
-          put(L.vmark, w, mkw | 1u);
-          put(L.tstk, tsp++, w);
-          put(L.fv, fsp, w);
+          visit(w, mkw, idc);
+          lput(L.tstk, tsp++, w);
           if (partial) put(L.fm, fsp, 0);
           ++fsp;
           cv = w;
@@ -263,9 +363,9 @@ struct W {
           cid = idc;
           clow = idc;
           cdot = d;
-          cnd = rd(L.vnd, w);
+          cnd = nd_of(w);
           drow = lid < cnd ? at(L.vdeps, w * L.D + lid) : 0u;
-        } else if (mkw & 1u) {  // on the stack
+        } else if (onstack_of(mkw)) {  // on the stack
           clow = min(clow, idw);
         }
         continue;
@@ -277,8 +377,8 @@ struct W {
         uint32_t base = tsp;
         while (base > 0) {
           --base;
-          const uint32_t x = rd(L.tstk, base);
-          put(L.vmark, x, rd(L.vmark, x) & ~1u);
+          const uint32_t x = lrd(L.tstk, base);
+          pop_stack(x);
           clock_add(rd(L.vdot, x));  // executed_clock.add at pop time (tarjan.rs:293)
           if (x == cv) break;
         }
@@ -289,13 +389,14 @@ struct W {
       }
       --fsp;
       if (fsp) {  // resume the parent frame (tarjan.rs:211: low = min(low, dep low))
-        const uint32_t p = rd(L.fv, fsp - 1);
+        uint32_t p, pi, plow;
+        frame_load(fsp - 1, p, pi, plow);
         cv = p;
-        ci = rd(L.fi, fsp - 1);
-        cid = rd(L.vid, p);
-        clow = min(rd(L.vlow, p), lowv);
+        ci = pi;
+        cid = rd_id(p, rd_mark(p));
+        clow = min(plow, lowv);
         cdot = rd(L.vdot, p);
-        cnd = rd(L.vnd, p);
+        cnd = nd_of(p);
         drow = lid < cnd ? at(L.vdeps, p * L.D + lid) : 0u;
         if (mcount) put(L.fm, fsp - 1, rd(L.fm, fsp - 1) + mcount);  // tarjan.rs:198-200
       } else if (mcount) {
@@ -303,11 +404,7 @@ struct W {
       }
     }
     // finalize: ids of the vertices left on the stack; failed searches mark them visited
-    for (uint32_t k = 0; k < tsp; ++k) {
-      const uint32_t x = rd(L.tstk, k);
-      put(L.vid, x, 0);
-      if (mark_epoch && result == MISSING) put(L.vmark, x, (rd(L.vmark, x) & 1u) | (mark_epoch << 1));
-    }
+    for (uint32_t k = 0; k < tsp; ++k) unvisit(lrd(L.tstk, k), (mark_epoch && result == MISSING) ? mark_epoch : 0u);
     // ids of finished (popped) vertices are gone with their slots; a finished
     // vertex still present was on the stack, handled above
     tsp = 0;
@@ -380,21 +477,21 @@ struct W {
         }
         const uint64_t b = __ballot(w);
         if (w) {
-          at(L.tmp, cnt + __builtin_popcountll(b & ((1ull << lid) - 1ull))) = at(L.vdot, v);
+          lset(L.tmp, cnt + __builtin_popcountll(b & ((1ull << lid) - 1ull)), v);
           if (!partial) at(L.vwait, v) = 0;
         }
         cnt += __builtin_popcountll(b);
       }
       __syncthreads();
       if (!cnt) continue;
-      // rank sort the waiters' dots into tl
+      // rank sort the waiters by dot into tl
       for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
         const uint32_t i = i0 + lid;
         if (i < cnt) {
-          const uint32_t x = at(L.tmp, i);
+          const uint32_t x = lget(L.tmp, i), xd = at(L.vdot, x);
           uint32_t r = 0;
-          for (uint32_t k = 0; k < cnt; ++k) r += at(L.tmp, k) < x ? 1u : 0u;
-          at(L.tl, r) = x;
+          for (uint32_t k = 0; k < cnt; ++k) r += at(L.vdot, lget(L.tmp, k)) < xd ? 1u : 0u;
+          lset(L.tl, r, x);
         }
       }
       __syncthreads();
@@ -402,24 +499,42 @@ struct W {
       ++epoch;
       uint32_t cur = epoch;
       for (uint32_t k = 0; k < cnt && !err; ++k) {
-        const uint32_t wd = rd(L.tl, k);
-        const uint32_t wv = find(wd);
-        if (wv != NONE && (rd(L.vmark, wv) >> 1) == cur) continue;  // visited by a failed search
+        const uint32_t wv = lrd(L.tl, k);
+        // a waiter executed by an earlier search of this round is not pending
+        // (its slot is not reused before the next Add)
+        const uint32_t wd = rd(L.vdot, wv);
+        if (wd == 0) continue;
+        if (epoch_of(rd_mark(wv)) == cur) continue;  // visited by a failed search
         uint32_t missing = 0;
         bool saved = false;
         const uint32_t r = find_scc(wd, &missing, cur, &saved);
         if (r == FOUND) {
           cur = ++epoch;  // visited.clear()
         } else if (r == MISSING) {
-          const uint32_t v2 = find(wd);
-          if (v2 != NONE) index_pending(v2, missing);
+          if (rd(L.vdot, wv) == wd) {
+            index_pending(wv, missing);
+            if (!partial) put(L.vce, wv, saved ? NONE : nexec);
+          }
           if (saved) cur = ++epoch;
         }
       }
     }
   }
 
+  // packed marks hold 21 epoch bits: restart the epochs before they run out
+  // (between Adds no search is running, so every id is 0 and no vertex is on
+  // the stack; one Add advances the epoch by at most 2 P + 1 < 4096)
+  __device__ void renew_epochs() {
+    if constexpr (PK) {
+      if (epoch < PK_EPOCH_MAX) return;
+      for (uint32_t i = lid; i < L.P; i += 64) m[L.vmark + i] = 0u;
+      __syncthreads();
+      epoch = 1;
+    }
+  }
+
   __device__ void handle_add(uint32_t r) {
+    renew_epochs();
     const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.dot[ix(r)]);
     const uint32_t src = FX_DOT_SRC(d);
     if (src < 1 || src > L.n || FX_DOT_SEQ(d) == 0) { err = FX_ERR_DOT_RANGE; return; }
@@ -435,29 +550,62 @@ struct W {
     }
     if (kind != FX_KIND_ADD && kind != FX_KIND_INDEX_ONLY) { err = FX_ERR_UNSUPPORTED; return; }
     const uint32_t h = hslot(d);
-    const uint32_t old = rd(L.hidx, h);
+    const uint32_t old = lrd(L.hidx, h);
     if (old != 0) {
-      if ((old & 0xFFFF0000u) == htag(d)) { err = FX_ERR_DOUBLE_INDEX; return; }
+      const bool same = PK ? rd(L.vdot, old - 1u) == d : (old & 0xFFFF0000u) == htag(d);
+      if (same) { err = FX_ERR_DOUBLE_INDEX; return; }
       err = FX_ERR_CAPACITY;  // two pending dots of a source share an index slot
       return;
     }
     if (!nfree) { err = FX_ERR_CAPACITY; return; }
-    const uint32_t v = rd(L.vfree, --nfree);
+    const uint32_t v = lrd(L.vfree, --nfree);
     put(L.vdot, v, d);
-    put(L.vrec, v, r);
     const uint32_t nd = ndeps(r);
-    put(L.vnd, v, nd);
+    if constexpr (PK) {
+      put(L.vrec, v, r | (nd << PK_REC_BITS));
+    } else {
+      put(L.vrec, v, r);
+      put(L.vnd, v, nd);
+      put(L.vid, v, 0);
+    }
     if (lid < nd) m[L.vdeps + v * L.D + lid] = dep(r, lid);
     put(L.vwait, v, 0);
-    put(L.vid, v, 0);
     put(L.vmark, v, 0);
+    put(L.vce, v, NONE);
     if (partial) put(L.vwn, v, 0);
-    put(L.hidx, h, (v + 1) | htag(d));
+    lput(L.hidx, h, hword(v, d));
     __syncthreads();
     if (kind == FX_KIND_INDEX_ONLY) return;  // VertexIndex::index without a search (test hook)
+    nwl = 0;
+    // Search-result cache (as sim_big.hip x_add_): the first search from v
+    // enters its first dep u that is neither v nor executed (deps ascend,
+    // C1).  If u is pending and the last search rooted at u stopped at
+    // missing dep m with no execution here since (vce = executions then; m is
+    // the dot u waits on, vwait), and m is still missing and is not v, this
+    // search stops at m too having found no SCC: u's walk meets the same deps
+    // in the same states (a vertex pending then is still pending; one missing
+    // then would have stopped that walk, so only m can have arrived; v was
+    // missing then, so it is reachable only through m).  v just waits on m.
+    if (!partial) {
+      uint32_t u = 0;
+      for (uint32_t j = 0; j < nd && !u; ++j) {
+        const uint32_t dj = rd(L.vdeps, v * L.D + j);
+        if (dj != d && !contains(dj)) u = dj;
+      }
+      const uint32_t uv = u ? find(u) : NONE;
+      if (uv != NONE && rd(L.vce, uv) == nexec) {
+        const uint32_t cm = rd(L.vwait, uv);
+        const uint32_t cs = FX_DOT_SRC(cm);
+        if (cm && cm != d && cs >= 1 && cs <= L.n && find(cm) == NONE && !contains(cm)) {
+          index_pending(v, cm);
+          put(L.vce, v, nexec);
+          __syncthreads();
+          return;  // no search ran: nothing released
+        }
+      }
+    }
     uint32_t missing = 0;
     bool saved = false;
-    nwl = 0;
     const uint32_t res = find_scc(d, &missing, 0, &saved, partial);
     if (res == MISSING) {
       const uint32_t v2 = find(d);
@@ -466,6 +614,7 @@ struct W {
           for (uint32_t k = 0; k < nml && !err; ++k) index_pending(v2, rd(L.ml, k));
         } else {
           index_pending(v2, missing);
+          put(L.vce, v2, saved ? NONE : nexec);
         }
       }
     } else if (res == NOT_PENDING) {
@@ -482,7 +631,7 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t lane_idx = blockIdx.x;
   if (lane_idx >= a.num_lanes) return;
-  W w;
+  W<!HBM> w;
   w.a = a;
   w.L = L;
   w.lid = threadIdx.x;
@@ -495,7 +644,7 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
     for (uint32_t i = w.lid; i < L.words; i += 64)
       if (i < L.vdeps || i >= L.vdeps + L.P * L.D) w.m[i] = 0;
     __syncthreads();
-    for (uint32_t i = w.lid; i < L.P; i += 64) w.m[L.vfree + i] = L.P - 1u - i;
+    for (uint32_t i = w.lid; i < L.P; i += 64) w.lset(L.vfree, i, L.P - 1u - i);
     if (a.init_frontier && w.lid < L.n) w.m[L.front + w.lid] = a.init_frontier[(size_t)w.s * 8 + w.lid];
     __syncthreads();
     w.nfree = L.P;
@@ -505,6 +654,8 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
     w.nexec = w.rd(L.sc, 1);
     w.epoch = w.rd(L.sc, 2);
   }
+  // packed records hold 26-bit arrival indices: longer streams take the HBM tables
+  if (!HBM && a.steps >= (1u << PK_REC_BITS)) w.err = FX_ERR_CAPACITY;
   const uint32_t end = min(len, a.step_end);
   for (uint32_t r = a.step_begin; r < end && !w.err; ++r) {
     w.step = r;
@@ -531,14 +682,14 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
 
 }  // namespace wide
 
-// LDS tables: 512 vertices, 512 index slots per source, 1024-bit windows
-// (32 words); HBM tables: 16384 vertices, 32768 index slots, 32768-bit
+// LDS tables (packed): 512 vertices, 256 index slots per source, 1024-bit
+// windows (32 words): 31.2 KB at n = 5, five streams per CU; HBM tables: 16384 vertices, 32768 index slots, 32768-bit
 // windows, dep rows of
 // the widest Add (31) so a saved table stays valid when later Adds are wider
 static wide::Lay wide_layout(bool hbm, uint32_t n, uint32_t dmax, bool partial = false) {
   wide::Lay L;
   if (hbm) L.make(16384, 32768, 1024, n, 31, partial);
-  else L.make(512, 512, 32, n, std::max(dmax, 1u));
+  else L.make(512, 256, 32, n, std::max(dmax, 1u), false, true);
   return L;
 }
 

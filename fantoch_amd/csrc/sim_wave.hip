@@ -1924,12 +1924,15 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   const bool four = lds <= 160u * 1024u / 16u;  // 16 instances per CU: 4 waves per SIMD
   // the BASELINE geometries compiled in (same results as the run-time build)
   const bool fixed_ok = one_p && !(b->flags & FX_SIM_FLAG_GENERIC) && a.g.L <= 64;
-  // 20 instances per CU: 5 waves per SIMD (the compiled-in configs[1] / [2]
-  // n = 5 geometry is 8,192 B)
-#ifdef FX_SIM_NO_WPS5
-  const bool five = false;
-#else
+  // 5 waves per SIMD (a 102-VGPR budget) for the compiled-in configs[1] / [2]
+  // n = 5 geometry (8,192 B of LDS) is opt-in: a CU holds at most 16
+  // single-wave workgroups, so it still runs 4 per SIMD, with more spills
+  // (configs[1] 416 vs 418 M cmds/s at 4; two instances per 128-lane
+  // workgroup, 20 waves per CU, 399 M — r03f A/B)
+#ifdef FX_SIM_WPS5
   const bool five = lds <= 160u * 1024u / 20u;
+#else
+  const bool five = false;
 #endif
   if (fixed_ok && one_f && five && geo_is<GeoC1>(a.g, s0)) {
     hipLaunchKernelGGL((sim::k_sim<1, 1, 5, XNX, GeoC1>), grid, block, lds, hs, a);

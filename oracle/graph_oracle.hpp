@@ -198,7 +198,7 @@ struct DependencyGraph {
     } else {
       fr = strong_connect(first_find, dot, v, scc_count, missing_deps_count, result_missing);
     }
-    ORACLE_CENSUS(search(first_find, (int)fr, scc_count, stack.size(), dot, result_missing.first));
+    ORACLE_CENSUS(search(first_find, (int)fr, scc_count, stack, dot, result_missing.first));
     total_scc_count += scc_count;
     // save new SCCs (mod.rs:438-444)
     std::vector<std::set<Dot>> found;

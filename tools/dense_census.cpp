@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <map>
+#include <vector>
 
 struct Census {
   uint64_t rec[2] = {0, 0}, edges[2] = {0, 0}, srch[2] = {0, 0}, found[2] = {0, 0}, miss[2] = {0, 0};
@@ -19,8 +20,24 @@ struct Census {
   uint64_t execs = 0, hits = 0, hit_ok = 0;
   bool predicted = false;
   std::pair<uint32_t, uint64_t> pred_m;
+  // refined rule: the walk's vertices (the stack at the failure) all still pending
+  std::map<std::pair<uint32_t, uint64_t>, std::pair<std::pair<uint32_t, uint64_t>, std::vector<std::pair<uint32_t, uint64_t>>>> rcache;
+  uint64_t rhits = 0, rhit_ok = 0;
+  bool rpredicted = false;
+  std::pair<uint32_t, uint64_t> rpred_m;
   template <class D>
-  void search(bool f, int fr, size_t scc, size_t stk, const D& root, const D& m) {
+  void search(bool f, int fr, size_t scc, const std::vector<D>& stack, const D& root, const D& m) {
+    const size_t stk = stack.size();
+    if (f && rpredicted) {
+      if (fr == 1 && scc == 0 && m.source == rpred_m.first && m.sequence == rpred_m.second) rhit_ok++;
+      rpredicted = false;
+    }
+    if (fr == 1 && scc == 0) {
+      auto& e = rcache[{root.source, root.sequence}];
+      e.first = {m.source, m.sequence};
+      e.second.clear();
+      for (auto& x : stack) e.second.push_back({x.source, x.sequence});
+    }
     if (f && predicted) {
       if (fr == 1 && scc == 0 && m.source == pred_m.first && m.sequence == pred_m.second) hit_ok++;
       predicted = false;
@@ -76,6 +93,17 @@ int main(int argc, char** argv) {
           if (u == v || gr.executed_clock.contains(u.source, u.sequence)) continue;
           if (gr.find(u)) {
             auto it = C.cache.find({u.source, u.sequence});
+            auto rt = C.rcache.find({u.source, u.sequence});
+            if (rt != C.rcache.end()) {
+              const oracle::Dot m{rt->second.first.first, rt->second.first.second};
+              bool ok = !(m == v) && !gr.find(m) && !gr.executed_clock.contains(m.source, m.sequence);
+              for (auto& x : rt->second.second) ok = ok && gr.find(oracle::Dot{x.first, x.second}) != nullptr;
+              if (ok) {
+                C.rhits++;
+                C.rpredicted = true;
+                C.rpred_m = rt->second.first;
+              }
+            }
             if (it != C.cache.end() && it->second.second == C.execs) {
               const oracle::Dot m{it->second.first.first, it->second.first.second};
               if (!(m == v) && !gr.find(m) && !gr.executed_clock.contains(m.source, m.sequence)) {
@@ -121,6 +149,8 @@ int main(int argc, char** argv) {
          (double)C.stack_left / (double)(C.miss[0] + C.miss[1] + 1));
   printf("max per-source pending seq spread %llu; Adds with an index collision at Q=256: %llu, Q=512: %llu\n",
          (unsigned long long)maxspread, (unsigned long long)coll256, (unsigned long long)coll512);
+  printf("refined cache hits %.3f/Add, prediction held %llu of %llu\n", C.rhits / A, (unsigned long long)C.rhit_ok,
+         (unsigned long long)C.rhits);
   printf("cache hits %.3f/Add, prediction held %llu of %llu\n", C.hits / A, (unsigned long long)C.hit_ok,
          (unsigned long long)C.hits);
   return 0;
