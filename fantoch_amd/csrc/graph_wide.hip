@@ -155,16 +155,6 @@ struct W {
     if constexpr (PK) put(L.vmark, x, rd(L.vmark, x) & ~PK_ONSTACK);
     else put(L.vmark, x, rd(L.vmark, x) & ~1u);
   }
-  // finalize: id reset; a failed search marks the vertex visited in `ep`
-  __device__ __forceinline__ void unvisit(uint32_t x, uint32_t ep) {
-    if constexpr (PK) {
-      const uint32_t mk = rd(L.vmark, x);
-      put(L.vmark, x, ep ? (mk & PK_ONSTACK) | (ep << PK_EPOCH_SHIFT) : mk & ~PK_ID_MASK);
-    } else {
-      put(L.vid, x, 0);
-      if (ep) put(L.vmark, x, (rd(L.vmark, x) & 1u) | (ep << 1));
-    }
-  }
   // DFS frame f: its vertex, next dep and low (packed: one word)
   __device__ __forceinline__ void frame_save(uint32_t f, uint32_t v, uint32_t i, uint32_t low) {
     if constexpr (PK) {
@@ -329,11 +319,14 @@ struct W {
         const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)frv, (int)si);
         const bool executed = inr && (sq <= f || (sq - f - 1u < L.WB * 32u && ((bw >> (bb & 31u)) & 1u)));
         if (d == cdot || executed) continue;  // self or executed (tarjan.rs:128-145)
-        // the named vertex's Tarjan word (and, packed, its dot) in one round trip
+        // the named vertex's Tarjan word (and, packed, its dot), dep count and
+        // dep row in one round trip: a recursion into it then waits on nothing
         const uint32_t hv = inr ? (hw & 0xFFFFu) : 0u;
         const uint32_t hx = hv ? hv - 1u : 0u;
         const uint32_t mkw = rd(L.vmark, hx);
         const uint32_t aux = PK ? rd(L.vdot, hx) : rd(L.vid, hx);  // packed: its dot; HBM: its id
+        const uint32_t wnd = nd_of(hx);
+        const uint32_t wrow = lid < L.D ? at(L.vdeps, hx * L.D + lid) : 0u;
         const uint32_t w = inr ? hmatch(hw, d, aux) : NONE;
         if (w == NONE) {
           if (collect) {  // partial replication, first search (tarjan.rs:158-166)
@@ -363,8 +356,8 @@ struct W {
           cid = idc;
           clow = idc;
           cdot = d;
-          cnd = nd_of(w);
-          drow = lid < cnd ? at(L.vdeps, w * L.D + lid) : 0u;
+          cnd = wnd;
+          drow = lid < cnd ? wrow : 0u;
         } else if (onstack_of(mkw)) {  // on the stack
           clow = min(clow, idw);
         }
@@ -403,8 +396,23 @@ struct W {
         result = MISSING;  // NotFound -> MissingDependencies(collected) (mod.rs:478-484)
       }
     }
-    // finalize: ids of the vertices left on the stack; failed searches mark them visited
-    for (uint32_t k = 0; k < tsp; ++k) unvisit(lrd(L.tstk, k), (mark_epoch && result == MISSING) ? mark_epoch : 0u);
+    // finalize: ids of the vertices left on the stack; failed searches mark
+    // them visited (the members are distinct: one lane each)
+    const uint32_t ep = (mark_epoch && result == MISSING) ? mark_epoch : 0u;
+    for (uint32_t k0 = 0; k0 < tsp; k0 += 64) {
+      const uint32_t k = k0 + lid;
+      if (k < tsp) {
+        const uint32_t x = lget(L.tstk, k);
+        if constexpr (PK) {
+          const uint32_t mk = at(L.vmark, x);
+          at(L.vmark, x) = ep ? (mk & PK_ONSTACK) | (ep << PK_EPOCH_SHIFT) : mk & ~PK_ID_MASK;
+        } else {
+          at(L.vid, x) = 0u;
+          if (ep) at(L.vmark, x) = (at(L.vmark, x) & 1u) | (ep << 1);
+        }
+      }
+    }
+    __syncthreads();
     // ids of finished (popped) vertices are gone with their slots; a finished
     // vertex still present was on the stack, handled above
     tsp = 0;
