@@ -43,6 +43,13 @@ variant: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o fantoch_amd/build_$(V)/libfantoch_amd.so \
 	  $(filter-out $(OBJDIR)/sim_wave.hip.o,$(OBJS)) fantoch_amd/build_$(V)/sim_wave.o
 
+# the same for the wide executor tier (graph_wide.hip): make wvariant V=name D="-DFOO=1"
+wvariant: $(OBJS)
+	@mkdir -p fantoch_amd/build_$(V)
+	$(HIPCC) $(HIPFLAGS) $(D) -c -o fantoch_amd/build_$(V)/graph_wide.o fantoch_amd/csrc/graph_wide.hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o fantoch_amd/build_$(V)/libfantoch_amd.so \
+	  $(filter-out $(OBJDIR)/graph_wide.hip.o,$(OBJS)) fantoch_amd/build_$(V)/graph_wide.o
+
 ORACLE_SRCS := oracle/graph_oracle.cpp oracle/sim_oracle.cpp oracle/pred_oracle.cpp
 $(ORACLE): $(ORACLE_SRCS) oracle/graph_oracle.hpp include/fantoch_amd.h
 	@mkdir -p oracle/build
