@@ -634,11 +634,16 @@ struct W {
   }
 };
 
-template <bool HBM>
-__global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay L) {
+// FN / FD != 0: the layout of n = FN sources and FD dep planes compiled in
+// (the configs[3] shape, n = 5): table offsets become immediates and the
+// layout's fields leave the scalar registers, which the DFS is short of
+template <bool HBM, uint32_t FN = 0, uint32_t FD = 0>
+__global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay Lrt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t lane_idx = blockIdx.x;
   if (lane_idx >= a.num_lanes) return;
+  Lay L = Lrt;
+  if constexpr (FN != 0) L.make(512, 256, 32, FN, FD, false, true);
   W<!HBM> w;
   w.a = a;
   w.L = L;
@@ -755,11 +760,16 @@ int launch_wide(const KArgs& a, bool hbm, hipStream_t hs) {
   } else {
     static bool configured = false;
     if (!configured) {
+      (void)hipFuncSetAttribute((const void*)wide::k_graph_wide<false, 5, 5>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipFuncSetAttribute((const void*)wide::k_graph_wide<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
       configured = true;
     }
-    hipLaunchKernelGGL(wide::k_graph_wide<false>, dim3(a.num_lanes), dim3(64), (size_t)L.words * 4, hs, a, L);
+    if (a.n == 5 && std::max(a.dmax, 1u) == 5)
+      hipLaunchKernelGGL((wide::k_graph_wide<false, 5, 5>), dim3(a.num_lanes), dim3(64), (size_t)L.words * 4, hs, a, L);
+    else
+      hipLaunchKernelGGL(wide::k_graph_wide<false>, dim3(a.num_lanes), dim3(64), (size_t)L.words * 4, hs, a, L);
   }
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
