@@ -256,24 +256,30 @@ struct W {
       }
     }
     __syncthreads();
-    for (uint32_t r = 0; r < cnt; ++r) {
-      const uint32_t v = lrd(L.tmp, r);
-      const uint32_t d = rd(L.vdot, v), rec = rec_of(rd(L.vrec, v));
-      if (nexec >= a.steps) { err = FX_ERR_ORDER_OVERFLOW; return; }
-      if (lid == 0) {
-        a.order[ix(nexec)] = rec | (r == 0 ? FX_ORDER_SCC_START : 0u);
+    if (nexec + cnt > a.steps) { err = FX_ERR_ORDER_OVERFLOW; return; }
+    if (nwl + cnt > L.wlcap) { err = FX_ERR_CAPACITY; return; }
+    // emission, one lane per member (members are distinct vertices): the
+    // order rows, release steps, index / slot release and the released-dots
+    // worklist in the member order (LIFO pops see the same sequence)
+    for (uint32_t r0 = 0; r0 < cnt; r0 += 64) {
+      const uint32_t r = r0 + lid;
+      if (r < cnt) {
+        const uint32_t v = lget(L.tmp, r);
+        const uint32_t d = at(L.vdot, v), rec = rec_of(at(L.vrec, v));
+        a.order[ix(nexec + r)] = rec | (r == 0 ? FX_ORDER_SCC_START : 0u);
         a.release[ix(rec)] = step;
+        lset(L.hidx, hslot(d), 0u);
+        at(L.vdot, v) = 0u;
+        at(L.vwait, v) = 0u;
+        if (partial) at(L.vwn, v) = 0u;
+        lset(L.vfree, nfree + r, v);
+        at(L.wl, nwl + r) = d;
       }
-      ++nexec;
-      // remove from the index, free the slot; push to the released list
-      lput(L.hidx, hslot(d), 0u);
-      put(L.vdot, v, 0u);
-      put(L.vwait, v, 0u);
-      if (partial) put(L.vwn, v, 0u);
-      lput(L.vfree, nfree++, v);
-      if (nwl >= L.wlcap) { err = FX_ERR_CAPACITY; return; }
-      put(L.wl, nwl++, d);
     }
+    __syncthreads();
+    nexec += cnt;
+    nfree += cnt;
+    nwl += cnt;
   }
 
   // find_scc (mod.rs:409-486) + strong_connect (tarjan.rs:96-316) + finalize
@@ -576,7 +582,8 @@ struct W {
       put(L.vnd, v, nd);
       put(L.vid, v, 0);
     }
-    if (lid < nd) m[L.vdeps + v * L.D + lid] = dep(r, lid);
+    const uint32_t drj = lid < nd ? dep(r, lid) : 0u;  // lane j: dep j
+    if (lid < nd) m[L.vdeps + v * L.D + lid] = drj;
     put(L.vwait, v, 0);
     put(L.vmark, v, 0);
     put(L.vce, v, NONE);
@@ -595,11 +602,15 @@ struct W {
     // then would have stopped that walk, so only m can have arrived; v was
     // missing then, so it is reachable only through m).  v just waits on m.
     if (!partial) {
-      uint32_t u = 0;
-      for (uint32_t j = 0; j < nd && !u; ++j) {
-        const uint32_t dj = rd(L.vdeps, v * L.D + j);
-        if (dj != d && !contains(dj)) u = dj;
-      }
+      // the executed check of every dep at once (lane j: dep j)
+      const uint32_t sj = FX_DOT_SRC(drj), qj = FX_DOT_SEQ(drj);
+      const bool okj = lid < nd && sj >= 1 && sj <= L.n;
+      const uint32_t bj = qj & (L.WB * 32u - 1u);
+      const uint32_t fj = okj ? at(L.front, sj - 1) : 0u;
+      const uint32_t wj = okj ? at(L.bits, (sj - 1) * L.WB + (bj >> 5)) : 0u;
+      const bool exj = okj && (qj <= fj || (qj - fj - 1u < L.WB * 32u && ((wj >> (bj & 31u)) & 1u)));
+      const uint64_t cand = __ballot(lid < nd && drj != d && !exj);
+      const uint32_t u = cand ? (uint32_t)__builtin_amdgcn_readlane((int)drj, (int)__builtin_ctzll(cand)) : 0u;
       const uint32_t uv = u ? find(u) : NONE;
       if (uv != NONE && rd(L.vce, uv) == nexec) {
         const uint32_t cm = rd(L.vwait, uv);
