@@ -91,8 +91,17 @@ struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-
   }
 };
 
-template <bool PK>
+// RS = FD != 0 (the compiled-in layout): the states of a frame's deps are
+// looked up for all of its deps at once when the frame is entered (lane j:
+// dep j, one round trip), so an edge only reads the dep's vertex
+constexpr uint32_t RS_EXEC = 0x80000000u;
+template <bool PK, uint32_t FD = 0>
 struct W {
+#ifdef FX_WIDE_NO_RS
+  static constexpr bool RS = false;
+#else
+  static constexpr bool RS = PK && FD != 0;
+#endif
   KArgs a;
   Lay L;
   uint32_t* m;  // table memory (LDS or this stream's HBM block)
@@ -282,6 +291,50 @@ struct W {
     nwl += cnt;
   }
 
+  // lane j < nd: RS_EXEC if dep j is executed now, else its index word
+  // (vertex + 1; 0 = missing).  Exact for the whole life of the frame with
+  // one check at use: no vertex is added during a search, a missing dep
+  // cannot execute, and a pending one can only execute (its slot's dot then
+  // no longer matches)
+  __device__ __forceinline__ uint32_t row_state(uint32_t row, uint32_t nd) {
+    const uint32_t src = FX_DOT_SRC(row), sq = FX_DOT_SEQ(row);
+    const bool ok = lid < nd && src >= 1 && src <= L.n;
+    const uint32_t si = ok ? src - 1u : 0u;
+    const uint32_t bb = sq & (L.WB * 32u - 1u);
+    const uint32_t f = ok ? at(L.front, si) : 0u;
+    const uint32_t bw = ok ? at(L.bits, si * L.WB + (bb >> 5)) : 0u;
+    const uint32_t hw = ok ? lget(L.hidx, si * L.Q + (sq & (L.Q - 1u))) : 0u;
+    const bool ex = ok && (sq <= f || (sq - f - 1u < L.WB * 32u && ((bw >> (bb & 31u)) & 1u)));
+    return ex ? RS_EXEC : hw;
+  }
+  uint32_t fst[FD ? FD : 1];  // RS: lane f = the state of dep j of DFS frame f < 64
+  __device__ __forceinline__ void fst_save(uint32_t f, uint32_t st) {
+    if constexpr (RS) {
+      if (f < 64) {
+#pragma unroll
+        for (uint32_t j = 0; j < FD; ++j) {
+          const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)st, (int)j);
+          fst[j] = lid == f ? v : fst[j];
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ uint32_t fst_load(uint32_t f, uint32_t row, uint32_t nd) {
+    if constexpr (RS) {
+      if (f < 64) {
+        uint32_t st = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < FD; ++j) {
+          const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)fst[j], (int)f);
+          st = lid == j ? v : st;
+        }
+        return st;
+      }
+      return row_state(row, nd);
+    }
+    return 0u;
+  }
+
   // find_scc (mod.rs:409-486) + strong_connect (tarjan.rs:96-316) + finalize
   // (tarjan.rs:60-93).  Released dots are appended to the worklist; on a
   // missing dep, *missing = it and the stack members are marked visited with
@@ -309,8 +362,44 @@ struct W {
     uint32_t cv = root, ci = 0, cid = 1, clow = 1, cdot = root_dot;
     uint32_t cnd = nd_of(root);
     uint32_t drow = lid < cnd ? at(L.vdeps, root * L.D + lid) : 0u;
+    uint32_t cst = RS ? row_state(drow, cnd) : 0u;
     uint32_t result = FOUND;
     while (fsp && !err) {
+      if (RS && ci < cnd) {
+        const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)drow, (int)ci);
+        const uint32_t st = (uint32_t)__builtin_amdgcn_readlane((int)cst, (int)ci);
+        ++ci;
+        if (d == cdot || (st & RS_EXEC)) continue;  // self or executed (tarjan.rs:128-145)
+        if (st == 0) {  // missing (tarjan.rs:148-157)
+          *missing = d;
+          result = MISSING;
+          break;
+        }
+        const uint32_t hx = st - 1u;
+        const uint32_t mkw = rd(L.vmark, hx), vd = rd(L.vdot, hx), wnd = nd_of(hx);
+        const uint32_t wrow = lid < L.D ? at(L.vdeps, hx * L.D + lid) : 0u;
+        if (vd != d) continue;  // executed since the frame was entered
+        const uint32_t idw = mkw & PK_ID_MASK;
+        if (idw == 0) {  // recurse
+          frame_save(fsp - 1, cv, ci, clow);
+          fst_save(fsp - 1, cst);
+          ++idc;
+          visit(hx, mkw, idc);
+          lput(L.tstk, tsp++, hx);
+          ++fsp;
+          cv = hx;
+          ci = 0;
+          cid = idc;
+          clow = idc;
+          cdot = d;
+          cnd = wnd;
+          drow = lid < cnd ? wrow : 0u;
+          cst = row_state(drow, cnd);
+        } else if (onstack_of(mkw)) {
+          clow = min(clow, idw);
+        }
+        continue;
+      }
       if (ci < cnd) {
         const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)drow, (int)ci);
         ++ci;
@@ -397,6 +486,7 @@ struct W {
         cdot = rd(L.vdot, p);
         cnd = nd_of(p);
         drow = lid < cnd ? at(L.vdeps, p * L.D + lid) : 0u;
+        if (RS) cst = fst_load(fsp - 1, drow, cnd);
         if (mcount) put(L.fm, fsp - 1, rd(L.fm, fsp - 1) + mcount);  // tarjan.rs:198-200
       } else if (mcount) {
         result = MISSING;  // NotFound -> MissingDependencies(collected) (mod.rs:478-484)
@@ -655,7 +745,7 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay Lrt) {
   if (lane_idx >= a.num_lanes) return;
   Lay L = Lrt;
   if constexpr (FN != 0) L.make(512, 256, 32, FN, FD, false, true);
-  W<!HBM> w;
+  W<!HBM, FD> w;
   w.a = a;
   w.L = L;
   w.lid = threadIdx.x;
