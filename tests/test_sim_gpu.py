@@ -100,6 +100,25 @@ def test_conflict_sweep_n5(protocol, n, f):
     run_and_compare(specs)
 
 
+def test_config1_full_size_bench_instances():
+    """BASELINE configs[1] at the bench's full size: EPaxos n=5 f=2, GCP regions,
+    1 client per region, 1,000 commands per client, two instances per conflict
+    rate {100,50,10,2,0} % taken from the bench's own rate-major enumeration
+    (bench_sim.global_spec: seed 20250213, instance = global index, 4,096 seeds
+    per rate), bit-exact vs the oracle like every other instance."""
+    pl = planet()
+    regs = pl.ids(S.GCP5[:5])
+    specs = []
+    for k, c in enumerate([100, 50, 10, 2, 0]):
+        for g in (k * 4096, k * 4096 + 4095):
+            specs.append(S.spec(S.EPAXOS, 5, 2, regs, regs, commands_per_client=1000, conflict_rate=c,
+                                seed=20250213, instance=g))
+    res, orc = run_and_compare(specs)
+    # the run stops when the last client is done: a far process may still
+    # hold a few committed commands (the bench executes 24,996 of 25,000)
+    assert all(4900 <= len(e) <= 5000 for i in range(len(specs)) for e in res.executed(i))
+
+
 def test_region_subsets_n7():
     """configs[2] shape: Atlas n=7 f=1/2 over region subsets of the 20 GCP regions."""
     import itertools
