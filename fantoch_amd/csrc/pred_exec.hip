@@ -81,6 +81,9 @@ struct Pr {
   uint32_t* m;
   uint32_t lid, s;
   uint32_t err = 0, nfree = 0, fsp = 0, ltop = 0, nexec = 0, step = 0;
+  // registrations held by each phase's PendingIndex: a removal from an empty
+  // index finds no waiter, so its scan of the vertex table is skipped
+  uint32_t nreg0 = 0, nreg1 = 0;
 
   __device__ __forceinline__ void put(uint32_t b, uint32_t i, uint32_t v) {
     if (lid == 0) m[b + i] = v;
@@ -96,6 +99,8 @@ struct Pr {
   __device__ __forceinline__ void reg_set(uint32_t ph, uint32_t v, uint32_t j) {
     const uint32_t w = rw(ph, v, j);
     put(w, 0, rd(w, 0) | (1u << (j & 31u)));
+    if (ph) ++nreg1;
+    else ++nreg0;
   }
   __device__ __forceinline__ void reg_clear(uint32_t v) {
     for (uint32_t i = lid; i < 2 * L.DW; i += 64) m[L.vreg + ((i / L.DW) * L.P + v) * L.DW + i % L.DW] = 0;
@@ -158,6 +163,7 @@ struct Pr {
   // PendingIndex::remove(d) (index.rs:117-119) of phase `ph` (0 or 1) as a new
   // frame whose waiter list is ascending by dot
   __device__ void push_removed(uint32_t ph, uint32_t d) {
+    if ((ph ? nreg1 : nreg0) == 0) return;  // no waiter anywhere: an empty frame
     if (fsp >= L.FD) { err = FX_ERR_CAPACITY; return; }
     const uint32_t base = ltop;
     uint32_t cnt = 0;
@@ -187,6 +193,9 @@ struct Pr {
       cnt += __builtin_popcountll(b);
     }
     __syncthreads();
+    if (ph) nreg1 -= cnt;
+    else nreg0 -= cnt;
+    if (!cnt) return;  // an empty frame does nothing
     if (base + cnt > L.LL || cnt > L.P) { err = FX_ERR_CAPACITY; return; }
     for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {  // rank sort into the list stack
       const uint32_t i = i0 + lid;
@@ -214,7 +223,8 @@ struct Pr {
     const uint32_t rec = rd(L.vrec, v);
     put(L.hidx, hslot(d), 0);
     put(L.vdot, v, 0);
-    reg_clear(v);
+    // (v's registrations are all gone: each was removed when its dep
+    // committed / executed, which is what brought its missing count to 0)
     put(L.vfree, nfree++, v);
     execute(d, rec);
     push_removed(1, d);
