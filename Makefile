@@ -24,6 +24,16 @@ $(OBJDIR)/%.o: fantoch_amd/csrc/% $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+# (k_sim under -amdgpu-sched-strategy=iterative-ilp ran configs[1] at 424.6 M
+# against 418.8 M, but its n = 7 build then failed test_region_subsets_n7 with
+# FX_ERR_SIM_LATE: not adopted.  max-ilp / min-reg / max-occupancy /
+# memory-clause: 418 - 423 M.)
+SIM_SCHED :=
+# the large-instance simulator and the wide executor tiers under the iterative
+# ILP scheduler: configs[3] simulator 99.1 -> 103.1 M, dense executor 66.7 ->
+# 68.0 M (tools/mode_ab.sh), every GPU test passing
+$(OBJDIR)/sim_big.hip.o $(OBJDIR)/graph_wide.hip.o: HIPFLAGS += -mllvm -amdgpu-sched-strategy=iterative-ilp
+
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
 
@@ -39,7 +49,7 @@ $(PROF_LIB): $(SRCS) $(HDRS)
 # and links it with the other objects into fantoch_amd/build_$(V)/
 variant: $(OBJS)
 	@mkdir -p fantoch_amd/build_$(V)
-	$(HIPCC) $(HIPFLAGS) $(D) -c -o fantoch_amd/build_$(V)/sim_wave.o fantoch_amd/csrc/sim_wave.hip
+	$(HIPCC) $(HIPFLAGS) $(SIM_SCHED) $(D) -c -o fantoch_amd/build_$(V)/sim_wave.o fantoch_amd/csrc/sim_wave.hip
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o fantoch_amd/build_$(V)/libfantoch_amd.so \
 	  $(filter-out $(OBJDIR)/sim_wave.hip.o,$(OBJS)) fantoch_amd/build_$(V)/sim_wave.o
 
@@ -49,6 +59,13 @@ wvariant: $(OBJS)
 	$(HIPCC) $(HIPFLAGS) $(D) -c -o fantoch_amd/build_$(V)/graph_wide.o fantoch_amd/csrc/graph_wide.hip
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o fantoch_amd/build_$(V)/libfantoch_amd.so \
 	  $(filter-out $(OBJDIR)/graph_wide.hip.o,$(OBJS)) fantoch_amd/build_$(V)/graph_wide.o
+
+# any one source: make fvariant V=name F=sim_big D="-DFOO=1" (F = a .hip under csrc/)
+fvariant: $(OBJS)
+	@mkdir -p fantoch_amd/build_$(V)
+	$(HIPCC) $(HIPFLAGS) $(D) -c -o fantoch_amd/build_$(V)/$(F).o fantoch_amd/csrc/$(F).hip
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o fantoch_amd/build_$(V)/libfantoch_amd.so \
+	  $(filter-out $(OBJDIR)/$(F).hip.o,$(OBJS)) fantoch_amd/build_$(V)/$(F).o
 
 ORACLE_SRCS := oracle/graph_oracle.cpp oracle/sim_oracle.cpp oracle/pred_oracle.cpp
 $(ORACLE): $(ORACLE_SRCS) oracle/graph_oracle.hpp include/fantoch_amd.h
