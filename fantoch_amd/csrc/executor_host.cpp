@@ -53,6 +53,36 @@ struct DevBuf {
   uint32_t* u32() const { return static_cast<uint32_t*>(p); }
 };
 
+// pinned host memory mapped into the device's address space: the handle's
+// upload staging and the words a flush reports (written by the device)
+struct HostBuf {
+  void* p = nullptr;
+  void* dp = nullptr;
+  size_t bytes = 0;
+  ~HostBuf() { release(); }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = dp = nullptr;
+    bytes = 0;
+  }
+  bool ensure(size_t b) {
+    if (bytes >= b) return true;
+    release();
+    if (hipHostMalloc(&p, b, hipHostMallocMapped) != hipSuccess) {
+      p = nullptr;
+      return false;
+    }
+    if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
+      release();
+      return false;
+    }
+    bytes = b;
+    return true;
+  }
+  uint32_t* u32() const { return static_cast<uint32_t*>(p); }
+  uint32_t* du32() const { return static_cast<uint32_t*>(dp); }
+};
+
 constexpr uint32_t kDmaxDev = 31;
 
 }  // namespace
@@ -120,6 +150,9 @@ struct fx_graph_executor {
   std::map<uint64_t, uint64_t> chain_size, execution_delay;
   std::map<uint32_t, std::vector<fx_rifl>> monitor;
   DevBuf d_gather;            // release steps of the entries of one flush
+  HostBuf h_up;               // upload staging (pinned), copied to d_up and scattered into the planes
+  DevBuf d_up;
+  HostBuf h_out;              // nexec, err, (order word, release step) per new entry (device-written)
   uint64_t bytes_h2d = 0, bytes_d2h = 0;  // transfer accounting (fx_graph_executor_transfer_stats)
   int sticky = FX_OK;
 };
@@ -148,23 +181,24 @@ int upload_tail(fx_graph_executor* ex) {
   if (ex->uploaded >= N) return FX_OK;
   const uint32_t r0 = ex->uploaded & ~3u;
   const uint32_t r1 = (N + 3) & ~3u;
-  const size_t tiles = (r1 - r0) / 4, w0 = fx_index(r0, 0, ex->cap);
-  const size_t plane = fx_plane_words(1, ex->cap);
-  std::vector<uint32_t> hd(tiles * 4, 0), hh(tiles * 4, 0), hp(tiles * 4 * ex->dmax, 0);
+  const uint32_t rows = r1 - r0, nplanes = 2 + ex->dmax;
+  // one staging block, plane-major (dot, hdr, dep planes), one copy, one scatter
+  const size_t words = (size_t)nplanes * rows;
+  if (!ex->h_up.ensure(words * 4) || !ex->d_up.ensure(words * 4)) return FX_ERR_HIP;
+  uint32_t* st = ex->h_up.u32();
+  std::memset(st, 0, words * 4);
   for (uint32_t i = r0; i < N; ++i) {
     const size_t at = i - r0;
-    hd[at] = ex->dots[i];
-    hh[at] = ex->hdrs[i];
-    for (uint32_t j = 0; j < ex->deps[i].size(); ++j) hp[j * tiles * 4 + at] = ex->deps[i][j];
+    st[at] = ex->dots[i];
+    st[rows + at] = ex->hdrs[i];
+    for (uint32_t j = 0; j < ex->deps[i].size(); ++j) st[(size_t)(2 + j) * rows + at] = ex->deps[i][j];
   }
-  ex->bytes_h2d += (uint64_t)(hd.size() + hh.size() + hp.size()) * 4;
-  auto put2d = [&](uint32_t* dst, const uint32_t* src) {
-    return hipMemcpy2DAsync(dst, 256 * 4, src, 4 * 4, 4 * 4, tiles, hipMemcpyHostToDevice, ex->stream);
-  };
-  if (put2d(ex->d_dot.u32() + w0, hd.data()) || put2d(ex->d_hdr.u32() + w0, hh.data())) return FX_ERR_HIP;
-  for (uint32_t j = 0; j < ex->dmax; ++j)
-    if (put2d(ex->d_deps.u32() + j * plane + w0, hp.data() + j * tiles * 4)) return FX_ERR_HIP;
-  if (hipStreamSynchronize(ex->stream)) return FX_ERR_HIP;
+  ex->bytes_h2d += (uint64_t)words * 4;
+  // the staging block stays untouched until the flush's synchronisation
+  if (hipMemcpyAsync(ex->d_up.p, st, words * 4, hipMemcpyHostToDevice, ex->stream)) return FX_ERR_HIP;
+  if (fx::scatter_rows(ex->d_up.u32(), nplanes, r0, rows, ex->cap, ex->d_dot.u32(), ex->d_hdr.u32(),
+                       ex->d_deps.u32(), ex->stream))
+    return FX_ERR_HIP;
   ex->uploaded = N;
   return FX_OK;
 }
@@ -252,10 +286,15 @@ int flush(fx_graph_executor* ex) {
     int st = fx_batch_execute(&in, &out, ex->tier, nullptr, 1, ex->d_state.p, ex->processed, N, flags,
                               nullptr, ex->stream);
     if (st) return ex->sticky = st;
-    if (hipMemcpyAsync(&nexec, ex->d_nexec.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
-        hipMemcpyAsync(&err, ex->d_err.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
+    // nexec, err and the new entries straight into mapped host memory: one
+    // synchronisation per flush
+    if (!ex->h_out.ensure((size_t)(2 + 2 * (size_t)ex->cap) * 4)) return ex->sticky = FX_ERR_HIP;
+    if (fx::flush_pack(ex->d_order.u32(), ex->d_release.u32(), ex->d_nexec.u32(), ex->d_err.u32(), ex->cap,
+                       ex->consumed, ex->h_out.du32(), ex->stream) ||
         hipStreamSynchronize(ex->stream))
       return ex->sticky = FX_ERR_HIP;
+    nexec = ex->h_out.u32()[0];
+    err = ex->h_out.u32()[1];
     if (err == FX_ERR_CAPACITY && ex->tier != FX_TIER_WIDE_HBM) {
       // rerun the whole log one tier up (group -> LDS -> HBM slots -> HBM
       // tables, the last one resumable like the others); the already-consumed
@@ -271,10 +310,20 @@ int flush(fx_graph_executor* ex) {
   if (err) return ex->sticky = (int)err;
   ex->processed = N;
   if (nexec <= ex->consumed) return FX_OK;
-  // read back the new order entries and the release steps they need
+  // the new order entries and the release steps they need: packed by the
+  // flush (non-partial), else read back here
   std::vector<uint32_t> order(nexec - ex->consumed);
   const uint32_t k0 = ex->consumed;
-  {
+  std::vector<uint32_t> rel(nexec - k0);
+  if (!ex->partial) {
+    const uint32_t* w = ex->h_out.u32() + 2;
+    for (uint32_t t = 0; t < nexec - k0; ++t) {
+      order[t] = w[2 * t];
+      rel[t] = w[2 * t + 1];
+    }
+    ex->bytes_d2h += 8 + (uint64_t)(nexec - k0) * 8;
+  }
+  if (ex->partial) {
     const uint32_t r0 = k0 & ~3u, r1 = (nexec + 3) & ~3u;
     // the first 4 words of each tile (this stream's rows), strided
     std::vector<uint32_t> rows((size_t)(r1 - r0));
@@ -286,8 +335,7 @@ int flush(fx_graph_executor* ex) {
   }
   // the release steps of exactly the commands converted below, gathered on
   // the device (bytes moved per flush are linear in its new order entries)
-  std::vector<uint32_t> rel(nexec - k0);
-  {
+  if (ex->partial) {
     if (!ex->d_gather.ensure((size_t)(nexec - k0) * 4)) return ex->sticky = FX_ERR_HIP;
     if (fx::gather_release(ex->d_order.u32(), ex->d_release.u32(), ex->cap, k0, nexec,
                            ex->d_gather.u32(), ex->stream) ||

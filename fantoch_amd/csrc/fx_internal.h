@@ -87,6 +87,11 @@ void split_profile_record(int which, bool end, hipStream_t s);
 // Single-stream gather used by the executor handle: out[k - k0] =
 // release[rec(order[k])] for k in [k0, k1), so a flush reads back only the
 // release steps of the commands it converts (bytes linear in the executed count).
+// the drop-in handle's transfers (graph_exec.hip)
+int scatter_rows(const uint32_t* stage, uint32_t nplanes, uint32_t r0, uint32_t rows, uint32_t cap, uint32_t* dot,
+                 uint32_t* hdr, uint32_t* deps, hipStream_t stream);
+int flush_pack(const uint32_t* order, const uint32_t* release, const uint32_t* nexec, const uint32_t* err,
+               uint32_t cap, uint32_t k0, uint32_t* out, hipStream_t stream);
 int gather_release(const uint32_t* order, const uint32_t* release, uint32_t steps, uint32_t k0,
                    uint32_t k1, uint32_t* out, hipStream_t stream);
 

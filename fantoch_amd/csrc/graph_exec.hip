@@ -847,6 +847,60 @@ int gather_release(const uint32_t* order, const uint32_t* release, uint32_t step
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 
+// ---------------------------------------- single-stream handle transfers
+// The handle's uploads arrive as one contiguous staging block (plane-major:
+// rows [r0, r0 + rows) of dot, hdr, then each dep plane) and are scattered
+// into the stream's words of each 64-stream tile on the device.
+__global__ __launch_bounds__(256) void k_scatter_rows(const uint32_t* __restrict__ stage, uint32_t nplanes,
+                                                      uint32_t r0, uint32_t rows, uint32_t cap, uint32_t* dot,
+                                                      uint32_t* hdr, uint32_t* deps, size_t plane) {
+  const size_t total = (size_t)nplanes * rows;
+  for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t pl = (uint32_t)(x / rows), t = (uint32_t)(x % rows);
+    uint32_t* dst = pl == 0 ? dot : pl == 1 ? hdr : deps + (size_t)(pl - 2) * plane;
+    dst[fx_index(r0 + t, 0, cap)] = stage[x];
+  }
+}
+
+int scatter_rows(const uint32_t* stage, uint32_t nplanes, uint32_t r0, uint32_t rows, uint32_t cap, uint32_t* dot,
+                 uint32_t* hdr, uint32_t* deps, hipStream_t stream) {
+  if (!rows || !nplanes) return FX_OK;
+  const size_t total = (size_t)nplanes * rows;
+  const uint32_t blocks = (uint32_t)std::min<size_t>((total + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_scatter_rows, dim3(blocks), dim3(256), 0, stream, stage, nplanes, r0, rows, cap, dot, hdr,
+                     deps, fx_plane_words(1, cap));
+  return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
+}
+
+// After a handle's flush: out[0] = nexec, out[1] = err, then for each new
+// order entry k in [k0, nexec) its order word and its release step, written
+// straight into host-mapped memory (one synchronisation per flush, and only
+// the words a flush produced cross the bus).
+__global__ __launch_bounds__(256) void k_flush_pack(const uint32_t* __restrict__ order,
+                                                    const uint32_t* __restrict__ release,
+                                                    const uint32_t* __restrict__ nexec,
+                                                    const uint32_t* __restrict__ err, uint32_t cap, uint32_t k0,
+                                                    uint32_t* out) {
+  const uint32_t ne = *nexec;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    out[0] = ne;
+    out[1] = *err;
+  }
+  const uint32_t cnt = ne > k0 ? min(ne, cap) - k0 : 0u;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < cnt; t += gridDim.x * blockDim.x) {
+    const uint32_t o = order[fx_index(k0 + t, 0, cap)];
+    const uint32_t rec = FX_ORDER_REC(o);
+    out[2 + 2 * t] = o;
+    out[3 + 2 * t] = rec < cap ? release[fx_index(rec, 0, cap)] : FX_RELEASE_NONE;
+  }
+}
+
+int flush_pack(const uint32_t* order, const uint32_t* release, const uint32_t* nexec, const uint32_t* err,
+               uint32_t cap, uint32_t k0, uint32_t* out, hipStream_t stream) {
+  hipLaunchKernelGGL(k_flush_pack, dim3(4), dim3(256), 0, stream, order, release, nexec, err, cap, k0, out);
+  return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
+}
+
 // ----------------------------------------------------------- synthesis
 __global__ __launch_bounds__(256) void k_synth(fx_synth_params p, uint32_t S, uint32_t steps,
                                                uint32_t* dot, uint32_t* hdr, uint32_t* deps) {
