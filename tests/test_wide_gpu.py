@@ -74,3 +74,36 @@ def test_config3_many_clients_escalation(clients, cmds, window):
     assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
     assert np.nonzero(chain)[0].max() > 5 * clients // 2  # SCCs far beyond n
     assert res.tier_counts[_lib.FX_TIER_WIDE] > 0
+
+
+def test_wide_lds_index_collision_escalates():
+    """The packed LDS tables index 256 seqs per source: two pending dots of one
+    source 256 seqs apart share a slot, the LDS tier stops the stream with
+    FX_ERR_CAPACITY and the tiered driver reruns it on the HBM tables, where
+    the output equals the oracle's.  (1, 1) waits on the missing (2, 1); every
+    later (1, s) depends on (1, s - 1), so (1, 1) ... (1, 257) are all pending
+    when (1, 257) arrives; (2, 1) then releases the whole chain."""
+    stream = [((1, 1), [(2, 1)], 0)]
+    stream += [((1, s), [(1, s - 1)], s) for s in range(2, 258)]
+    stream.append(((2, 1), [], 300))
+    planes = fs.pack_streams([stream], 2)
+    res = fd.run_batch(planes, tiered=False, tier=_lib.FX_TIER_WIDE)
+    assert int(res.err[0]) == _lib.FX_ERR_CAPACITY
+    res = fd.run_batch(planes, tier=_lib.FX_TIER_WIDE)
+    assert res.status == _lib.FX_OK and int(res.err[0]) == 0
+    assert_parity(planes, res)
+    assert int(res.nexec[0]) == len(stream)
+    assert res.tier_counts[_lib.FX_TIER_WIDE_HBM] == 1
+
+
+def test_wide_lds_chain_one_below_the_index_span():
+    """The same chain 255 seqs long fits the LDS tier's index (no collision)
+    and runs there, bit-exact."""
+    stream = [((1, 1), [(2, 1)], 0)]
+    stream += [((1, s), [(1, s - 1)], s) for s in range(2, 257)]
+    stream.append(((2, 1), [], 300))
+    planes = fs.pack_streams([stream], 2)
+    res = fd.run_batch(planes, tiered=False, tier=_lib.FX_TIER_WIDE)
+    assert int(res.err[0]) == 0
+    assert_parity(planes, res)
+    assert int(res.nexec[0]) == len(stream)
