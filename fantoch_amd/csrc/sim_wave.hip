@@ -331,6 +331,12 @@ struct Sim : GP {
     if (!err) prm_set(P_ERRSITE, line);
     err = FX_ERR_SIM_CAPACITY;
   }
+  // a simulated message that found no state for its dot (the reference
+  // panics): the site is recorded like a capacity failure's
+  __device__ __forceinline__ void fail_late(uint32_t line) {
+    if (!err) prm_set(P_ERRSITE, line);
+    err = FX_ERR_SIM_LATE;
+  }
   uint32_t now = 0;       // ms
   uint32_t seq = 0;       // insertion counter (C3)
   uint32_t events = 0;  // <= max_events < 2^32
@@ -719,7 +725,7 @@ struct Sim : GP {
   // atlas.rs:251-325 / epaxos.rs:223-301
   __device__ __forceinline__ void h_mcollect(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = slot_find(dot);
-    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
+    if (sl == NONE) { fail_late(__LINE__); return; }
     const uint32_t ps = pst(sl, p);
     if ((ps & 3u) != ST_START) return;
     const uint32_t src = (dot >> FX_SEQ_BITS) - 1u;
@@ -754,7 +760,7 @@ struct Sim : GP {
   // atlas.rs:327-402 / epaxos.rs:303-368
   __device__ __forceinline__ void h_mcollectack(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = slot_find(dot);
-    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
+    if (sl == NONE) { fail_late(__LINE__); return; }
     if ((pst(sl, p) & 3u) != ST_COLLECT) return;
     const uint32_t masks = uni(S(sl, SL_MASKS));
     const uint32_t part = (masks & 0xFFu) | (1u << from);
@@ -810,7 +816,7 @@ struct Sim : GP {
   // atlas.rs:404-475 / epaxos.rs:370-428
   __device__ __forceinline__ void h_mcommit(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = slot_find(dot);
-    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
+    if (sl == NONE) { fail_late(__LINE__); return; }
     const uint32_t ps = pst(sl, p);
     if ((ps & 3u) == ST_START) {  // buffered_commits.insert
       set_pst(sl, p, (ps & 0x0Bu) | 4u | (from << 4));
@@ -830,7 +836,7 @@ struct Sim : GP {
   // atlas.rs:477-524 / epaxos.rs:430-477
   __device__ __forceinline__ void h_mconsensus(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = slot_find(dot);
-    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
+    if (sl == NONE) { fail_late(__LINE__); return; }
     const uint32_t ps = pst(sl, p);
     if ((ps & 3u) == ST_COMMIT) {  // chosen: reply with the chosen value
       act_send(M_COMMIT, dot, 1u << from);
@@ -843,13 +849,13 @@ struct Sim : GP {
   // atlas.rs:526-558 / epaxos.rs:479-517
   __device__ __forceinline__ void h_mconsensusack(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = slot_find(dot);
-    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
+    if (sl == NONE) { fail_late(__LINE__); return; }
     if (!((uni(S(sl, SL_CNT)) >> 16) & 1u)) return;  // proposer ballot != b
     const uint32_t masks = uni(S(sl, SL_MASKS));
     const uint32_t acc = ((masks >> 8) & 0xFFu) | (1u << from);
     if (pop32(acc) == synod_f + 1u) {
       put(S(sl, SL_MASKS), masks & ~0xFF00u);  // reset_state
-      if (!(pst(sl, p) & 8u)) { err = FX_ERR_SIM_LATE; return; }  // single.rs:346-349 panic
+      if (!(pst(sl, p) & 8u)) { fail_late(__LINE__); return; }  // single.rs:346-349 panic
       act_send(M_COMMIT, dot, (1u << n) - 1u);
     } else {
       put(S(sl, SL_MASKS), (masks & ~0xFF00u) | (acc << 8));
@@ -1134,12 +1140,12 @@ struct Sim : GP {
     const uint32_t delay = now - start;  // ExecutionDelay (graph/mod.rs:514-518)
     hist_delay(delay);
     const uint32_t sl = slot_find(d);
-    if (sl == NONE) { err = FX_ERR_SIM_LATE; return; }
+    if (sl == NONE) { fail_late(__LINE__); return; }
     const uint32_t c = uni(S(sl, SL_CLIENT));
     const uint32_t nk = (uni(S(sl, SL_CNT)) >> 20) & 3u;
     if ((rl(ca, c) & 0xFFu) == p) {  // pending.wait_for registered this rifl at p
       const uint32_t pend = rl(cb, 32u + c);
-      if (pend < nk) { err = FX_ERR_SIM_LATE; return; }
+      if (pend < nk) { fail_late(__LINE__); return; }
       lset(cb, 32u + c, pend - nk);  // one ExecutorResult per key
       if (pend == nk) {
         const uint32_t fi = nfrm - 1;
