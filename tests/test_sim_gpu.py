@@ -174,3 +174,24 @@ def test_capacity_escalation_is_exact():
     # 24 messages / 16 dots in flight: the lagging placements outgrow them
     res, _ = run_and_compare(specs, ring_entries=24, dot_slots=16)
     assert res.reruns > 0
+
+
+def test_config2_bench_placements_full_size():
+    """BASELINE configs[2] at the bench's size: placements taken from
+    bench_placements' own global enumeration (every (n, f) group, spread over
+    the 186,048-placement sweep), Atlas, one client per process region, 100
+    commands per client, 2 % conflicts, seed 20250213, instance = placement
+    id, exactly as `bench.py --mode placements` builds them; bit-exact vs the
+    oracle, one launch per geometry."""
+    import bench_placements as BP
+    pl = planet()
+    allp = BP.enumerate_placements(pl.R)
+    assert len(allp) == 186048
+    for n in (5, 7):
+        ids = []
+        for f in (1, 2):  # 6 placements spread over each (n, f) group
+            grp = [g for g, (n2, f2, _) in enumerate(allp) if (n2, f2) == (n, f)]
+            ids += [grp[k * (len(grp) - 1) // 5] for k in range(6)]
+        specs = [S.spec(S.ATLAS, n, allp[g][1], list(allp[g][2]), list(allp[g][2]), commands_per_client=100,
+                        conflict_rate=2, seed=20250213, instance=g) for g in ids]
+        run_and_compare(specs)
