@@ -593,8 +593,11 @@ struct Sim : GP {
     uint32_t e = 0;
     if (tq) {
       e = lds[g.off_free + nfree - 1u - r];
-      uint4* m = reinterpret_cast<uint4*>(&lds[g.off_pool + e * 4u]);
-      *m = make_uint4(t | (kind << 28), seq + r, w2, LNIL);
+      // one 16-byte store of the entry's four words; the vector type may
+      // alias the u32 words the message is read back through (msg)
+      typedef uint32_t u32x4_alias __attribute__((ext_vector_type(4), may_alias));
+      u32x4_alias v4 = {t | (kind << 28), seq + r, w2, LNIL};
+      *reinterpret_cast<u32x4_alias*>(&lds[g.off_pool + e * 4u]) = v4;
       if (head != LNIL) msg(rh >> 16, 3) = e;  // after the tail
     }
     const uint32_t nrh = head == LNIL ? (e | (e << 16)) : (head | (e << 16));
