@@ -15,7 +15,9 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-functi
 SRCS := fantoch_amd/csrc/graph_exec.hip fantoch_amd/csrc/graph_group.hip fantoch_amd/csrc/graph_wave.hip fantoch_amd/csrc/graph_lane.hip fantoch_amd/csrc/graph_split.hip fantoch_amd/csrc/graph_cut.hip fantoch_amd/csrc/graph_wide.hip fantoch_amd/csrc/pred_exec.hip fantoch_amd/csrc/executor_host.cpp fantoch_amd/csrc/exec_log.cpp fantoch_amd/csrc/config.cpp fantoch_amd/csrc/planet.cpp fantoch_amd/csrc/sim_wave.hip fantoch_amd/csrc/sim_big.hip
 HDRS := include/fantoch_amd.h include/fantoch_amd.hpp fantoch_amd/csrc/fx_synth.h fantoch_amd/csrc/fx_internal.h
 
-all: $(LIB) $(ORACLE) $(CPPTEST)
+POISON := tests/poison/build/libpoison.so
+
+all: $(LIB) $(ORACLE) $(CPPTEST) $(POISON)
 
 # one object per source (make -j compiles them in parallel), then one link
 OBJDIR := fantoch_amd/build/obj
@@ -77,6 +79,12 @@ $(CPPTEST): tests/cpp/test_graph_executor.cpp include/fantoch_amd.hpp include/fa
 	@mkdir -p tests/cpp/build
 	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ tests/cpp/test_graph_executor.cpp \
 	  -Lfantoch_amd -lfantoch_amd -Wl,-rpath,'$$ORIGIN/../../../fantoch_amd'
+
+# test-only: fills the register file with tagged garbage before a kernel under
+# test (tests/test_sim_poison.py)
+$(POISON): tests/poison/poison.hip
+	@mkdir -p tests/poison/build
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -o $@ $<
 
 # kernel resource usage (VGPR/SGPR/LDS/occupancy) for DESIGN.md / tuning
 resource-usage:

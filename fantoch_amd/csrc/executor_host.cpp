@@ -203,6 +203,14 @@ int upload_tail(fx_graph_executor* ex) {
   return FX_OK;
 }
 
+// An error after upload_tail queued the staging copy: the copy may still be
+// reading the pinned staging block, which a later ensure() or the destructor
+// frees, so the stream is drained before the error is returned (sticky)
+int fail_sync(fx_graph_executor* ex, int st) {
+  (void)hipStreamSynchronize(ex->stream);
+  return ex->sticky = st;
+}
+
 // Runs the steps not yet executed; converts new order entries.
 int flush(fx_graph_executor* ex) {
   if (ex->sticky) return ex->sticky;
@@ -218,7 +226,7 @@ int flush(fx_graph_executor* ex) {
   }
   {
     int st = upload_tail(ex);
-    if (st) return ex->sticky = st;
+    if (st) return fail_sync(ex, st);
   }
   fx_stream_batch in{};
   in.dot = ex->d_dot.u32();
@@ -235,28 +243,28 @@ int flush(fx_graph_executor* ex) {
     // the ring holds this flush's first-missing parents (<= its deps + records)
     const uint32_t want = std::max<uint32_t>(1024, (N - ex->processed) * (ex->dmax + 1) * 2);
     if (want > ex->req_cap) {
-      if (!ex->d_req.ensure((size_t)(1 + 2 * (size_t)want) * 4)) return ex->sticky = FX_ERR_HIP;
+      if (!ex->d_req.ensure((size_t)(1 + 2 * (size_t)want) * 4)) return fail_sync(ex, FX_ERR_HIP);
       ex->req_cap = want;
     }
-    if (!ex->d_state.ensure(fx_partial_state_bytes(ex->nsrc, 1))) return ex->sticky = FX_ERR_HIP;
+    if (!ex->d_state.ensure(fx_partial_state_bytes(ex->nsrc, 1))) return fail_sync(ex, FX_ERR_HIP);
     uint32_t flags = FX_FLAG_SAVE_STATE;
     if (ex->processed == 0) flags |= FX_FLAG_INIT;
-    else if (hipMemsetAsync(ex->d_req.p, 0, 4, ex->stream)) return ex->sticky = FX_ERR_HIP;
+    else if (hipMemsetAsync(ex->d_req.p, 0, 4, ex->stream)) return fail_sync(ex, FX_ERR_HIP);
     int st = fx_batch_execute_partial(&in, &out, ex->d_state.p, ex->processed, N, flags, nullptr, ex->d_req.u32(),
                                       ex->req_cap, ex->stream);
-    if (st) return ex->sticky = st;
+    if (st) return fail_sync(ex, st);
     uint32_t nreq = 0;
     if (hipMemcpyAsync(&nexec, ex->d_nexec.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipMemcpyAsync(&err, ex->d_err.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipMemcpyAsync(&nreq, ex->d_req.p, 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipStreamSynchronize(ex->stream))
-      return ex->sticky = FX_ERR_HIP;
-    if (err) return ex->sticky = (int)err;
+      return fail_sync(ex, FX_ERR_HIP);
+    if (err) return fail_sync(ex, (int)err);
     std::vector<uint32_t> ring((size_t)2 * nreq);
     if (nreq && (hipMemcpyAsync(ring.data(), ex->d_req.u32() + 1, ring.size() * 4, hipMemcpyDeviceToHost,
                                 ex->stream) ||
                  hipStreamSynchronize(ex->stream)))
-      return ex->sticky = FX_ERR_HIP;
+      return fail_sync(ex, FX_ERR_HIP);
     ex->bytes_d2h += 4 + ring.size() * 4;
     // PendingIndex::index: a first-missing parent this shard does not
     // replicate is requested from its target shard (index.rs:187-197)
@@ -264,7 +272,7 @@ int flush(fx_graph_executor* ex) {
       const uint32_t m = ring[2 * k + 1];
       auto it = ex->dep_mask.find(m);
       const uint32_t mask = it == ex->dep_mask.end() ? 0u : it->second;
-      if (mask == 0) return ex->sticky = FX_ERR_UNSUPPORTED;  // "shards should be set if it's not a noop"
+      if (mask == 0) return fail_sync(ex, FX_ERR_UNSUPPORTED);  // "shards should be set if it's not a noop"
       if (!((mask >> ex->shard_id) & 1u))
         ex->requests.insert({(uint64_t)(FX_DOT_SRC(m) - 1) / ex->cfg.n, m});  // Dot::target_shard (id.rs:59-61)
     }
@@ -279,20 +287,20 @@ int flush(fx_graph_executor* ex) {
       ex->tier = FX_TIER_LDS_LARGE;
       ex->processed = 0;
     }
-    if (!ex->d_state.ensure(fx_batch_state_bytes(ex->tier, ex->nsrc, 1))) return ex->sticky = FX_ERR_HIP;
+    if (!ex->d_state.ensure(fx_batch_state_bytes(ex->tier, ex->nsrc, 1))) return fail_sync(ex, FX_ERR_HIP);
     uint32_t flags = FX_FLAG_SAVE_STATE;
     if (ex->processed == 0) flags |= FX_FLAG_INIT;
     if (ex->cfg.execute_at_commit) flags |= FX_FLAG_EXECUTE_AT_COMMIT;
     int st = fx_batch_execute(&in, &out, ex->tier, nullptr, 1, ex->d_state.p, ex->processed, N, flags,
                               nullptr, ex->stream);
-    if (st) return ex->sticky = st;
+    if (st) return fail_sync(ex, st);
     // nexec, err and the new entries straight into mapped host memory: one
     // synchronisation per flush
-    if (!ex->h_out.ensure((size_t)(2 + 2 * (size_t)ex->cap) * 4)) return ex->sticky = FX_ERR_HIP;
+    if (!ex->h_out.ensure((size_t)(2 + 2 * (size_t)ex->cap) * 4)) return fail_sync(ex, FX_ERR_HIP);
     if (fx::flush_pack(ex->d_order.u32(), ex->d_release.u32(), ex->d_nexec.u32(), ex->d_err.u32(), ex->cap,
                        ex->consumed, ex->h_out.du32(), ex->stream) ||
         hipStreamSynchronize(ex->stream))
-      return ex->sticky = FX_ERR_HIP;
+      return fail_sync(ex, FX_ERR_HIP);
     nexec = ex->h_out.u32()[0];
     err = ex->h_out.u32()[1];
     if (err == FX_ERR_CAPACITY && ex->tier != FX_TIER_WIDE_HBM) {
@@ -307,7 +315,7 @@ int flush(fx_graph_executor* ex) {
     }
     break;
   }
-  if (err) return ex->sticky = (int)err;
+  if (err) return fail_sync(ex, (int)err);
   ex->processed = N;
   if (nexec <= ex->consumed) return FX_OK;
   // the new order entries and the release steps they need: packed by the
@@ -330,18 +338,18 @@ int flush(fx_graph_executor* ex) {
     if (hipMemcpy2DAsync(rows.data(), 4 * 4, ex->d_order.u32() + fx_index(r0, 0, ex->cap), 256 * 4, 4 * 4,
                          (r1 - r0) / 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipStreamSynchronize(ex->stream))
-      return ex->sticky = FX_ERR_HIP;
+      return fail_sync(ex, FX_ERR_HIP);
     for (uint32_t k = k0; k < nexec; ++k) order[k - k0] = rows[k - r0];
   }
   // the release steps of exactly the commands converted below, gathered on
   // the device (bytes moved per flush are linear in its new order entries)
   if (ex->partial) {
-    if (!ex->d_gather.ensure((size_t)(nexec - k0) * 4)) return ex->sticky = FX_ERR_HIP;
+    if (!ex->d_gather.ensure((size_t)(nexec - k0) * 4)) return fail_sync(ex, FX_ERR_HIP);
     if (fx::gather_release(ex->d_order.u32(), ex->d_release.u32(), ex->cap, k0, nexec,
                            ex->d_gather.u32(), ex->stream) ||
         hipMemcpyAsync(rel.data(), ex->d_gather.p, rel.size() * 4, hipMemcpyDeviceToHost, ex->stream) ||
         hipStreamSynchronize(ex->stream))
-      return ex->sticky = FX_ERR_HIP;
+      return fail_sync(ex, FX_ERR_HIP);
     ex->bytes_d2h += (uint64_t)(order.size() + rel.size()) * 4;
   }
   // convert (fetch_commands_to_execute -> execute), collecting metrics
@@ -474,7 +482,10 @@ int fx_graph_executor_handle_add_sharded(fx_graph_executor* ex, fx_dot dot, fx_r
                                          uint64_t cmd_shards) {
   if (!ex || (ndeps && !dep_shards)) return FX_ERR_INVALID_ARG;
   if (!ex->partial) return FX_ERR_UNSUPPORTED;
-  if (cmd_shards && !((cmd_shards >> ex->shard_id) & 1u)) return FX_ERR_INVALID_ARG;  // a command of this shard
+  // cmd_shards: the command's shard set, 0 = unknown.  An Add of this shard's
+  // command includes shard_id; a RequestReply::Info carries a command this
+  // shard does not replicate (mod.rs:391-393: only shards outside cmd.shards()
+  // are sent one), so any non-empty set is accepted
   return append(ex, dot, rifl, keys, nkeys, read_only, deps, ndeps, now_ms, FX_KIND_ADD, dep_shards, cmd_shards);
 }
 

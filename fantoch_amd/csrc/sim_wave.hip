@@ -84,7 +84,9 @@ constexpr uint32_t PT_SEQ = 0, PT_FAST = 8, PT_SLOW = 16, PT_EXEC = 24, PT_OCC =
 // message kinds (numbering of the oracle's trace, sim_oracle.cpp MK)
 enum : uint32_t { M_COLLECT = 0, M_COLLECT_ACK = 1, M_COMMIT = 2, M_CONSENSUS = 3, M_CONSENSUS_ACK = 4,
                   M_COMMIT_DOT = 5, M_GC = 6, M_STABLE = 7,
-                  M_SUBMIT = 8 /* SubmitToProc (handle_submit_to_proc), not a message */ };
+                  // Basic (basic.rs:363-385; run-time geometry builds only)
+                  M_STORE = 8, M_STORE_ACK = 9, M_COMMIT_BASIC = 10,
+                  M_SUBMIT = 15 /* SubmitToProc (handle_submit_to_proc), not a message */ };
 enum : uint32_t { ST_START = 0, ST_PAYLOAD = 1, ST_COLLECT = 2, ST_COMMIT = 3 };
 enum : uint32_t { PH_IDLE = 0, PH_DFS = 1, PH_TRY = 2, PH_CHECK = 3 };
 
@@ -228,6 +230,7 @@ struct SimArgs {
   uint32_t delay_bins;
   unsigned long long* stats;
   uint32_t* err;
+  uint32_t* dot_client;  // [instances][n][exec_cap]: the client (1-based) that submitted dot (p, s)
 };
 
 // The kernel's arguments, read where a rarely taken path needs them through
@@ -710,6 +713,13 @@ struct Sim : GP {
     const uint32_t sl = slot_alloc();
     if (sl == NONE) { fail_cap(__LINE__); return; }
     const uint32_t idx = rl(ca, 32u + c) - 1u;
+    // the rifl of the dot (Result.rifls / monitors): dot (p, s) was
+    // submitted by client c + 1, whose k-th dot is its command k
+    const uint32_t inst = prm(P_INST);
+    if (lid == 0) {
+      KSimArgs* k = kargs();
+      if (k->dot_client && s <= k->exec_cap) k->dot_client[((size_t)inst * n + p) * k->exec_cap + s - 1u] = c + 1u;
+    }
     uint32_t nk = 0;
     const uint32_t keys = gen_keys(c + 1, idx, nk);
     // fresh slot
@@ -718,11 +728,82 @@ struct Sim : GP {
     put(S(sl, SL_CLIENT), c);
     put(S(sl, SL_IDX), idx);
     put(S(sl, SL_KEYS), keys);
+    if (!GP::fixed && protocol == FX_PROTOCOL_BASIC) {  // basic.rs:171-185: MStore to all
+      put(S(sl, SL_CNT), nk << 20);
+      act_send(M_STORE, dot, (1u << n) - 1u);
+      return;
+    }
     uint32_t depv = 0;
     const uint32_t nd = add_cmd(p, dot, keys, nk, 0, 0, depv);
     if (lid < nd) S(sl, SL_COLLECT + lid) = depv;
     put(S(sl, SL_CNT), (nd << 8) | (nk << 20));
     act_send(M_COLLECT, dot, (1u << n) - 1u);
+  }
+
+  // ------------------------------------------------------------- Basic
+  // basic.rs:187-211 handle_mstore: the command arrives; a member of the
+  // coordinator's quorum acks; a commit that arrived first is applied now
+  __device__ __forceinline__ void h_mstore(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_find(dot);
+    if (sl == NONE) { fail_late(__LINE__); return; }
+    const uint32_t ps = pst(sl, p);
+    set_pst(sl, p, (ps & ~7u) | ST_PAYLOAD);
+    const uint32_t src = (dot >> FX_SEQ_BITS) - 1u;
+    if ((rl(pq, src) >> p) & 1u) act_send(M_STORE_ACK, dot, 1u << from);
+    if (ps & 4u) h_bcommit(p, dot);  // buffered_mcommits.remove
+  }
+  // basic.rs:213-230 handle_mstoreack: f + 1 acks commit
+  __device__ __forceinline__ void h_mstoreack(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_find(dot);
+    if (sl == NONE) { fail_late(__LINE__); return; }
+    const uint32_t masks = uni(S(sl, SL_MASKS));
+    const uint32_t acks = (masks & 0xFFu) | (1u << from);
+    put(S(sl, SL_MASKS), (masks & ~0xFFu) | acks);
+    if (pop32(acks) == f + 1u) act_send(M_COMMIT_BASIC, dot, (1u << n) - 1u);
+  }
+  // basic.rs:232-257 handle_mcommit: BasicExecutor::handle runs one
+  // BasicExecutionInfo per key at once (executor/basic.rs:39-53): the dot is
+  // logged once per key (the oracle's execution log) and the key results go
+  // to AggregatePending; no ExecutionDelay / ChainSize samples
+  __device__ __forceinline__ void h_bcommit(uint32_t p, uint32_t dot) {
+    const uint32_t sl = slot_find(dot);
+    if (sl == NONE) { fail_late(__LINE__); return; }
+    const uint32_t ps = pst(sl, p);
+    if ((ps & 3u) == ST_START) {  // buffered_mcommits.insert
+      set_pst(sl, p, ps | 4u);
+      return;
+    }
+    set_pst(sl, p, (ps & ~7u) | ST_COMMIT);
+    const uint32_t c = uni(S(sl, SL_CLIENT));
+    const uint32_t nk = (uni(S(sl, SL_CNT)) >> 20) & 3u;
+    const uint32_t inst = prm(P_INST);
+    const uint32_t x0 = rl(pt, PT_EXEC + p);
+    if (lid == 0) {
+      KSimArgs* k = kargs();
+      for (uint32_t j = 0; j < nk; ++j)
+        if (x0 + j < k->exec_cap && k->executed) k->executed[((size_t)inst * n + p) * k->exec_cap + x0 + j] = dot;
+    }
+    lset(pt, PT_EXEC + p, x0 + nk);
+    if ((rl(ca, c) & 0xFFu) == p) {  // pending.wait_for registered this rifl at p
+      const uint32_t pend = rl(cb, 32u + c);
+      if (pend < nk) { fail_late(__LINE__); return; }
+      lset(cb, 32u + c, pend - nk);
+      if (pend == nk) {
+        const uint32_t fi = nfrm - 1;
+        const uint32_t w = rl(frw, fi);
+        const uint32_t nr = (w >> 20) & 31u;
+        if (nr >= g.rdm) { fail_cap(__LINE__); return; }
+        put(FRR(fi, nr), c);
+        lset(frw, fi, w + (1u << 20));
+      }
+    }
+    const uint32_t masks = uni(S(sl, SL_MASKS));
+    if (((masks >> 24) & 0xFFu) + 1u == n) {
+      slot_set(sl, 0u);  // executed everywhere: nothing about the dot is in flight
+    } else {
+      put(S(sl, SL_MASKS), masks + (1u << 24));
+    }
+    if (prm(P_GC)) h_mcommitdot(p, dot);  // Forward(MCommitDot) (basic.rs:246-251)
   }
 
   // atlas.rs:251-325 / epaxos.rs:223-301
@@ -1424,7 +1505,13 @@ struct Sim : GP {
           case M_COMMIT: h_mcommit(p, from, w2); break;
           case M_CONSENSUS: h_mconsensus(p, from, w2); break;
           case M_CONSENSUS_ACK: h_mconsensusack(p, from, w2); break;
-          default: err = FX_ERR_INVALID_ARG;
+          default:
+            if constexpr (!GP::fixed) {
+              if (kind == M_STORE) { h_mstore(p, from, w2); break; }
+              if (kind == M_STORE_ACK) { h_mstoreack(p, from, w2); break; }
+              if (kind == M_COMMIT_BASIC) { h_bcommit(p, w2); break; }
+            }
+            err = FX_ERR_INVALID_ARG;
         }
 #ifdef FX_SIM_PROFILE
         prof[8 + min(kind, 7u)] += __builtin_amdgcn_s_memtime() - prof_t0_;
@@ -1628,6 +1715,10 @@ __global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
     s.fq = n / 2 + s.f;
     s.wq = s.f + 1;
     s.synod_f = s.f;
+  } else if (!GP::fixed && s.protocol == FX_PROTOCOL_BASIC) {
+    s.fq = s.f + 1;  // basic_quorum_size (config.rs:285-287); no write quorum
+    s.wq = 0;
+    s.synod_f = 0;
   } else {
     const uint32_t fe = n / 2;
     s.fq = fe + (fe + 1) / 2;
@@ -1858,7 +1949,8 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
     const fx_sim_spec& s = b->host_specs[i];
     if (s.protocol != s0.protocol) one_p = false;
     if (s.f != s0.f) one_f = false;
-    if (s.protocol != FX_PROTOCOL_ATLAS && s.protocol != FX_PROTOCOL_EPAXOS) return FX_ERR_UNSUPPORTED;
+    if (s.protocol != FX_PROTOCOL_ATLAS && s.protocol != FX_PROTOCOL_EPAXOS && s.protocol != FX_PROTOCOL_BASIC)
+      return FX_ERR_UNSUPPORTED;
     if (s.n != s0.n || s.clients_per_region != s0.clients_per_region ||
         s.num_client_regions != s0.num_client_regions || s.keys_per_command != s0.keys_per_command ||
         s.pool_size != s0.pool_size)
@@ -1880,6 +1972,8 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   if (!large && (!sim_geometry(s0, ring, W, a.g) || (size_t)a.g.words * 4 > 160 * 1024 || a.g.ncli_keys > 0xFFFFu))
     large = true;
   if (large) {
+    // Basic runs on the all-on-chip kernel only (the runner's own KAT shape)
+    if (s0.protocol == FX_PROTOCOL_BASIC) return FX_ERR_UNSUPPORTED;
     if (s0.pool_size + s0.clients_per_region * s0.num_client_regions + 1 > 0xFFFFu) return FX_ERR_UNSUPPORTED;
     return simx_launch(b, o, (hipStream_t)hip_stream);
   }
@@ -1904,6 +1998,7 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   a.delay_bins = o->delay_bins ? o->delay_bins : 1;
   a.stats = (unsigned long long*)o->stats;
   a.err = o->err;
+  a.dot_client = o->dot_client;
   static bool configured = false;
   if (!configured) {
     (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);

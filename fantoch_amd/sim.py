@@ -216,12 +216,14 @@ class Result:
 
 def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bins=256,
         delay_bins=8192, ring_entries=0, dot_slots=0, max_events=0, flags=0, stream=None,
-        large=False, generic=False, tiered=True):
+        large=False, generic=False, tiered=True, before_launch=None):
     """Simulates every instance of `specs` on the GPU; returns a Result.
     large=True forces the large-instance kernel (FX_SIM_FLAG_LARGE);
     generic=True the run-time-geometry build of the all-on-chip kernel even
     for a compiled-in geometry (FX_SIM_FLAG_GENERIC); tiered=False: one
-    fx_sim_run, instances that outgrow the tables keep FX_ERR_SIM_CAPACITY."""
+    fx_sim_run, instances that outgrow the tables keep FX_ERR_SIM_CAPACITY.
+    before_launch(stream): called once the inputs and outputs are on the
+    device, right before the launch (diagnostics: tools/sim_poison.py)."""
     lib = _lib.load()
     planet = planet or Planet()
     N = len(specs)
@@ -258,6 +260,8 @@ def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bi
                        out["chain"].ptr, out["delay"].ptr, out["stats"].ptr, out["err"].ptr,
                        lat_bins, chain_bins, delay_bins, 0, out["dot_client"].ptr)
     reruns = ctypes.c_uint32()
+    if before_launch is not None:
+        before_launch(stream)
     if tiered:
         check(lib.fx_sim_run_tiered(ctypes.byref(b), ctypes.byref(o), stream, ctypes.byref(reruns)),
               "fx_sim_run_tiered")

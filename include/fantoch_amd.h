@@ -382,7 +382,9 @@ int fx_graph_executor_handle_add_sharded(fx_graph_executor* ex, fx_dot dot, fx_r
                                          const fx_dot* deps, const uint32_t* dep_shards, uint32_t ndeps,
                                          uint64_t now_ms, uint64_t cmd_shards);
 /* cmd_shards: the shards the command has ops on (Command::replicated_by,
- * command.rs:90-92) as a bitmask; 0 = this handle's shard only.  A Request for
+ * command.rs:90-92) as a bitmask; 0 = this handle's shard only.  An Info
+ * reply's command is one this shard does not replicate, so its set (the
+ * request_replies row's cmd_shards) is passed back as it is.  A Request for
  * a pending dot from a shard that replicates it is the reference's panic
  * (graph/mod.rs:308-316): FX_ERR_INVALID_ARG from handle_request / cleanup. */
 int fx_graph_executor_handle_executed(fx_graph_executor* ex, const fx_dot* dots, uint32_t n, uint64_t now_ms);

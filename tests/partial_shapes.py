@@ -77,8 +77,10 @@ def drive(hist, order, backend, reply_delay=6, seed=0):
     t = 0
 
     def add_cmd(dot):
-        _, _, deps = by_dot[dot]
-        backend.add(dot, [idx_dot[k] for k in deps], [hist[k][1] for k in deps], t)
+        # an own command and an Info reply (a command of other shards) both
+        # carry the command's shard set (Command::shards)
+        _, m, deps = by_dot[dot]
+        backend.add(dot, [idx_dot[k] for k in deps], [hist[k][1] for k in deps], t, cmd_shards=m)
 
     def step():
         log.append(backend.pull())
@@ -116,7 +118,7 @@ class OracleBackend:
         from oracle import oracle_lib
         self.g = oracle_lib.Graph(1 + shard * n, n, shard_id=shard, shard_count=shards)
 
-    def add(self, dot, deps, masks, t):
+    def add(self, dot, deps, masks, t, cmd_shards=0):
         self.g.handle_add_sharded(dot, deps, masks, t)
 
     def executed(self, dots, t):
@@ -135,8 +137,8 @@ class GpuBackend:
         from fantoch_amd.executor import GraphExecutor
         self.ex = GraphExecutor(1 + shard * n, shard, n, shard_count=shards, monitor=False)
 
-    def add(self, dot, deps, masks, t):
-        self.ex.handle_add_sharded(dot, dot, [0], deps, masks, t)
+    def add(self, dot, deps, masks, t, cmd_shards=0):
+        self.ex.handle_add_sharded(dot, dot, [0], deps, masks, t, cmd_shards=cmd_shards)
 
     def executed(self, dots, t):
         self.ex.handle_executed(dots, t)

@@ -94,3 +94,44 @@ def test_gpu_request_from_replicating_shard_is_an_error():
         c.handle_request(2, [(1, 1)])  # shard 2 replicates it
     assert e.value.status == _lib.FX_ERR_INVALID_ARG
     c.close()
+
+
+@pytest.mark.gpu
+def test_gpu_info_reply_feeds_back_into_requesting_shard():
+    """RequestReply::Info round trip (graph/mod.rs:390-393): shard 0's clone
+    answers shard 1's request for a pending command of shards {0, 2} with an
+    Info carrying that shard set; shard 1's executor takes it back through
+    handle_add_sharded with the set as it came (a command it does not
+    replicate) and executes it exactly as the oracle does."""
+    from fantoch_amd.executor import GraphExecutor
+    from oracle import oracle_lib
+    n = 2
+    ex0 = GraphExecutor(1, 0, n, shard_count=3, monitor=False)
+    # (1, 1), a command of shards {0, 2}, waits on (5, 1) of shard 2
+    ex0.handle_add_sharded((1, 1), (1, 1), [0], [(5, 1)], [0b100], 1, cmd_shards=0b101)
+    c = ex0.clone()
+    c.handle_request(1, [(1, 1)])
+    rep = c.replies(with_cmd_shards=True)
+    assert [(r[0], r[1], r[2], r[4]) for r in rep] == [(1, "info", (1, 1), 0b101)]
+    deps = rep[0][3]
+    # shard 1 (processes 3, 4): its own command (3, 1) depends on (1, 1)
+    ex1 = GraphExecutor(3, 1, n, shard_count=3, monitor=False)
+    o1 = oracle_lib.Graph(3, n, shard_id=1, shard_count=3)
+    steps = [("add", (3, 1), [(1, 1)], [0b101], 0b010),
+             ("add", (1, 1), [d for d, _ in deps], [m for _, m in deps], rep[0][4]),  # the Info
+             ("executed", (5, 1))]
+    lg, lo = [], []
+    for t, st in enumerate(steps, 1):
+        if st[0] == "add":
+            ex1.handle_add_sharded(st[1], st[1], [0], st[2], st[3], t, cmd_shards=st[4])
+            o1.handle_add_sharded(st[1], st[2], st[3], t)
+        else:
+            ex1.handle_executed([st[1]], t)
+            o1.executed_reply(st[1], t)
+        lg.append(([d for d, _ in ex1.drain_dots()], ex1.requests()))
+        lo.append(([d for d, _, _ in o1.drain()], o1.requests()))
+    assert lg == lo
+    assert (3, 1) in [d for step in lg for d in step[0]]
+    ex1.close()
+    c.close()
+    ex0.close()

@@ -195,3 +195,57 @@ def test_config2_bench_placements_full_size():
         specs = [S.spec(S.ATLAS, n, allp[g][1], list(allp[g][2]), list(allp[g][2]), commands_per_client=100,
                         conflict_rate=2, seed=20250213, instance=g) for g in ids]
         run_and_compare(specs)
+
+
+def basic_runner_specs(f, clients_per_process):
+    """sim/runner.rs:730-816 run(f, clients_per_process): Basic, n = 3 in
+    asia-east1 / us-central1 / us-west1, clients in us-west1 and us-west2,
+    100 % conflicts on a pool of 1, 1,000 commands per client, GC every 100 ms,
+    one extra simulated second."""
+    pl = planet()
+    return [S.spec(S.BASIC, 3, f, pl.ids(["asia-east1", "us-central1", "us-west1"]),
+                   pl.ids(["us-west1", "us-west2"]), clients_per_region=clients_per_process,
+                   commands_per_client=1000, conflict_rate=100, pool_size=1, gc_interval_ms=100,
+                   executed_notification_ms=50, extra_sim_time_ms=1000)]
+
+
+def region_hist(res, s, region):
+    """The client latency histogram of one region, from the GPU's latency log."""
+    lat = res.latencies(0)
+    regs = client_regions(s)
+    h = np.zeros(int(lat.max()) + 1, np.int64)
+    for c, r in enumerate(regs):
+        if r == region:
+            np.add.at(h, lat[c, :s.commands_per_client], 1)
+    return h
+
+
+def test_runner_basic_reference_means_on_gpu():
+    """The reference's only numeric simulator KAT (runner.rs:818-843,
+    runner_single_client_per_process) asserted on GPU output: us-west1 /
+    us-west2 mean latency 0 / 24 ms at f = 0 and 34 / 58 ms at f = 1, every
+    command stable at every process (runner.rs:800-812); bit-exact vs the
+    oracle besides."""
+    from test_sim_oracle import hist_mean
+    pl = planet()
+    w1, w2 = pl.index["us-west1"], pl.index["us-west2"]
+    for f, means in ((0, (0.0, 24.0)), (1, (34.0, 58.0))):
+        specs = basic_runner_specs(f, 1)
+        res, _ = run_and_compare(specs)
+        assert (hist_mean(region_hist(res, specs[0], w1)), hist_mean(region_hist(res, specs[0], w2))) == means
+        assert [int(x) for x in res.stable(0)] == [2000] * 3
+
+
+def test_runner_basic_multiple_clients_on_gpu():
+    """runner.rs:845-864 runner_multiple_clients_per_process on GPU output: 1 and
+    10 clients per region give the same mean and cov in both regions."""
+    from test_sim_oracle import hist_cov, hist_mean
+    pl = planet()
+    out = []
+    for cpp in (1, 10):
+        specs = basic_runner_specs(1, cpp)
+        res, _ = run_and_compare(specs)
+        assert [int(x) for x in res.stable(0)] == [2000 * cpp] * 3
+        out.append([region_hist(res, specs[0], pl.index[r]) for r in ("us-west1", "us-west2")])
+    for one, ten in zip(out[0], out[1]):
+        assert hist_mean(one) == hist_mean(ten) and hist_cov(one) == hist_cov(ten)

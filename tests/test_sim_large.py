@@ -144,8 +144,8 @@ def test_reference_protocol_simulations(name, protocol, n, f, ro, keys, nfr, slo
             assert int(res.slow(i).sum()) == 0
         else:
             assert int(res.slow(i).sum()) > 0
-    if name == "sim_epaxos_7_3_nfr":
-        assert int(res.slow_reads(0).sum()) == 0 and int(res.fast_reads(0).sum()) > 0
+        if nfr:  # assert_eq!(metrics.slow_paths_reads(), 0) (mod.rs:381, 492)
+            assert int(res.slow_reads(i).sum()) == 0 and int(res.fast_reads(i).sum()) > 0
 
 
 def test_small_shapes_equal_on_both_kernels():
@@ -166,6 +166,8 @@ def test_small_shapes_equal_on_both_kernels():
         for name in ("fast", "slow", "stable"):
             assert np.array_equal(getattr(a, name)(i), getattr(b, name)(i)), name
         assert a.trace(i) == b.trace(i) and a.end_ms(i) == b.end_ms(i) and a.events(i) == b.events(i)
+        # both kernels record every dot's rifl (dot_client): equal monitors
+        assert a.rifls(i) == b.rifls(i) and a.monitors(i) == b.monitors(i)
     assert np.array_equal(a.chain, b.chain) and np.array_equal(a.delay, b.delay)
     assert np.array_equal(a.latency_hist, b.latency_hist)
 

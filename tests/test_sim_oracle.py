@@ -284,6 +284,17 @@ def test_sim_atlas_5_2():  # protocol/mod.rs:355-365
     assert sim_test(ATLAS, 5, 2)["slow"].sum() > 0
 
 
+def test_sim_atlas_5_1():  # protocol/mod.rs:343-353 (the reference builds config!(3, 1) here)
+    assert sim_test(ATLAS, 3, 1, seed=4)["slow"].sum() == 0
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_sim_atlas_5_2_nfr(seed):  # protocol/mod.rs:367-383 (20 % single-key reads, NFR)
+    r = sim_test(ATLAS, 5, 2, read_only=20, keys=1, nfr=True, seed=seed)
+    assert r["slow"].sum() > 0
+    assert r["slow_reads"].sum() == 0 and r["fast_reads"].sum() > 0  # slow_paths_reads() == 0
+
+
 def test_sim_epaxos_3_1():  # protocol/mod.rs:454-464
     assert sim_test(EPAXOS, 3, 1)["slow"].sum() == 0
 
@@ -292,8 +303,11 @@ def test_sim_epaxos_5_2():  # protocol/mod.rs:466-476
     assert sim_test(EPAXOS, 5, 2)["slow"].sum() > 0
 
 
-def test_sim_epaxos_7_3_nfr():  # protocol/mod.rs:478-493 (100 % single-key reads, NFR)
-    assert sim_test(EPAXOS, 7, 3, read_only=100, keys=1, nfr=True)["slow"].sum() == 0
+@pytest.mark.parametrize("seed", [3, 4])
+def test_sim_epaxos_7_3_nfr(seed):  # protocol/mod.rs:478-493 (100 % single-key reads, NFR)
+    r = sim_test(EPAXOS, 7, 3, read_only=100, keys=1, nfr=True, seed=seed)
+    assert r["slow"].sum() == 0
+    assert r["slow_reads"].sum() == 0 and r["fast_reads"].sum() > 0  # slow_paths_reads() == 0
 
 
 def test_sim_is_deterministic_and_seeded():
