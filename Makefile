@@ -26,15 +26,17 @@ $(OBJDIR)/%.o: fantoch_amd/csrc/% $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
-# (k_sim under -amdgpu-sched-strategy=iterative-ilp ran configs[1] at 424.6 M
-# against 418.8 M, but its n = 7 build then failed test_region_subsets_n7 with
-# FX_ERR_SIM_LATE: not adopted.  max-ilp / min-reg / max-occupancy /
-# memory-clause: 418 - 423 M.)
-SIM_SCHED :=
+# k_sim under the iterative ILP scheduler: configs[1] 425.8 -> 430.0 M
+# (round 4, tools/sim_ab.sh).  Round 3 could not adopt it: its n = 7 build
+# stopped with FX_ERR_SIM_LATE, because prm()'s inline v_readlane lacked the
+# one wait state a VALU write of the same VGPR needs (sim_wave.hip prm, fixed
+# in round 4; tests/test_sim_poison.py's zero fill catches it deterministically).
+# max-ilp / min-reg / max-occupancy / memory-clause: 418 - 423 M (round 3).
+SIM_SCHED := -mllvm -amdgpu-sched-strategy=iterative-ilp
 # the large-instance simulator and the wide executor tiers under the iterative
 # ILP scheduler: configs[3] simulator 99.1 -> 103.1 M, dense executor 66.7 ->
 # 68.0 M (tools/mode_ab.sh), every GPU test passing
-$(OBJDIR)/sim_big.hip.o $(OBJDIR)/graph_wide.hip.o: HIPFLAGS += -mllvm -amdgpu-sched-strategy=iterative-ilp
+$(OBJDIR)/sim_big.hip.o $(OBJDIR)/graph_wide.hip.o $(OBJDIR)/sim_wave.hip.o: HIPFLAGS += -mllvm -amdgpu-sched-strategy=iterative-ilp
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
@@ -44,7 +46,7 @@ PROF_LIB := fantoch_amd/build_prof/libfantoch_amd.so
 prof: $(PROF_LIB)
 $(PROF_LIB): $(SRCS) $(HDRS)
 	@mkdir -p fantoch_amd/build_prof
-	$(HIPCC) $(HIPFLAGS) -DFX_SIM_PROFILE -shared -o $@ $(SRCS)
+	$(HIPCC) $(HIPFLAGS) $(SIM_SCHED) -DFX_SIM_PROFILE -shared -o $@ $(SRCS)
 
 # measurement-only variants of the library (A/B and ablations, FX_LIB=...):
 # make variant V=name D="-DFOO=1" rebuilds sim_wave.hip with the extra flags

@@ -63,10 +63,11 @@ constexpr uint32_t LDS_WORDS = HC_BINS + HD_BINS + 2 * HL_SLOTS;
 enum : uint32_t {
   M_COLLECT = 0, M_COLLECT_ACK = 1, M_COMMIT = 2, M_CONSENSUS = 3, M_CONSENSUS_ACK = 4,
   M_GC = 6,        // MGarbageCollection delivery (payload: the sender's committed frontier)
-  M_SUBMIT = 8,    // SubmitToProc
-  E_CLIENT = 9,    // SendToClient
-  E_TICK = 10,     // PeriodicProcessEvent (GarbageCollection)
-  E_NOTIF = 11     // PeriodicExecutedNotification
+  M_STORE = 8, M_STORE_ACK = 9, M_COMMIT_BASIC = 10,  // Basic (basic.rs:363-385)
+  M_SUBMIT = 12,   // SubmitToProc
+  E_CLIENT = 13,   // SendToClient
+  E_TICK = 14,     // PeriodicProcessEvent (GarbageCollection)
+  E_NOTIF = 15     // PeriodicExecutedNotification
 };
 enum : uint32_t { ST_START = 0, ST_PAYLOAD = 1, ST_COLLECT = 2, ST_COMMIT = 3 };
 // per-process record word R_PST: status (2) | buffered commit | accepted |
@@ -479,8 +480,9 @@ struct Big {
     uint32_t nk = 0;
     const uint32_t keys = gen_keys(c + 1, idx, nk);
     const bool ro = gen_read_only(c + 1, idx);
+    const bool basic = protocol == FX_PROTOCOL_BASIC;  // no deps (basic.rs:171-185)
     uint32_t depv = 0;
-    const uint32_t nd = add_cmd(p, dot, keys, nk, ro, 0, 0, depv);
+    const uint32_t nd = basic ? 0u : add_cmd(p, dot, keys, nk, ro, 0, 0, depv);
     // maybe_adjust_fast_quorum: a single-key read under NFR goes to a majority
     const uint32_t qw = rl(pq, p);
     const uint32_t qm = (nfr && ro && nk == 1) ? (qw >> 16) & 0xFFu : qw & 0xFFu;
@@ -500,7 +502,63 @@ struct Big {
     for (uint32_t i = lid; i < g.n * RW; i += 64) M[g.o_rec + sl * g.n * RW + i] = 0;
     if (A.dot_client && s <= A.exec_cap && lid == 0)
       A.dot_client[((size_t)inst * n + p) * A.exec_cap + s - 1u] = c + 1u;
-    act_send(M_COLLECT, dot, (1u << n) - 1u);
+    act_send(basic ? M_STORE : M_COLLECT, dot, (1u << n) - 1u);
+  }
+
+  // ------------------------------------------------------------- Basic
+  // basic.rs:187-211 handle_mstore: the command arrives; a member of the
+  // coordinator's quorum acks; a commit that arrived first is applied now
+  __device__ __forceinline__ void h_mstore(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (sl == NONE) {
+      err = FX_ERR_SIM_LATE;
+      return;
+    }
+    const uint32_t ps = rd(RC(sl, p, R_PST));
+    put(RC(sl, p, R_PST), (ps & ~(3u | PS_BUF)) | ST_PAYLOAD);
+    if ((rd(S(sl, SL_QUORUM)) >> p) & 1u) act_send(M_STORE_ACK, dot, 1u << from);
+    if (ps & PS_BUF) h_bcommit(p, dot);  // buffered_mcommits.remove
+  }
+  // basic.rs:213-230 handle_mstoreack: f + 1 acks commit
+  __device__ __forceinline__ void h_mstoreack(uint32_t p, uint32_t from, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (sl == NONE) {
+      err = FX_ERR_SIM_LATE;
+      return;
+    }
+    const uint32_t masks = rd(S(sl, SL_MASKS));
+    const uint32_t acks = (masks & 0xFFu) | (1u << from);
+    put(S(sl, SL_MASKS), (masks & ~0xFFu) | acks);
+    if (pop32(acks) == f + 1u) act_send(M_COMMIT_BASIC, dot, (1u << n) - 1u);
+  }
+  // basic.rs:232-257 handle_mcommit, and BasicExecutor::handle for each key at
+  // once (executor/basic.rs:39-53): the dot is logged once per key (the
+  // oracle's execution log), the key results go to AggregatePending; no
+  // ExecutionDelay / ChainSize samples
+  __device__ __forceinline__ void h_bcommit(uint32_t p, uint32_t dot) {
+    const uint32_t sl = slot_of(dot);
+    if (sl == NONE) {
+      err = FX_ERR_SIM_LATE;
+      return;
+    }
+    const uint32_t ps = rd(RC(sl, p, R_PST));
+    if ((ps & 3u) == ST_START) {  // buffered_mcommits.insert
+      put(RC(sl, p, R_PST), ps | PS_BUF);
+      return;
+    }
+    put(RC(sl, p, R_PST), (ps & ~3u) | ST_COMMIT);
+    const uint32_t c = rd(S(sl, SL_CLIENT));
+    const uint32_t nk = (rd(S(sl, SL_CNT)) >> 16) & 3u;
+    const uint32_t x0 = rl(pexec, p);
+    if (lid < nk && A.executed && x0 + lid < A.exec_cap)
+      A.executed[((size_t)inst * n + p) * A.exec_cap + x0 + lid] = dot;
+    lset(pexec, p, x0 + nk);
+    if ((rd(CL(c, 0)) & 0xFFu) == p) client_result(c, nk);  // pending.wait_for registered this rifl at p
+    if (err) return;
+    if (gc_ms) gc_commit(p, dot);  // Forward(MCommitDot) (basic.rs:246-251), before the slot can go
+    const uint32_t masks = rd(S(sl, SL_MASKS));
+    if (((masks >> 24) & 0xFFu) + 1u == n) put(S(sl, SL_DOT), 0u);  // executed everywhere: free the slot
+    else put(S(sl, SL_MASKS), masks + (1u << 24));
   }
 
   // atlas.rs:251-325 / epaxos.rs:223-301
@@ -1238,6 +1296,9 @@ struct Big {
           case M_COMMIT: h_mcommit(p, from, w2); break;
           case M_CONSENSUS: h_mconsensus(p, from, w2); break;
           case M_CONSENSUS_ACK: h_mconsensusack(p, from, w2); break;
+          case M_STORE: h_mstore(p, from, w2); break;
+          case M_STORE_ACK: h_mstoreack(p, from, w2); break;
+          case M_COMMIT_BASIC: h_bcommit(p, w2); break;
           default: err = FX_ERR_INVALID_ARG;
         }
         XPROF_ADD(PF_HANDLER);
@@ -1387,6 +1448,10 @@ __global__ __launch_bounds__(64, 3) void k_simx(ArgsX a) {
     fq = n / 2 + s.f;
     wq = s.f + 1;
     s.synod_f = s.f;
+  } else if (s.protocol == FX_PROTOCOL_BASIC) {
+    fq = s.f + 1;  // basic_quorum_size (config.rs:285-287); no write quorum
+    wq = 0;
+    s.synod_f = 0;
   } else {
     const uint32_t fe = n / 2;
     fq = fe + (fe + 1) / 2;

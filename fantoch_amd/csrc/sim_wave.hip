@@ -316,9 +316,21 @@ struct Sim : GP {
   // also right inside lane-divergent code
   __device__ __forceinline__ uint32_t prm(uint32_t k) const {
     uint32_t r;
-    // s_nop: the hazard recognizer does not see the asm's SGPR write (a VALU
-    // write read by a VMEM / lane-select operand needs wait states)
-    asm volatile("v_readlane_b32 %0, %1, %2\n\ts_nop 4" : "=s"(r) : "v"(pv), "i"(k));
+    // The hazard recognizer does not look inside inline asm, so the asm
+    // carries the wait states of both of its hazards itself:
+    //  * before: a VALU write of a VGPR followed by a v_readlane of it needs
+    //    one wait state on gfx940 / gfx950 (the compiler emits `s_nop 0`
+    //    between its own v_cndmask and v_readlane).  Without it the
+    //    readlane returns the VGPR's previous contents: under the iterative-
+    //    ILP schedule the compiler put the v_cndmask that builds pv directly
+    //    before prm(P_CMDS), the kernel read whatever an earlier kernel had
+    //    left in that register as the command count, a client never started
+    //    and the run ended in FX_ERR_SIM_LATE (round-3 open item, located in
+    //    round 4 by tools/sim_stale_repro.py: divergence at the first event;
+    //    vector-register poisoning hid it, scalar poisoning did not);
+    //  * after: the asm's SGPR write read by a VALU lane select / VMEM needs
+    //    wait states.
+    asm volatile("s_nop 1\n\tv_readlane_b32 %0, %1, %2\n\ts_nop 4" : "=s"(r) : "v"(pv), "i"(k));
     return r;
   }
   __device__ __forceinline__ uint64_t prm64(uint32_t k) const {
@@ -1972,8 +1984,6 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   if (!large && (!sim_geometry(s0, ring, W, a.g) || (size_t)a.g.words * 4 > 160 * 1024 || a.g.ncli_keys > 0xFFFFu))
     large = true;
   if (large) {
-    // Basic runs on the all-on-chip kernel only (the runner's own KAT shape)
-    if (s0.protocol == FX_PROTOCOL_BASIC) return FX_ERR_UNSUPPORTED;
     if (s0.pool_size + s0.clients_per_region * s0.num_client_regions + 1 > 0xFFFFu) return FX_ERR_UNSUPPORTED;
     return simx_launch(b, o, (hipStream_t)hip_stream);
   }

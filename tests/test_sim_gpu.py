@@ -231,7 +231,12 @@ def test_runner_basic_reference_means_on_gpu():
     w1, w2 = pl.index["us-west1"], pl.index["us-west2"]
     for f, means in ((0, (0.0, 24.0)), (1, (34.0, 58.0))):
         specs = basic_runner_specs(f, 1)
-        res, _ = run_and_compare(specs)
+        # f = 0: the us-west1 client's commands commit at its own process in
+        # 0 ms, so all 1,000 are issued at t = 0 and wait for the far
+        # replicas: ~1,000 live dots and ~4,000 messages in flight, the
+        # large-instance kernel's tables
+        kw = dict(large=True, ring_entries=8192, dot_slots=4096) if f == 0 else {}
+        res, _ = run_and_compare(specs, **kw)
         assert (hist_mean(region_hist(res, specs[0], w1)), hist_mean(region_hist(res, specs[0], w2))) == means
         assert [int(x) for x in res.stable(0)] == [2000] * 3
 

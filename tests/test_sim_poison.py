@@ -1,14 +1,20 @@
 """The all-on-chip simulator must not read register state it never wrote.
 
-Before every launch the register file of every SIMD is filled with tagged
-garbage (tests/poison/poison.hip: VGPR / AGPR r of lane l holds
-tag << 24 | r << 6 | l), so a read of a lane the kernel never defined returns
-that garbage instead of whatever an earlier kernel happened to leave there.
-The cases are the simulator parity cases of test_sim_gpu.py whose results once
-changed with the compiler's instruction schedule (test_region_subsets_n7,
-test_no_gc) plus the configs[0] / configs[1] shapes; each must stay bit-exact
-vs the oracle under two different tags.  Run it on another build of the library
-with FX_LIB=... (e.g. the iterative-ILP k_sim variant, `make variant`)."""
+Before every launch the register file of every SIMD is filled with known
+garbage (tests/poison/poison.hip): tagged values (VGPR / AGPR r of lane l
+holds tag << 24 | r << 6 | l) under two tags, and zeros.  A read of a register
+the kernel never wrote (or read too early: round 3's k_sim read the VGPR
+holding its parameters one wait state too soon, so it saw the register's
+previous contents) then returns that garbage instead of whatever an earlier
+kernel happened to leave there.  The big tagged values and the zeros push such
+a read to opposite sides of every count and bound: the round-3 failure read
+the per-client command count, which zero turns into "no commands" (a client
+never starts).  The cases are the simulator parity cases of test_sim_gpu.py
+whose results once changed with the compiler's instruction schedule
+(test_region_subsets_n7, test_no_gc) plus the configs[0] / configs[1] shapes;
+each must stay bit-exact vs the oracle under every fill.  Run it on another
+build of the library with FX_LIB=... (e.g. the iterative-ILP k_sim variant,
+`make variant`)."""
 import ctypes
 import itertools
 import os
@@ -24,7 +30,7 @@ from test_sim_gpu import assert_instance_parity, planet, to_oracle
 pytestmark = pytest.mark.gpu
 
 POISON = os.path.join(os.path.dirname(os.path.abspath(__file__)), "poison", "build", "libpoison.so")
-TAGS = (0x5A, 0xC3)
+FILLS = ((1, 0x5A), (1, 0xC3), (4, 0))  # (mode, tag): tagged vector registers twice, zeroed
 _LIB = None
 
 
@@ -32,15 +38,15 @@ def poison_lib():
     global _LIB
     if _LIB is None:
         _LIB = ctypes.CDLL(POISON)
-        _LIB.fx_dbg_poison.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+        _LIB.fx_dbg_poison_mode.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
     return _LIB
 
 
-def poisoner(tag):
+def poisoner(mode, tag):
     def before(stream):
         # 4,096 single-wave workgroups of 512 registers: every SIMD of the
         # 256 CUs runs at least one, so every register line is overwritten
-        assert poison_lib().fx_dbg_poison(tag, 4096, stream) == 0
+        assert poison_lib().fx_dbg_poison_mode(tag, 4096, mode, stream) == 0
     return before
 
 
@@ -93,8 +99,8 @@ def describe(res, specs, tag):
 def test_poisoned_registers_do_not_change_results(case, generic):
     specs = CASES[case]()
     orc = O.sim_batch([to_oracle(s) for s in specs], threads=8)
-    for tag in TAGS:
-        res = S.run(specs, planet(), generic=generic, before_launch=poisoner(tag))
+    for mode, tag in FILLS:
+        res = S.run(specs, planet(), generic=generic, before_launch=poisoner(mode, tag))
         bad = [(i, int(e)) for i, e in enumerate(res.err) if e]
         assert not bad, "tag %#x: %s" % (tag, describe(res, specs, tag))
         for i, (s, o) in enumerate(zip(specs, orc)):

@@ -25,6 +25,8 @@ ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--max-events", type=str, default="0", help="comma list of event bounds (0 = none)")
 ap.add_argument("--probes", type=str, default="n7_0,n7_2,n7_3,nogc_2")
 ap.add_argument("--bisect", type=int, default=0, help="bisect the first diverging event below this bound")
+ap.add_argument("--poison", type=str, default="", help="after the dirtying batch, poison registers: "
+                "comma list of mode:tag runs (mode 1 vector, 2 scalar, 3 both; tag 0-255)")
 args = ap.parse_args()
 
 pl = S.Planet()
@@ -40,6 +42,12 @@ for i in range(4):
     probes["nogc_%d" % i] = S.spec(S.EPAXOS, 5, 2, regs5, regs5, commands_per_client=80, conflict_rate=50,
                                    gc_interval_ms=0, seed=4, instance=i)
 names = args.probes.split(",")
+PLIB = None
+if args.poison:
+    import ctypes
+    PLIB = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "tests", "poison", "build", "libpoison.so"))
+    PLIB.fx_dbg_poison_mode.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
 
 
 def groups(name, me):
@@ -63,15 +71,20 @@ if args.bisect:
         print("%s: copies agree after %d events, differ after %d" % (name, lo, hi), flush=True)
         print("  at %d: %s" % (hi, groups(name, hi).most_common(3)), flush=True)
     sys.exit(0)
+runs = [(None, None)] + [tuple(int(v) for v in x.split(":")) for x in args.poison.split(",") if x]
 for me in [int(x) for x in args.max_events.split(",")]:
+  for mode, tag in runs:
     for rnd in range(args.rounds):
         for name in names:
             S.run(dirty, pl)
-            res = S.run([probes[name]] * args.copies, pl, max_events=me, tiered=False)
+            before = None
+            if mode is not None:
+                before = lambda st, m=mode, t=tag: PLIB.fx_dbg_poison_mode(t, 4096, m, st)
+            res = S.run([probes[name]] * args.copies, pl, max_events=me, tiered=False, before_launch=before)
             rows = [(int(res.err[i]), res.events(i), res.trace(i), res.end_ms(i),
                      int(res.stats[i, _lib.FX_SIM_STAT_ERR_SITE])) for i in range(args.copies)]
             cnt = Counter(rows)
             major, nmaj = cnt.most_common(1)[0]
             odd = sorted(((r, c) for r, c in cnt.items() if r != major), key=lambda x: -x[1])[:4]
-            print("max_events %d round %d %s: majority %s x%d; others %d %s" % (
+            print("poison %s:%s " % (mode, tag) + "max_events %d round %d %s: majority %s x%d; others %d %s" % (
                 me, rnd, name, major, nmaj, args.copies - nmaj, odd), flush=True)
