@@ -53,16 +53,18 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--seeds", type=int, default=4096)
-    ap.add_argument("--conflicts", type=str, default="0,2,10,50,100")
+    # --seeds / --conflicts / --protocol / --f: None = the mode's default
+    # (MODE_DEFAULTS); an explicit value is always honoured
+    ap.add_argument("--seeds", type=int, default=None)
+    ap.add_argument("--conflicts", type=str, default=None)
     ap.add_argument("--n", type=int, default=5)
     ap.add_argument("--cmds", type=int, default=None,
                     help="commands per client (sim default 1000, SURVEY.md §8(a) C2; "
                          "executor default 1000)")
-    ap.add_argument("--protocol", choices=["epaxos", "atlas", "both"], default="epaxos")
+    ap.add_argument("--protocol", choices=["epaxos", "atlas", "both"], default=None)
     ap.add_argument("--clients-per-region", type=int, default=None,
                     help="sim: clients per region (default 1; dense-sim 64)")
-    ap.add_argument("--f", type=int, default=2)
+    ap.add_argument("--f", type=int, default=None)
     ap.add_argument("--window", type=int, default=8)
     ap.add_argument("--cycle-pct", type=int, default=30)
     ap.add_argument("--seed", type=int, default=20250213)
@@ -84,7 +86,27 @@ def parse(argv=None):
     ap.add_argument("--placement-limit", type=int, default=None,
                     help="placements mode: run only the first K placements of the enumeration")
     ap.add_argument("--traffic-json", type=str, default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    for k, v in MODE_DEFAULTS.get(args.mode, MODE_DEFAULTS["sim"]).items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    import bench_pmc
+    args.pmc_key = bench_pmc.workload_key(args)  # before a mode fills in its own defaults
+    return args
+
+
+# per-mode defaults of the workload arguments (filled in only when the command
+# line leaves them unset, and reported in the bench line's config)
+MODE_DEFAULTS = {
+    "sim": dict(seeds=4096, conflicts="0,2,10,50,100", protocol="epaxos", f=2),
+    # BASELINE configs[3] on the simulator: one resident wavefront per
+    # instance, k_simx runs 3 waves per SIMD (164 VGPRs): 12 per CU x 256 CUs
+    # = 3,072 (4,096 adds a second, one-third-occupied round: 99 -> 72 M)
+    "dense-sim": dict(seeds=3072, conflicts="100", protocol="both", f=2),
+    # configs[3] on the batched executor: 768 instances = 3,840 streams, 5
+    # rounds of 768 workgroups (3 per CU)
+    "dense": dict(seeds=768, conflicts="100", protocol="epaxos", f=2),
+}
 
 
 def measured_copy_gbps(torch, dev, nbytes=2 << 30, reps=10):

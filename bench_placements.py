@@ -23,6 +23,8 @@ import json
 import os
 import time
 
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+
 import numpy as np
 
 from bench_sim import METRIC, _to_oracle
@@ -160,9 +162,24 @@ def main_placements(args):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    # each launch (one geometry: n = 7, then n = 5) timed by HIP events on the
+    # stream it runs on (fx_sim_run_tiered: the kernel, plus any capacity reruns)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in launches]
+    launch_ms = [[] for _ in launches]
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sweep()
+        lat_hist.zero_()
+        chain.zero_()
+        delay.zero_()
+        for i, L in enumerate(launches):
+            evs[i][0].record(stream)
+            _lib.check(lib.fx_sim_run_tiered(ctypes.byref(L["batch"]), ctypes.byref(L["out"]), hs, reruns),
+                       "fx_sim_run_tiered")
+            evs[i][1].record(stream)
+            L["reruns"] = int(reruns.value)
+        for i in range(len(launches)):
+            evs[i][1].synchronize()
+            launch_ms[i].append(evs[i][0].elapsed_time(evs[i][1]))
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -198,6 +215,34 @@ def main_placements(args):
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = _cpu_baseline(args, launches, cmds)
+    # roofline of rank 0's launches: SURVEY.md 8(d) bytes (32 + 4k + 8 d per
+    # executed command, d = mean deps of the executor Adds, from the kernel's
+    # per-instance counters) over the launches' own time (HIP events)
+    import bench_pmc
+    per = []
+    alg_total, ms_total = 0.0, 0.0
+    for i, L in enumerate(launches):
+        st = L["stats"].view(len(L["ids"]), _lib.FX_SIM_STATS)
+        ex = int(L["executed_len"].to(torch.int64).sum().item())
+        dsum = int(st[:, _lib.FX_SIM_STAT_DEPS].sum().item())
+        alg = 36.0 * ex + 8.0 * dsum
+        ms = sum(launch_ms[i]) / len(launch_ms[i])
+        per.append({"n": L["n"], "instances": len(L["ids"]), "kernel_ms_avg": round(ms, 3),
+                    "executed": ex, "alg_bytes": int(alg)})
+        alg_total += alg
+        ms_total += ms
+    roof = None
+    if per:
+        ach = alg_total / (ms_total * 1e-3) / 1e9
+        dom = max(per, key=lambda x: x["kernel_ms_avg"])
+        roof = {"bound": "hbm", "achieved": round(ach, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 6), "kernel": "k_sim (n = %d launch dominant)" % dom["n"],
+                "kernel_ms_avg": round(ms_total, 3), "per_launch": per, "alg_bytes_per_launch": int(alg_total),
+                "alg_bytes_definition": "SURVEY.md 8(d): 32 + 4k + 8d per executed command, k = 1",
+                "note": "the simulator is bound by scalar issue, not bytes (see issue)"}
+        bench_pmc.attach(roof, bench_pmc.load("placements", args), alg_total)
+        if roof.get("issue"):
+            roof["issue"].update(bound="salu-issue", frac=roof["issue"].get("salu_per_cu_cycle"))
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "cmds/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
@@ -213,6 +258,7 @@ def main_placements(args):
         "failed_placements": int((R[:, 8] != 0).sum()),
         "reruns_at_larger_tables_rank0": int(sum(L.get("reruns", 0) for L in launches)),
         "best_placement_by_mean_latency": best,
+        "roofline": roof,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

@@ -80,13 +80,22 @@ def main_pred(args):
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    # the dominant kernel: the SMALL tier's launch over every stream (HIP
+    # events on the stream it runs on); the capacity reruns beside it
+    lib.fx_profile_enable(1)
+    slot_ms = {t: [] for t in (_lib.FX_PRED_TIER_SMALL, _lib.FX_PRED_TIER_LDS, _lib.FX_PRED_TIER_HBM)}
     t0 = time.time()
     for _ in range(args.steps):
         step()
+        for t in slot_ms:
+            ms = ctypes.c_float()
+            if lib.fx_profile_slot_ms(_lib.FX_PROFILE_SLOT_PRED + t, ctypes.byref(ms)) == 0:
+                slot_ms[t].append(ms.value)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.time() - t0
+    lib.fx_profile_enable(0)
     executed = int(nexec.to(torch.int64).sum().item())
     nd_total = int(((hdr.to(torch.int64) >> 24) & 31).sum().item())
     n_adds = S * steps
@@ -98,10 +107,13 @@ def main_pred(args):
         if world > 1:
             dist.destroy_process_group()
         return None
+    import bench_pmc
     value = executed * world * args.steps / elapsed
     # §8(d) record bytes (k = 1) plus the 8-byte clock
     alg_bytes = 44.0 * n_adds + 8.0 * nd_total
-    achieved = alg_bytes / (elapsed / args.steps) / 1e9
+    kms = {t: (sum(v) / len(v) if v else None) for t, v in slot_ms.items()}
+    k_main = kms[_lib.FX_PRED_TIER_SMALL]
+    achieved = alg_bytes / ((k_main * 1e-3) if k_main else elapsed / args.steps) / 1e9
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = _cpu_baseline(args, S, steps, dmax, pw, dot, hdr, deps, clo, chi, order, release, nexec)
@@ -116,9 +128,15 @@ def main_pred(args):
                    "streams_per_gpu": S, "adds_per_stream": steps,
                    "parallelism": "one wavefront per stream; instances sharded over %d GPU(s)" % world},
         "executed_per_step": executed, "reruns": int(reruns.value),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": None, "kernel": "fx_pred_run (k_pred)",
-                     "alg_bytes_per_cmd": round(alg_bytes / n_adds, 3)},
+        "roofline": bench_pmc.attach(
+            {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+             "frac": round(achieved / HBM_PEAK_GBPS, 6), "kernel": "k_pred<false> (SMALL tier, every stream)",
+             "kernel_ms_avg": round(k_main, 3) if k_main else None,
+             "rerun_ms_avg": {"lds": round(kms[_lib.FX_PRED_TIER_LDS], 3) if kms[_lib.FX_PRED_TIER_LDS] else None,
+                              "hbm": round(kms[_lib.FX_PRED_TIER_HBM], 3) if kms[_lib.FX_PRED_TIER_HBM] else None},
+             "alg_bytes_per_cmd": round(alg_bytes / n_adds, 3), "alg_bytes_per_launch": int(alg_bytes),
+             "alg_bytes_definition": "SURVEY.md 8(d): 32 + 4k + 8d per command, k = 1, plus the 8-byte Caesar clock"},
+            bench_pmc.load("pred", args), alg_bytes),
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

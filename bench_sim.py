@@ -117,15 +117,7 @@ def main_sim(args):
     dense = args.mode == "dense-sim"
     if dense:  # BASELINE configs[3]
         args.clients_per_region = 64 if args.clients_per_region is None else args.clients_per_region
-        if args.conflicts == "0,2,10,50,100":
-            args.conflicts = "100"
-        if args.protocol == "epaxos" and args.f == 2:
-            args.protocol = "both"
-        if args.seeds == 4096:
-            # one resident wavefront per instance: k_simx runs 3 waves per SIMD
-            # (164 VGPRs), 12 per CU x 256 CUs = 3,072 (4,096 adds a second,
-            # one-third-occupied round: 99 -> 72 M cmds/s)
-            args.seeds = 3072
+        # (seeds, conflicts, protocol: bench.MODE_DEFAULTS["dense-sim"])
         if args.cmds is None:
             args.cmds = 50
     if args.clients_per_region is None:
@@ -281,6 +273,16 @@ def main_sim(args):
             # scalar unit's one per cycle (PMC passes of the same workload)
             roof["issue"] = dict(issue, bound="salu-issue", frac=issue.get("salu_per_cu_cycle"),
                                  source="profiles/sim_traffic_latest.json (rocprofv3 --pmc SQ_INSTS_*, GRBM_GUI_ACTIVE)")
+        # the per-mode counter record of this exact workload (tools/mode_pmc.sh), when there is one
+        import bench_pmc
+        pm = bench_pmc.load(args.mode, args)
+        if pm:
+            bench_pmc.attach(roof, pm, alg_bytes)
+            if dense:
+                roof["note"] = ("k_simx walks its per-instance HBM arena with dependent round trips: "
+                                "latency-bound, see issue.wait_any_frac_of_wave_cycles")
+            elif roof.get("issue"):
+                roof["issue"].update(bound="salu-issue", frac=roof["issue"].get("salu_per_cu_cycle"))
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_sim(args, specs, rates, executed, executed_len, st, lat_hist, n, exec_cap,
@@ -315,6 +317,8 @@ def main_sim(args):
                                "simulated instance" % world,
                 "kernel": kernel_name,
                 "arena_bytes_per_instance": int(arena.value) if large else 0,
+                "effective_args": {k: getattr(args, k) for k in ("seeds", "conflicts", "protocol", "f", "cmds",
+                                                                  "clients_per_region", "seed")},
             },
             "executed_per_step": int(executed_all),
             "client_cmds_per_s": round(client_all * args.steps / elapsed, 1),

@@ -56,6 +56,7 @@ FX_FLAG_SAVE_STATE = 4
 FX_TIER_WIDE, FX_TIER_WIDE_HBM = 7, 8
 FX_NUM_TIERS = 9
 FX_PRED_TIER_SMALL, FX_PRED_TIER_LDS, FX_PRED_TIER_HBM = 0, 1, 2
+FX_PROFILE_SLOT_PRED = 16
 FX_TIER_GROUP = 0
 FX_TIER_WAVE = 4
 FX_TIER_LANE_REG = 5
@@ -303,6 +304,7 @@ SIGNATURES = [
     ("fx_profile_enable", ctypes.c_int, [ctypes.c_int]),
     ("fx_profile_last_exec_ms", ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
     ("fx_profile_last_kernel_ms", ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_float)]),
+    ("fx_profile_slot_ms", ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_float)]),
     ("fx_status_string", ctypes.c_char_p, [ctypes.c_int]),
     ("fx_version", ctypes.c_char_p, []),
 ]

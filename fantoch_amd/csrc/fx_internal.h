@@ -83,6 +83,8 @@ constexpr uint32_t SPLIT_DEFAULT_THRESHOLD = 16;  // mean deps per Add x 8 at or
 // dominant kernel's duration is measured where it runs.
 bool profile_on();
 void split_profile_record(int which, bool end, hipStream_t s);
+// fx_profile_slot_ms: events around one kernel slot's launch (graph_exec.hip)
+void profile_slot_record(uint32_t slot, bool end, hipStream_t s);
 
 // Single-stream gather used by the executor handle: out[k - k0] =
 // release[rec(order[k])] for k in [k0, k1), so a flush reads back only the

@@ -996,6 +996,19 @@ static bool g_kev_valid[3] = {};
 
 bool profile_on() { return g_profile; }
 
+// per-slot kernel events (fx_profile_slot_ms): slot = executor tier
+// (fx_batch_execute), FX_PROFILE_SLOT_PRED + tier (fx_pred_execute); each
+// holds its slot's last launch
+static hipEvent_t g_sev[FX_PROFILE_SLOTS][2] = {};
+static bool g_sev_valid[FX_PROFILE_SLOTS] = {};
+void profile_slot_record(uint32_t slot, bool end, hipStream_t s) {
+  if (!g_profile || slot >= FX_PROFILE_SLOTS) return;
+  hipEvent_t& e = g_sev[slot][end ? 1 : 0];
+  if (!e && hipEventCreate(&e) != hipSuccess) return;
+  (void)hipEventRecord(e, s);
+  g_sev_valid[slot] = end;
+}
+
 void split_profile_record(int which, bool end, hipStream_t s) {
   if (!g_profile || which < 1 || which > 2) return;
   hipEvent_t& e = g_kev[which][end ? 1 : 0];
@@ -1125,6 +1138,7 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
     (void)hipEventRecord(g_ev0, hs);
     g_kev_valid[1] = g_kev_valid[2] = false;
   }
+  profile_slot_record(tier, false, hs);
   switch (tier) {
     case 0: st = launch_group(a, hs); break;
     case 1: st = launch_exec<Tier1>(a, hs); break;
@@ -1140,6 +1154,7 @@ int fx_batch_execute(const fx_stream_batch* in, const fx_order_batch* out, uint3
   if (g_profile) {
     (void)hipEventRecord(g_ev1, hs);
     g_ev_valid = st == FX_OK;
+    if (st == FX_OK) profile_slot_record(tier, true, hs);
   }
   return st;
 }
@@ -1186,7 +1201,15 @@ int fx_profile_enable(int on) {
   g_profile = on != 0;
   g_ev_valid = false;
   g_kev_valid[1] = g_kev_valid[2] = false;
+  for (uint32_t i = 0; i < FX_PROFILE_SLOTS; ++i) g_sev_valid[i] = false;
   return FX_OK;
+}
+
+int fx_profile_slot_ms(uint32_t slot, float* ms) {
+  if (!ms || slot >= FX_PROFILE_SLOTS) return FX_ERR_INVALID_ARG;
+  if (!g_sev_valid[slot]) return FX_ERR_INVALID_ARG;
+  if (hipEventSynchronize(g_sev[slot][1]) != hipSuccess) return FX_ERR_HIP;
+  return hipEventElapsedTime(ms, g_sev[slot][0], g_sev[slot][1]) == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 
 int fx_profile_last_kernel_ms(uint32_t which, float* ms) {

@@ -430,10 +430,11 @@ extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* ou
   a.ndeps = in->ndeps;
   const pred::Lay L = pred_layout(tier, in->base.n, in->base.dmax);
   hipStream_t hs = (hipStream_t)hip_stream;
+  if (!hbm && L.words == 0) return FX_ERR_UNSUPPORTED;
+  fx::profile_slot_record(FX_PROFILE_SLOT_PRED + tier, false, hs);
   if (hbm) {
     hipLaunchKernelGGL(pred::k_pred<true>, dim3(num_lanes), dim3(64), 0, hs, a, L);
   } else {
-    if (L.words == 0) return FX_ERR_UNSUPPORTED;
     static bool configured = false;
     if (!configured) {
       (void)hipFuncSetAttribute((const void*)pred::k_pred<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -442,7 +443,9 @@ extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* ou
     }
     hipLaunchKernelGGL(pred::k_pred<false>, dim3(num_lanes), dim3(64), (size_t)L.words * 4, hs, a, L);
   }
-  return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
+  if (hipGetLastError() != hipSuccess) return FX_ERR_HIP;
+  fx::profile_slot_record(FX_PROFILE_SLOT_PRED + tier, true, hs);
+  return FX_OK;
 }
 
 // Every stream at SMALL, then the ones that ran out of capacity at LDS, then

@@ -658,6 +658,14 @@ int fx_profile_last_exec_ms(float* ms);
  * lane kernel of FX_TIER_SPLIT (events recorded on each kernel's own stream);
  * FX_ERR_INVALID_ARG if that kernel did not run. */
 int fx_profile_last_kernel_ms(uint32_t which, float* ms);
+/* The last profiled launch of one kernel slot, timed by HIP events on the
+ * stream it ran on: slot = an executor tier (FX_TIER_*, fx_batch_execute and
+ * the tiered drivers' launches), FX_PROFILE_SLOT_PRED + FX_PRED_TIER_* (the
+ * predecessors executor); FX_ERR_INVALID_ARG if it did not run since
+ * fx_profile_enable(1). */
+#define FX_PROFILE_SLOT_PRED 16u
+#define FX_PROFILE_SLOTS 20u
+int fx_profile_slot_ms(uint32_t slot, float* ms);
 const char* fx_status_string(int status);
 const char* fx_version(void);
 
