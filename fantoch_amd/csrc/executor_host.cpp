@@ -12,7 +12,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -65,10 +67,10 @@ struct HostBuf {
     p = dp = nullptr;
     bytes = 0;
   }
-  bool ensure(size_t b) {
+  bool ensure(size_t b, bool coherent = false) {
     if (bytes >= b) return true;
     release();
-    if (hipHostMalloc(&p, b, hipHostMallocMapped) != hipSuccess) {
+    if (hipHostMalloc(&p, b, hipHostMallocMapped | (coherent ? hipHostMallocCoherent : 0u)) != hipSuccess) {
       p = nullptr;
       return false;
     }
@@ -155,6 +157,24 @@ struct fx_graph_executor {
   HostBuf h_out;              // nexec, err, (order word, release step) per new entry (device-written)
   uint64_t bytes_h2d = 0, bytes_d2h = 0;  // transfer accounting (fx_graph_executor_transfer_stats)
   int sticky = FX_OK;
+
+  // Persistent mode (flush_persist): one resident wavefront runs the wave
+  // tier's executor over Adds published in host-mapped memory, so draining
+  // after every Add costs no launch and no stream synchronisation.  Used from
+  // the first flush while every Add fits the wave tier (<= 14 deps, 64
+  // pending, 32-bit clock windows); any capacity error moves the handle to
+  // the batch tiers for good (the log reruns from its start there, as every
+  // tier escalation does).  FX_HANDLE_PERSIST=0 turns it off.
+  struct Persist {
+    bool active = false;    // the log is executed by the persistent kernel
+    bool launched = false;  // a launch is outstanding on `stream` (it may have exited when idle)
+    hipStream_t stream = nullptr;
+    HostBuf ctl, rows, out;
+    DevBuf state;
+    uint32_t pub = 0;  // rows published
+    static constexpr uint32_t ROWS = 4096, OUT = 8192;
+  } ps;
+  bool persist_ok = true;
 };
 
 namespace {
@@ -211,11 +231,140 @@ int fail_sync(fx_graph_executor* ex, int st) {
   return ex->sticky = st;
 }
 
+void convert(fx_graph_executor* ex, const std::vector<uint32_t>& order, const std::vector<uint32_t>& rel,
+             uint32_t nexec);
+
+volatile uint32_t* pctl(fx_graph_executor* ex) { return reinterpret_cast<volatile uint32_t*>(ex->ps.ctl.u32()); }
+
+// Stops the persistent kernel (its executor state lands in ps.state).
+int persist_stop(fx_graph_executor* ex) {
+  if (!ex->ps.launched) return FX_OK;
+  pctl(ex)[fx::PERSIST_EXIT] = 1u;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  const bool ok = hipStreamSynchronize(ex->ps.stream) == hipSuccess;
+  ex->ps.launched = false;
+  pctl(ex)[fx::PERSIST_EXIT] = 0u;
+  return ok ? FX_OK : FX_ERR_HIP;
+}
+
+int persist_launch_now(fx_graph_executor* ex, bool init) {
+  fx::PersistArgs a{};
+  a.ctl = ex->ps.ctl.du32();
+  a.rows = ex->ps.rows.du32();
+  a.out = ex->ps.out.du32();
+  a.state = ex->ps.state.u32();
+  a.row_slots = fx_graph_executor::Persist::ROWS;
+  a.out_slots = fx_graph_executor::Persist::OUT;
+  a.n = ex->nsrc;
+  a.at_commit = ex->cfg.execute_at_commit ? 1u : 0u;
+  a.init = init ? 1u : 0u;
+  a.done0 = pctl(ex)[fx::PERSIST_DONE];
+  pctl(ex)[fx::PERSIST_RUN] = 1u;  // the kernel clears it when it exits
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (fx::persist_launch(a, ex->ps.stream) != FX_OK) return FX_ERR_HIP;
+  ex->ps.launched = true;
+  return FX_OK;
+}
+
+// The persistent-mode flush: publish the new rows, wait for the kernel's done
+// word, take the new (order word, release step) pairs from the mapped ring.
+// Returns FX_ERR_CAPACITY when the log must move to the batch tiers.
+int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
+  const uint32_t N = (uint32_t)ex->dots.size();
+  for (uint32_t i = ex->ps.pub; i < N; ++i)
+    if (ex->deps[i].size() > fx::WAVE_MAX_DEPS) return FX_ERR_CAPACITY;
+  auto& P = ex->ps;
+  if (!P.active) {  // the first flush of the handle
+    if (ex->processed != 0) return FX_ERR_CAPACITY;
+    if (!P.stream && hipStreamCreateWithFlags(&P.stream, hipStreamNonBlocking) != hipSuccess) return FX_ERR_HIP;
+    if (!P.ctl.ensure(fx::PERSIST_CTL_WORDS * 4, true) ||
+        !P.rows.ensure((size_t)fx_graph_executor::Persist::ROWS * fx::PERSIST_ROW_WORDS * 4, true) ||
+        !P.out.ensure((size_t)fx_graph_executor::Persist::OUT * 8, true) ||
+        !P.state.ensure((size_t)fx::wave_state_words_per_stream() * 4))
+      return FX_ERR_HIP;
+    std::memset(P.ctl.p, 0, fx::PERSIST_CTL_WORDS * 4);
+    P.pub = 0;
+    P.active = true;
+    int st = persist_launch_now(ex, true);
+    if (st) return st;
+  }
+  uint32_t nexec = pctl(ex)[fx::PERSIST_NEXEC];
+  while (P.pub < N) {
+    // a chunk the rings hold: every published row and pair was consumed
+    const uint32_t hi = std::min<uint32_t>(N, P.pub + fx_graph_executor::Persist::ROWS - 128u);
+    uint32_t* rows = P.rows.u32();
+    for (uint32_t i = P.pub; i < hi; ++i) {
+      uint32_t* r = rows + (size_t)(i & (fx_graph_executor::Persist::ROWS - 1u)) * fx::PERSIST_ROW_WORDS;
+      r[0] = ex->dots[i];
+      r[1] = ex->hdrs[i];
+      const auto& dv = ex->deps[i];
+      for (uint32_t j = 0; j < fx::PERSIST_ROW_WORDS - 2u; ++j) r[2 + j] = j < dv.size() ? dv[j] : 0u;
+    }
+    ex->bytes_h2d += (uint64_t)(hi - P.pub) * fx::PERSIST_ROW_WORDS * 4;
+    std::atomic_thread_fence(std::memory_order_seq_cst);  // the rows before the doorbell
+    pctl(ex)[fx::PERSIST_PUB] = hi;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (!P.launched) {
+      int st = persist_launch_now(ex, false);
+      if (st) return st;
+    }
+    // wait for the done word; a kernel that exited when idle just before the
+    // doorbell (RUN cleared, done short of hi) is relaunched from its state
+    for (uint64_t spin = 0; pctl(ex)[fx::PERSIST_DONE] != hi; ++spin) {
+      if ((spin & 1023u) == 1023u && pctl(ex)[fx::PERSIST_RUN] == 0u && pctl(ex)[fx::PERSIST_DONE] != hi) {
+        if (hipStreamSynchronize(P.stream) != hipSuccess) return FX_ERR_HIP;
+        P.launched = false;
+        if (pctl(ex)[fx::PERSIST_DONE] == hi) break;
+        if (pctl(ex)[fx::PERSIST_ERR]) break;
+        int st = persist_launch_now(ex, false);
+        if (st) return st;
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    const uint32_t err = pctl(ex)[fx::PERSIST_ERR];
+    if (err) {
+      persist_stop(ex);
+      return err == FX_ERR_CAPACITY || err == FX_ERR_ORDER_OVERFLOW ? FX_ERR_CAPACITY : (int)err;
+    }
+    nexec = pctl(ex)[fx::PERSIST_NEXEC];
+    P.pub = hi;
+    // the new pairs, straight out of the mapped ring
+    if (nexec > ex->consumed) {
+      if (nexec - ex->consumed > fx_graph_executor::Persist::OUT) return FX_ERR_CAPACITY;
+      const uint32_t* q = P.out.u32();
+      std::vector<uint32_t> order(nexec - ex->consumed), rel(nexec - ex->consumed);
+      for (uint32_t k = ex->consumed; k < nexec; ++k) {
+        order[k - ex->consumed] = q[2 * (k & (fx_graph_executor::Persist::OUT - 1u))];
+        rel[k - ex->consumed] = q[2 * (k & (fx_graph_executor::Persist::OUT - 1u)) + 1];
+      }
+      ex->bytes_d2h += 12 + (uint64_t)(nexec - ex->consumed) * 8;
+      convert(ex, order, rel, nexec);
+    }
+  }
+  ex->processed = N;
+  nexec_out = nexec;
+  return FX_OK;
+}
+
 // Runs the steps not yet executed; converts new order entries.
 int flush(fx_graph_executor* ex) {
   if (ex->sticky) return ex->sticky;
   const uint32_t N = (uint32_t)ex->dots.size();
   if (ex->processed >= N) return FX_OK;
+  if (!ex->partial && ex->persist_ok && (ex->ps.active || ex->processed == 0)) {
+    uint32_t nexec = 0;
+    const int st = flush_persist(ex, nexec);
+    if (st == FX_OK) return FX_OK;
+    if (st != FX_ERR_CAPACITY) return ex->sticky = st;
+    // to the batch tiers, from the start of the log (the consumed prefix of
+    // the deterministic order is skipped there)
+    persist_stop(ex);
+    ex->persist_ok = false;
+    ex->ps.active = false;
+    ex->tier = FX_TIER_GLOBAL;
+    ex->processed = 0;
+    ex->uploaded = 0;
+  }
   uint32_t need_dmax = ex->dmax;
   for (uint32_t i = ex->uploaded; i < N; ++i) need_dmax = std::max<uint32_t>(need_dmax, (uint32_t)ex->deps[i].size());
   if (N > ex->cap || need_dmax > ex->dmax) {
@@ -352,7 +501,14 @@ int flush(fx_graph_executor* ex) {
       return fail_sync(ex, FX_ERR_HIP);
     ex->bytes_d2h += (uint64_t)(order.size() + rel.size()) * 4;
   }
-  // convert (fetch_commands_to_execute -> execute), collecting metrics
+  convert(ex, order, rel, nexec);
+  return FX_OK;
+}
+
+// fetch_commands_to_execute -> execute for the new order entries
+// [consumed, nexec) and their release steps, collecting the metrics
+void convert(fx_graph_executor* ex, const std::vector<uint32_t>& order, const std::vector<uint32_t>& rel,
+             uint32_t nexec) {
   for (size_t x = 0; x < order.size(); ++x) {
     const uint32_t o = order[x];
     const uint32_t rec = FX_ORDER_REC(o);
@@ -379,7 +535,6 @@ int flush(fx_graph_executor* ex) {
     }
   }
   ex->consumed = nexec;
-  return FX_OK;
 }
 
 int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys, uint32_t nkeys,
@@ -432,6 +587,24 @@ int append(fx_graph_executor* ex, fx_dot dot, fx_rifl rifl, const uint32_t* keys
   return FX_OK;
 }
 
+int pending_out(fx_graph_executor* ex, const std::vector<uint32_t>& d, const std::vector<uint32_t>& w, uint32_t c,
+                fx_dot* dots, fx_dot* waiting_on, uint32_t cap, uint32_t* n_out) {
+  std::vector<std::pair<uint32_t, uint32_t>> pw;
+  for (uint32_t i = 0; i < c && i < d.size(); ++i) pw.emplace_back(d[i], w[i]);
+  std::sort(pw.begin(), pw.end());
+  uint32_t m = 0;
+  for (const auto& e : pw) {
+    if (m < cap) {
+      const uint32_t s0 = FX_DOT_SRC(e.first), s1 = FX_DOT_SRC(e.second);
+      dots[m] = fx_dot{s0, FX_DOT_SEQ(e.first) + ex->base[s0 - 1]};
+      waiting_on[m] = fx_dot{s1, FX_DOT_SEQ(e.second) + (s1 >= 1 && s1 <= ex->nsrc ? ex->base[s1 - 1] : 0)};
+    }
+    ++m;
+  }
+  *n_out = m;
+  return FX_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -449,6 +622,8 @@ fx_graph_executor* fx_graph_executor_new(uint8_t process_id, uint64_t shard_id, 
   ex->nsrc = config->n * config->shard_count;
   ex->partial = config->shard_count > 1;
   if (ex->partial) ex->tier = FX_TIER_WIDE_HBM;
+  const char* pe = std::getenv("FX_HANDLE_PERSIST");
+  ex->persist_ok = !(pe && pe[0] == '0');
   if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ex;
     return nullptr;
@@ -458,6 +633,8 @@ fx_graph_executor* fx_graph_executor_new(uint8_t process_id, uint64_t shard_id, 
 
 void fx_graph_executor_free(fx_graph_executor* ex) {
   if (!ex) return;
+  persist_stop(ex);
+  if (ex->ps.stream) (void)hipStreamDestroy(ex->ps.stream);
   hipStream_t s = ex->stream;
   delete ex;  // DevBufs free first
   if (s) (void)hipStreamDestroy(s);
@@ -735,6 +912,15 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
   if (st) return st;
   *n_out = 0;
   if (ex->processed == 0) return FX_OK;
+  if (ex->ps.active) {  // the persistent kernel's state, saved when it stops
+    if (persist_stop(ex)) return FX_ERR_HIP;
+    std::vector<uint32_t> block(fx::wave_state_words_per_stream());
+    if (hipMemcpy(block.data(), ex->ps.state.p, block.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+      return FX_ERR_HIP;
+    std::vector<uint32_t> d(64), w(64);
+    const uint32_t c = fx::decode_pending(FX_TIER_WAVE, block.data(), 0, d.data(), w.data(), 64);
+    return pending_out(ex, d, w, c, dots, waiting_on, cap, n_out);
+  }
   std::vector<uint32_t> block((ex->partial ? fx_partial_state_bytes(ex->nsrc, 1)
                                            : fx_batch_state_bytes(ex->tier, ex->nsrc, 1)) / 4);
   if (hipMemcpyAsync(block.data(), ex->d_state.p, block.size() * 4, hipMemcpyDeviceToHost, ex->stream) ||
@@ -745,21 +931,9 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
   const uint32_t c = ex->tier == FX_TIER_WIDE_HBM
                          ? fx::wide_decode_pending(block.data(), ex->nsrc, d.data(), w.data(), slots, ex->partial)
                          : fx::decode_pending(ex->tier, block.data(), 0, d.data(), w.data(), slots);
-  std::vector<std::pair<uint32_t, uint32_t>> pw;
-  for (uint32_t i = 0; i < c && i < slots; ++i) pw.emplace_back(d[i], w[i]);
-  std::sort(pw.begin(), pw.end());
-  uint32_t m = 0;
-  for (const auto& e : pw) {
-    if (m < cap) {
-      const uint32_t s0 = FX_DOT_SRC(e.first), s1 = FX_DOT_SRC(e.second);
-      dots[m] = fx_dot{s0, FX_DOT_SEQ(e.first) + ex->base[s0 - 1]};
-      waiting_on[m] = fx_dot{s1, FX_DOT_SEQ(e.second) + (s1 >= 1 && s1 <= ex->nsrc ? ex->base[s1 - 1] : 0)};
-    }
-    ++m;
-  }
-  *n_out = m;
-  return FX_OK;
+  return pending_out(ex, d, w, c, dots, waiting_on, cap, n_out);
 }
+
 
 int fx_graph_executor_parallel(void) { return 1; }
 

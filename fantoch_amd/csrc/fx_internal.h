@@ -83,6 +83,20 @@ constexpr uint32_t SPLIT_DEFAULT_THRESHOLD = 16;  // mean deps per Add x 8 at or
 // dominant kernel's duration is measured where it runs.
 bool profile_on();
 void split_profile_record(int which, bool end, hipStream_t s);
+// the drop-in handle's persistent executor kernel (graph_wave.hip, persist::)
+struct PersistArgs {
+  uint32_t* ctl;        // host-mapped control words (persist::P_*)
+  const uint32_t* rows; // host-mapped ring of published rows (persist::PRW words each)
+  uint32_t* out;        // host-mapped ring of (order word, release step) pairs
+  uint32_t* state;      // device: the wave tier's saved state of one stream
+  uint32_t row_slots, out_slots;  // powers of two
+  uint32_t n, at_commit, init, done0;
+};
+constexpr uint32_t PERSIST_ROW_WORDS = 16;  // dot, hdr, 14 deps
+constexpr uint32_t PERSIST_CTL_WORDS = 16;
+enum : uint32_t { PERSIST_PUB = 0, PERSIST_EXIT = 1, PERSIST_DONE = 2, PERSIST_NEXEC = 3, PERSIST_ERR = 4,
+                  PERSIST_RUN = 5 };
+int persist_launch(const PersistArgs& a, hipStream_t stream);
 // fx_profile_slot_ms: events around one kernel slot's launch (graph_exec.hip)
 void profile_slot_record(uint32_t slot, bool end, hipStream_t s);
 

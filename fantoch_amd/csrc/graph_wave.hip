@@ -71,6 +71,21 @@ __device__ __forceinline__ uint64_t bal(bool p) { return (uint64_t)__ballot(p); 
 __device__ __forceinline__ uint32_t ctz64(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
 __device__ __forceinline__ uint32_t pop64(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
 
+// Where an executed command goes.  PlaneOut: the batch tiers' order plane
+// (row k = the k-th executed command) and release plane (row rec = the step
+// that executed arrival rec).  The persistent handle kernel (handle_persist.hip)
+// writes the same (order word, release step) pairs into a host-mapped ring.
+struct PlaneOut {
+  uint32_t* order = nullptr;
+  uint32_t* release = nullptr;
+  uint32_t stream = 0, steps = 0;
+  __device__ __forceinline__ void put(uint32_t k, uint32_t word, uint32_t rec, uint32_t cur) const {
+    order[fx_index(k, stream, steps)] = word;
+    release[fx_index(rec, stream, steps)] = cur;
+  }
+};
+
+template <class Out>
 struct Wave {
   uint32_t lid;
   uint64_t lbit;  // 1 << lid
@@ -82,11 +97,10 @@ struct Wave {
   uint32_t k = 0, err = 0, epoch = 1, nwl = 0, cur = 0;
   uint32_t phase = PH_IDLE, root = 0, idc = 0, nfr = 0, missing = 0;
   uint32_t fv = 0, fdi = 0, fnc = 0, in_try = 0, emitted = 0;
-  // stream context
-  uint32_t stream = 0, n = 0, steps = 0;
+  // stream context; kcap: order entries the output holds
+  uint32_t stream = 0, n = 0, steps = 0, kcap = 0;
   uint32_t* lds = nullptr;
-  uint32_t* order = nullptr;
-  uint32_t* release = nullptr;
+  Out out;
 
   __device__ __forceinline__ size_t at(uint32_t step) const { return fx_index(step, stream, steps); }
   __device__ __forceinline__ bool mine(uint64_t m) const { return (m & lbit) != 0; }
@@ -170,11 +184,8 @@ struct Wave {
 
   // save_scc (mod.rs:488-523) for a singleton: to_execute + executed clock
   __device__ __forceinline__ void emit_one(uint32_t rec, uint32_t d) {
-    if (k >= steps) { err = FX_ERR_ORDER_OVERFLOW; return; }
-    if (lid == 0) {
-      order[at(k)] = rec | FX_ORDER_SCC_START;
-      release[at(rec)] = cur;
-    }
+    if (k >= kcap) { err = FX_ERR_ORDER_OVERFLOW; return; }
+    if (lid == 0) out.put(k, rec | FX_ORDER_SCC_START, rec, cur);
     ++k;
     clk_add(d);
   }
@@ -201,15 +212,14 @@ struct Wave {
     const bool mem = mine(occ) && tid(stl) >= idv;
     const uint64_t mm = bal(mem);
     const uint32_t cnt = pop64(mm);
-    if (k + cnt > steps) { err = FX_ERR_ORDER_OVERFLOW; return; }
+    if (cnt > kcap - k) { err = FX_ERR_ORDER_OVERFLOW; return; }
     if (nwl + cnt > WLC) { err = FX_ERR_CAPACITY; return; }
     uint32_t rank = 0;
     if (cnt == 1) {
       const uint32_t d = rl(sdot, fv);
       if (lid == 0) {
         const uint32_t rec = rl(srec, fv) & 0x03FFFFFFu;
-        order[at(k)] = rec | FX_ORDER_SCC_START;
-        release[at(rec)] = cur;
+        out.put(k, rec | FX_ORDER_SCC_START, rec, cur);
         wl(nwl) = d;
       }
       ++k;
@@ -219,8 +229,7 @@ struct Wave {
       for (uint64_t m = mm; m; m &= m - 1) rank += rl(sdot, ctz64(m)) < sdot ? 1u : 0u;
       if (mem) {
         const uint32_t rec = srec & 0x03FFFFFFu;
-        order[at(k + rank)] = rec | (rank == 0 ? FX_ORDER_SCC_START : 0u);
-        release[at(rec)] = cur;
+        out.put(k + rank, rec | (rank == 0 ? FX_ORDER_SCC_START : 0u), rec, cur);
         wl(nwl + rank) = sdot;
       }
       k += cnt;
@@ -341,10 +350,8 @@ struct Wave {
     if (nd > dmax || nd > MAXD) { err = FX_ERR_INVALID_ARG; return; }
     if ((d >> FX_SEQ_BITS) - 1u >= n || (d & FX_SEQ_MASK) == 0) { err = FX_ERR_DOT_RANGE; return; }
     if (at_commit) {  // execute_at_commit bypass (executor.rs:72-73)
-      if (lid == 0) {
-        order[at(k)] = i | FX_ORDER_SCC_START;
-        release[at(i)] = i;
-      }
+      if (k >= kcap) { err = FX_ERR_ORDER_OVERFLOW; return; }
+      if (lid == 0) out.put(k, i | FX_ORDER_SCC_START, i, i);
       ++k;
       return;
     }
@@ -400,15 +407,18 @@ __global__ __launch_bounds__(64 * WPB) void k_graph_wave(KArgs a) {
   const uint32_t len = a.lengths ? min(uni(a.lengths[s]), a.steps) : a.steps;
   uint32_t* gst = a.state ? a.state + (size_t)gg * WPS : nullptr;
 
-  Wave e;
+  Wave<PlaneOut> e;
   e.lid = lane;
   e.lbit = 1ull << lane;
   e.stream = s;
   e.n = a.n;
   e.steps = a.steps;
+  e.kcap = a.steps;
   e.lds = smem + w * LW;
-  e.order = a.order;
-  e.release = a.release;
+  e.out.order = a.order;
+  e.out.release = a.release;
+  e.out.stream = s;
+  e.out.steps = a.steps;
 
   if (a.flags & FX_FLAG_INIT) {
     if (a.init_frontier && lane < 8) e.cf = a.init_frontier[(size_t)s * 8 + lane];
@@ -493,7 +503,145 @@ __global__ __launch_bounds__(64 * WPB) void k_graph_wave(KArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The persistent single-executor kernel of the drop-in handle (executor_host.cpp,
+// "persistent mode").  The reference's simulator calls the executor once per
+// Add and drains it right after (fantoch/src/sim/runner.rs:406-424); a launch
+// plus a synchronisation per Add costs tens of microseconds, so instead ONE
+// wavefront stays resident and runs the wave tier's executor (the Wave above)
+// over Adds the host publishes in host-mapped memory:
+//   ctl[P_PUB]   rows published by the host (release store after the rows)
+//   ctl[P_EXIT]  host asks the kernel to stop
+//   ctl[P_DONE]  rows processed (the kernel's release store, after the outputs)
+//   ctl[P_NEXEC] / ctl[P_ERR]  executed count and status after those rows
+//   ctl[P_RUN]   1 while the kernel is resident
+// rows: a ring of PR rows of PRW words (dot, hdr, up to 14 deps), row i in slot
+// i mod PR; out: a ring of PO (order word, release step) pairs, pair k in slot
+// k mod PO.  The kernel polls; with nothing published for 0.25 s (or on an
+// error, or when asked) it saves the executor state in the wave tier's state
+// layout and exits, and the host relaunches it on the next flush, so no
+// kernel outlives an idle or vanished host (a device-wide synchronisation
+// waits for it at most that long).
+namespace persist {
+enum : uint32_t { P_PUB = 0, P_EXIT = 1, P_DONE = 2, P_NEXEC = 3, P_ERR = 4, P_RUN = 5, P_WORDS = 16 };
+constexpr uint32_t PRW = 16;                     // words per published row
+constexpr uint64_t IDLE_TICKS = 25000000ull;     // s_memrealtime runs at 100 MHz: 0.25 s
+
+struct RingOut {
+  uint32_t* ring = nullptr;  // host-mapped pairs
+  uint32_t mask = 0;         // PO - 1
+  __device__ __forceinline__ void put(uint32_t k, uint32_t word, uint32_t rec, uint32_t cur) const {
+    uint32_t* q = ring + 2u * (k & mask);
+    q[0] = word;
+    q[1] = cur;
+  }
+};
+
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t smem[LW];
+  const uint32_t lane = threadIdx.x;
+  Wave<RingOut> e;
+  e.lid = lane;
+  e.lbit = 1ull << lane;
+  e.stream = 0;
+  e.n = a.n;
+  e.steps = 0xFFFFFFFFu;
+  e.kcap = 0xFFFFFFFFu;
+  e.lds = smem;
+  e.out.ring = a.out;
+  e.out.mask = a.out_slots - 1u;
+  uint32_t* gst = a.state;
+  if (a.init) {
+    for (uint32_t q = lane; q < L_IN; q += 64) e.lds[q] = 0;
+  } else {  // the layout k_graph_wave saves
+    const uint32_t* r = gst + lane * RREGS;
+    e.sdot = r[0];
+    e.srec = r[1];
+    e.swait = r[2];
+    e.stl = r[3];
+    e.sfr = r[4];
+    e.cf = r[5];
+    e.cw = r[6];
+    for (uint32_t q = lane; q < L_IN; q += 64) e.lds[q] = gst[S_LDS + q];
+    e.occ = (uint64_t)uni(gst[S_SCAL + 0]) | ((uint64_t)uni(gst[S_SCAL + 1]) << 32);
+    e.wmask = (uint64_t)uni(gst[S_SCAL + 2]) | ((uint64_t)uni(gst[S_SCAL + 3]) << 32);
+    e.k = uni(gst[S_SCAL + 4]);
+    e.err = uni(gst[S_SCAL + 5]);
+    e.epoch = uni(gst[S_SCAL + 6]);
+  }
+  uint32_t* ctl = a.ctl;
+  if (lane == 0) st_sys(ctl + P_RUN, 1u);
+  uint32_t done = a.done0;
+  uint64_t idle0 = __builtin_amdgcn_s_memrealtime();
+  while (!e.err) {
+    const uint32_t pub = uni(ld_sys(ctl + P_PUB));
+    if (uni(ld_sys(ctl + P_EXIT))) break;
+    if (pub == done) {
+      if (__builtin_amdgcn_s_memrealtime() - idle0 > IDLE_TICKS) break;
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    // rows [done, pub), four per load: lane 16 r + w reads word w of row i + r
+    for (uint32_t i = done; i < pub && !e.err; i += 4) {
+      const uint32_t r4 = lane >> 4, w = lane & 15u;
+      const uint32_t row = i + r4;
+      const uint32_t v = row < pub ? a.rows[(size_t)(row & (a.row_slots - 1u)) * PRW + w] : 0u;
+      for (uint32_t r = 0; r < 4 && i + r < pub && !e.err; ++r) {
+        const uint32_t d = rl(v, 16u * r), h = rl(v, 16u * r + 1u);
+        const uint32_t depj = gather(v, (16u * r + 2u + lane) & 63u);
+        e.step_start(i + r, d, h, lane < MAXD ? depj : 0u, MAXD, a.at_commit != 0);
+        if (e.phase != PH_IDLE) e.run_slow();
+      }
+    }
+    // outputs first, then the counters, then the done word (release)
+    __threadfence_system();
+    if (lane == 0) {
+      st_sys(ctl + P_NEXEC, e.k);
+      st_sys(ctl + P_ERR, e.err);
+      st_sys(ctl + P_DONE, pub);
+    }
+    done = pub;
+    idle0 = __builtin_amdgcn_s_memrealtime();
+  }
+  uint32_t* r = gst + lane * RREGS;
+  r[0] = e.sdot;
+  r[1] = e.srec;
+  r[2] = e.swait;
+  r[3] = e.stl;
+  r[4] = e.sfr;
+  r[5] = e.cf;
+  r[6] = e.cw;
+  for (uint32_t q = lane; q < L_IN; q += 64) gst[S_LDS + q] = e.lds[q];
+  if (lane == 0) {
+    gst[S_SCAL + 0] = (uint32_t)e.occ;
+    gst[S_SCAL + 1] = (uint32_t)(e.occ >> 32);
+    gst[S_SCAL + 2] = (uint32_t)e.wmask;
+    gst[S_SCAL + 3] = (uint32_t)(e.wmask >> 32);
+    gst[S_SCAL + 4] = e.k;
+    gst[S_SCAL + 5] = e.err;
+    gst[S_SCAL + 6] = e.epoch;
+  }
+  __threadfence_system();
+  if (lane == 0) st_sys(ctl + P_RUN, 0u);
+}
+}  // namespace persist
+
 }  // namespace wav
+
+int persist_launch(const PersistArgs& a, hipStream_t stream) {
+  if ((a.row_slots & (a.row_slots - 1u)) || (a.out_slots & (a.out_slots - 1u)) || !a.ctl || !a.rows || !a.out ||
+      !a.state)
+    return FX_ERR_INVALID_ARG;
+  hipLaunchKernelGGL(wav::persist::k_handle_persist, dim3(1), dim3(64), 0, stream, a);
+  return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
+}
 
 int launch_wave(const KArgs& a, hipStream_t stream) {
   if (a.num_lanes == 0) return FX_OK;

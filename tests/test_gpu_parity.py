@@ -485,3 +485,51 @@ def test_full_size_single_instance_matches_oracle(gpu, name, cmds, conflict):
     if conflict == 100:
         # SCCs larger than one command exist (the worst-case graph of configs[3])
         assert chain[2:].sum() > 0
+
+
+def _drain_run(stream, n, every, env=None, sleep_at=None):
+    import os
+    import time
+    old = os.environ.get("FX_HANDLE_PERSIST")
+    if env is not None:
+        os.environ["FX_HANDLE_PERSIST"] = env
+    try:
+        ex = GraphExecutor(1, 0, n, monitor=True)
+    finally:
+        if env is not None:
+            if old is None:
+                del os.environ["FX_HANDLE_PERSIST"]
+            else:
+                os.environ["FX_HANDLE_PERSIST"] = old
+    got = []
+    for i, (dot, deps, t, _kind) in enumerate(stream):
+        ex.handle_add(dot, dot, [0], deps, t)
+        if i % every == 0:
+            got += ex.drain_dots()
+        if sleep_at is not None and i == sleep_at:
+            time.sleep(0.6)  # the persistent kernel exits when idle; the next flush relaunches it
+    got += ex.drain_dots()
+    out = (got, ex.metrics(CHAIN_SIZE), ex.metrics(EXECUTION_DELAY), ex.pending())
+    ex.close()
+    return out
+
+
+def test_executor_persistent_mode_equals_batch_tiers_and_oracle(gpu):
+    """The handle's persistent mode (one resident wavefront running the wave
+    tier over Adds published in host-mapped memory, drained after every Add as
+    runner.rs:406-424 does) against the batch-tier handle (FX_HANDLE_PERSIST=0)
+    and the oracle: same order, SCC starts, metrics; the kernel's idle exit and
+    relaunch in the middle of the log change nothing."""
+    p = fs.synth_params(seed=21, n=5, instances=1, cmds=3000, window=8, cycle_pct=30, conflicts=(50,))
+    stream = fs.synth_host(p).stream(0)
+    g = oracle_lib.Graph(1, 5)
+    for (dot, deps, t, _kind) in stream:
+        g.handle_add(dot, deps, t)
+    exp = [d for d, _, _ in g.drain()]
+    a = _drain_run(stream, 5, 1)
+    b = _drain_run(stream, 5, 7, env="0")
+    c = _drain_run(stream, 5, 3, sleep_at=len(stream) // 2)
+    assert [d for d, _ in a[0]] == exp
+    assert a[0] == b[0] == c[0]
+    assert a[1:] == b[1:] == c[1:]
+    assert a[1] == g.metrics(1) and a[2] == g.metrics(0)

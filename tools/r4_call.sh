@@ -1,9 +1,10 @@
-# round-4 GPU call: the zero-fill poisoned test against the pre-fix
-# iterative-ILP k_sim (must fail: the test catches the round-3 defect), then an
-# A/B of the fixed k_sim builds (default vs iterative-ILP schedule) on configs[1]
+# round-4 GPU call: the persistent handle (tests, then bench --mode handle),
+# then the whole measurement (tools/r4_measure.sh)
 set -u
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out/poison
-FX_LIB=fantoch_amd/build_iilp_old/libfantoch_amd.so timeout -k 10 300 python -u -m pytest -v --timeout 200 --timeout-method thread tests/test_sim_poison.py -k "n7 or no_gc" > gpurun_out/poison/old_iilp_poison.log 2>&1
-rc=$?; echo "old iilp poison rc=$rc (1 expected)"; if [ $rc -ne 1 ] && [ $rc -ne 0 ]; then exit $rc; fi
-bash tools/sim_ab.sh base iilp base iilp
+mkdir -p gpurun_out/r4
+timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "executor" > gpurun_out/r4/handle_tests.log 2>&1
+rc=$?; echo "handle tests rc=$rc"; tail -3 gpurun_out/r4/handle_tests.log; if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 300 python -u bench.py --mode handle > gpurun_out/r4/handle.log 2>&1
+rc=$?; echo "bench handle rc=$rc"; tail -c 600 gpurun_out/r4/handle.log; if [ $rc -ne 0 ]; then exit $rc; fi
+bash tools/r4_measure.sh
