@@ -134,6 +134,14 @@ struct Lane {
   uint32_t* order = nullptr;
   uint4 ob = make_uint4(0, 0, 0, 0);  // order words k & ~3 .. k - 1, not yet stored
   uint32_t* release = nullptr;
+  // release words of the block of `cur` (steps cur & ~3 .. +3), stored when the
+  // next block starts: a release in the block being read (every fast-path
+  // singleton) lands in the buffer, older ones go straight to memory after it
+  // was stored.  rlo: the block's first step this launch processed (NONE: no
+  // block yet); the words below rlo belong to an earlier launch and are not
+  // rewritten.
+  uint4 rb = make_uint4(FX_RELEASE_NONE, FX_RELEASE_NONE, FX_RELEASE_NONE, FX_RELEASE_NONE);
+  uint32_t rlo = 0xFFFFFFFFu;
 
   __device__ __forceinline__ uint32_t& w(uint32_t i) { return lds[i * WV]; }
   __device__ __forceinline__ uint32_t& tw(uint32_t sl) { return w(L_TW + sl); }
@@ -230,6 +238,32 @@ struct Lane {
     ob.w = q == 3 ? w : ob.w;
     if (q == 3) *reinterpret_cast<uint4*>(order + at(k - 3)) = ob;
   }
+  __device__ __forceinline__ void put_release(uint32_t r, uint32_t v) {
+    if (rlo != 0xFFFFFFFFu && (r >> 2) == (cur >> 2) && r >= rlo) {
+      const uint32_t q = r & 3u;
+      rb.x = q == 0 ? v : rb.x;
+      rb.y = q == 1 ? v : rb.y;
+      rb.z = q == 2 ? v : rb.z;
+      rb.w = q == 3 ? v : rb.w;
+    } else {
+      release[at(r)] = v;
+    }
+  }
+  // stores the release words of the block of `cur`, steps [rlo, cur]: one
+  // 16-byte store for a whole block, else word by word
+  __device__ __forceinline__ void flush_release() {
+    if (rlo == 0xFFFFFFFFu) return;
+    const uint32_t b = cur & ~3u;
+    if (rlo == b && cur == b + 3u) {
+      *reinterpret_cast<uint4*>(release + at(b)) = rb;
+    } else {
+      for (uint32_t t = rlo; t <= cur; ++t) {
+        const uint32_t q = t & 3u;
+        release[at(t)] = q == 0 ? rb.x : q == 1 ? rb.y : q == 2 ? rb.z : rb.w;
+      }
+    }
+    rlo = 0xFFFFFFFFu;
+  }
   // stores the buffered words of an incomplete segment (kernel end)
   __device__ __forceinline__ void flush_order() {
     const uint32_t q = k & 3u, b = k - q;
@@ -241,7 +275,7 @@ struct Lane {
   __device__ __forceinline__ void emit(uint32_t r, uint32_t d, bool start) {
     if (k >= steps) { err = FX_ERR_ORDER_OVERFLOW; return; }
     put_order(r | (start ? FX_ORDER_SCC_START : 0u));
-    release[at(r)] = cur;
+    put_release(r, cur);
     ++k;
     clk_add(d);
   }
@@ -348,6 +382,11 @@ struct Lane {
     uint32_t vec[DC], dw[DC];
     uint32_t lo = 0, hi = 0;
     if (start) {
+      if (rlo != 0xFFFFFFFFu && (i >> 2) != (cur >> 2)) flush_release();
+      if (rlo == 0xFFFFFFFFu) {
+        rb = make_uint4(FX_RELEASE_NONE, FX_RELEASE_NONE, FX_RELEASE_NONE, FX_RELEASE_NONE);
+        rlo = i;
+      }
       cur = i;
       nwl = 0;
       uint32_t e0 = 0, prev = 0;
@@ -402,7 +441,7 @@ struct Lane {
         err = FX_ERR_ORDER_OVERFLOW;
       } else {
         put_order(r | (fast || sfirst ? FX_ORDER_SCC_START : 0u));
-        release[at(r)] = cur;
+        put_release(r, cur);
         ++k;
         clk_add(ed);
         wt = waiters(ed);
@@ -416,7 +455,7 @@ struct Lane {
           err = FX_ERR_ORDER_OVERFLOW;
         } else {
           put_order(i | FX_ORDER_SCC_START);
-          release[at(i)] = i;
+          put_release(i, i);
           ++k;
         }
       } else if (!err && occ && m1) {
@@ -716,6 +755,7 @@ void k_graph_lane(KArgs a) {
   }
 
   if (!active) return;
+  e.flush_release();
   // vertices still pending have no release step (yet)
   for (uint32_t m = e.occ; m; m &= m - 1)
     a.release[e.at(e.rec(__builtin_ctz(m)) & 0x03FFFFFFu)] = FX_RELEASE_NONE;
