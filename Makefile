@@ -16,8 +16,9 @@ SRCS := fantoch_amd/csrc/graph_exec.hip fantoch_amd/csrc/graph_group.hip fantoch
 HDRS := include/fantoch_amd.h include/fantoch_amd.hpp fantoch_amd/csrc/fx_synth.h fantoch_amd/csrc/fx_internal.h
 
 POISON := tests/poison/build/libpoison.so
+HLAT := tools/build/handle_latency
 
-all: $(LIB) $(ORACLE) $(CPPTEST) $(POISON)
+all: $(LIB) $(ORACLE) $(CPPTEST) $(POISON) $(HLAT)
 
 # one object per source (make -j compiles them in parallel), then one link
 OBJDIR := fantoch_amd/build/obj
@@ -87,6 +88,12 @@ $(CPPTEST): tests/cpp/test_graph_executor.cpp include/fantoch_amd.hpp include/fa
 $(POISON): tests/poison/poison.hip
 	@mkdir -p tests/poison/build
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -fPIC -shared -o $@ $<
+
+# measurement helper: the handle's per-Add cost in a C++ loop (bench.py --mode handle)
+$(HLAT): tools/handle_latency.cpp include/fantoch_amd.h $(LIB)
+	@mkdir -p tools/build
+	$(CXX) -O2 -std=c++17 -Wall -Iinclude -o $@ tools/handle_latency.cpp \
+	  -Lfantoch_amd -lfantoch_amd -Wl,-rpath,'$$ORIGIN/../../fantoch_amd'
 
 # kernel resource usage (VGPR/SGPR/LDS/occupancy) for DESIGN.md / tuning
 resource-usage:

@@ -76,7 +76,10 @@ def main_handle(args):
         o_order, _, o_nexec, _ = O.batch_execute(planes, threads=1)
     cpu_loop_s = (time.perf_counter() - t0) / reps
     nadd = len(stream)
-    parity = got == want and cpu_order == want
+    # the same loop in C++ over the C-ABI (tools/handle_latency.cpp): the
+    # handle's own cost per Add, without ctypes argument marshalling
+    cpp = _cpp_loop(stream, want, p + 1)
+    parity = got == want and cpu_order == want and (cpp is None or cpp["order_parity"])
     line = {
         "metric": "GraphExecutor handle: Adds/s, drained after every Add (runner.rs:406-424 pattern)",
         "value": round(nadd / gpu_s, 1), "unit": "Adds/s", "n_gpus": 1, "steps": 1, "warmup": 0,
@@ -86,6 +89,8 @@ def main_handle(args):
         "config": {"workload": "EPaxos n=5 f=2, GCP regions, 1 client/region, %d cmds/client, %d%% conflicts: "
                                "process 1's %d Adds" % (cmds, conflict, nadd)},
         "gpu_us_per_add": round(gpu_s / nadd * 1e6, 2),
+        "gpu_us_per_add_cpp_loop": cpp["us_per_add_median"] if cpp else None,
+        "gpu_cpp_loop": {k: v for k, v in cpp.items() if k != "order"} if cpp else None,
         "cpu_oracle_us_per_add_ctypes": round(cpu_call_s / nadd * 1e6, 3),
         "cpu_oracle_us_per_add_cpp_loop": round(cpu_loop_s / nadd * 1e6, 4),
         "cpu_baseline": {"value": round(nadd / cpu_loop_s, 1), "unit": "Adds/s", "cores": 1, "kind": "port",
@@ -93,10 +98,44 @@ def main_handle(args):
                          "sample": "the same %d Adds through the oracle DependencyGraph in one C++ loop "
                                    "(batch_execute, 1 thread), %d repetitions" % (nadd, reps)},
         "order_parity": bool(parity),
-        "note": "the handle is launch-latency bound: every pull is one resumable executor launch plus its "
-                "strided copies; the batched entry points (fx_batch_*, fx_sim_run) are the throughput path",
+        "note": "persistent mode: one resident wavefront executes the Adds a pull publishes in host-mapped "
+                "memory (no launch, no stream synchronisation per pull); gpu_us_per_add includes the Python "
+                "ctypes calls (handle_add + drain_dots), gpu_us_per_add_cpp_loop the same loop in C++. The "
+                "batched entry points (fx_batch_*, fx_sim_run) are the throughput path",
     }
     print(json.dumps(line), flush=True)
     if not parity:
         raise SystemExit("handle order differs from the simulation's")
     return line
+
+
+def _cpp_loop(stream, want, pid, reps=5):
+    """Runs tools/build/handle_latency on the stream (None if it is not built)."""
+    import struct
+    import subprocess
+    import tempfile
+    root = os.path.dirname(os.path.abspath(__file__))
+    exe = os.path.join(root, "tools", "build", "handle_latency")
+    if not os.path.exists(exe):
+        return None
+    buf = [struct.pack("<III", 5, pid, len(stream))]
+    for (dot, deps, t) in stream:
+        buf.append(struct.pack("<IIII", dot[0], dot[1], t, len(deps)))
+        for d in deps:
+            buf.append(struct.pack("<II", d[0], d[1]))
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as fh:
+        fh.write(b"".join(buf))
+        path = fh.name
+    try:
+        out = subprocess.run([exe, path, str(reps)], capture_output=True, text=True, timeout=120)
+    finally:
+        os.unlink(path)
+    if out.returncode != 0:
+        return {"error": out.returncode, "order_parity": False, "us_per_add_median": None}
+    lines = out.stdout.strip().splitlines()
+    d = json.loads(lines[-1])
+    for ln in lines[:-1]:
+        if ln.startswith('{"persist"'):
+            d.update(json.loads(ln))
+    d["order_parity"] = [(x >> 24, x & 0xFFFFFF) for x in d["order"]] == want
+    return d

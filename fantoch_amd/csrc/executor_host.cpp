@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -173,6 +174,9 @@ struct fx_graph_executor {
     DevBuf state;
     uint32_t pub = 0;  // rows published
     static constexpr uint32_t ROWS = 4096, OUT = 8192;
+    // fx_graph_executor_persist_stats: flushes, host wait (ns), and the
+    // kernel's compute / fence ticks, polls and poll round trips (100 MHz)
+    uint64_t stats[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // + host prep / convert (ns), compute shader cycles
   } ps;
   bool persist_ok = true;
 };
@@ -290,6 +294,7 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
   }
   uint32_t nexec = pctl(ex)[fx::PERSIST_NEXEC];
   while (P.pub < N) {
+    const auto tp0 = std::chrono::steady_clock::now();
     // a chunk the rings hold: every published row and pair was consumed
     const uint32_t hi = std::min<uint32_t>(N, P.pub + fx_graph_executor::Persist::ROWS - 128u);
     uint32_t* rows = P.rows.u32();
@@ -301,7 +306,20 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
       for (uint32_t j = 0; j < fx::PERSIST_ROW_WORDS - 2u; ++j) r[2 + j] = j < dv.size() ? dv[j] : 0u;
     }
     ex->bytes_h2d += (uint64_t)(hi - P.pub) * fx::PERSIST_ROW_WORDS * 4;
+    if (hi == P.pub + 1u && ex->deps[P.pub].size() <= fx::PERSIST_MB_DEPS) {
+      // a one-Add flush: the row also goes into the mailbox line, which the
+      // kernel reads with the doorbell (tag last: the line is read as a unit)
+      volatile uint32_t* mb = pctl(ex) + fx::PERSIST_MB;
+      const auto& dv = ex->deps[P.pub];
+      mb[1] = ex->dots[P.pub];
+      mb[2] = ex->hdrs[P.pub];
+      for (uint32_t j = 0; j < fx::PERSIST_MB_DEPS; ++j) mb[3 + j] = j < dv.size() ? dv[j] : 0u;
+      std::atomic_thread_fence(std::memory_order_release);
+      mb[0] = hi;
+    }
     std::atomic_thread_fence(std::memory_order_seq_cst);  // the rows before the doorbell
+    const auto tw0 = std::chrono::steady_clock::now();
+    P.stats[6] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tw0 - tp0).count();
     pctl(ex)[fx::PERSIST_PUB] = hi;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     if (!P.launched) {
@@ -321,6 +339,14 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
       }
     }
     std::atomic_thread_fence(std::memory_order_seq_cst);
+    P.stats[0] += 1;
+    P.stats[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tw0)
+                      .count();
+    P.stats[2] += pctl(ex)[fx::PERSIST_TCOMP];
+    P.stats[3] += pctl(ex)[fx::PERSIST_TFENCE];
+    P.stats[4] += pctl(ex)[fx::PERSIST_TPOLLS];
+    P.stats[5] += pctl(ex)[fx::PERSIST_TRTT];
+    P.stats[8] += pctl(ex)[fx::PERSIST_TCYC];
     const uint32_t err = pctl(ex)[fx::PERSIST_ERR];
     if (err) {
       persist_stop(ex);
@@ -338,7 +364,10 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
         rel[k - ex->consumed] = q[2 * (k & (fx_graph_executor::Persist::OUT - 1u)) + 1];
       }
       ex->bytes_d2h += 12 + (uint64_t)(nexec - ex->consumed) * 8;
+      const auto tc0 = std::chrono::steady_clock::now();
       convert(ex, order, rel, nexec);
+      P.stats[7] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::steady_clock::now() - tc0).count();
     }
   }
   ex->processed = N;
@@ -936,6 +965,12 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
 
 
 int fx_graph_executor_parallel(void) { return 1; }
+
+int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out9) {
+  if (!ex || !out9) return FX_ERR_INVALID_ARG;
+  for (int i = 0; i < 9; ++i) out9[i] = ex->ps.stats[i];
+  return FX_OK;
+}
 
 int fx_graph_executor_transfer_stats(const fx_graph_executor* ex, uint64_t* h2d, uint64_t* d2h) {
   if (!ex || !h2d || !d2h) return FX_ERR_INVALID_ARG;

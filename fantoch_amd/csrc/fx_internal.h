@@ -93,9 +93,11 @@ struct PersistArgs {
   uint32_t n, at_commit, init, done0;
 };
 constexpr uint32_t PERSIST_ROW_WORDS = 16;  // dot, hdr, 14 deps
-constexpr uint32_t PERSIST_CTL_WORDS = 16;
-enum : uint32_t { PERSIST_PUB = 0, PERSIST_EXIT = 1, PERSIST_DONE = 2, PERSIST_NEXEC = 3, PERSIST_ERR = 4,
-                  PERSIST_RUN = 5 };
+constexpr uint32_t PERSIST_CTL_WORDS = 64;
+constexpr uint32_t PERSIST_MB_DEPS = 13;    // deps a mailbox row carries
+enum : uint32_t { PERSIST_PUB = 0, PERSIST_EXIT = 1, PERSIST_MB = 16, PERSIST_DONE = 32, PERSIST_NEXEC = 33,
+                  PERSIST_ERR = 34, PERSIST_TCOMP = 35, PERSIST_TFENCE = 36, PERSIST_TPOLLS = 37,
+                  PERSIST_TRTT = 38, PERSIST_TCYC = 39, PERSIST_RUN = 47 };
 int persist_launch(const PersistArgs& a, hipStream_t stream);
 // fx_profile_slot_ms: events around one kernel slot's launch (graph_exec.hip)
 void profile_slot_record(uint32_t slot, bool end, hipStream_t s);

@@ -510,9 +510,12 @@ __global__ __launch_bounds__(64 * WPB) void k_graph_wave(KArgs a) {
 // plus a synchronisation per Add costs tens of microseconds, so instead ONE
 // wavefront stays resident and runs the wave tier's executor (the Wave above)
 // over Adds the host publishes in host-mapped memory:
-//   ctl[P_PUB]   rows published by the host (release store after the rows)
+//   ctl[P_PUB]   rows published by the host (written after the rows)
 //   ctl[P_EXIT]  host asks the kernel to stop
-//   ctl[P_DONE]  rows processed (the kernel's release store, after the outputs)
+//   ctl[P_MB..]  mailbox: tag (= row index + 1), dot, hdr, 13 deps of the row of
+//                a one-Add flush, read in the same round trip as the doorbell
+//   ctl[P_DONE]  rows processed (written after one release fence that follows
+//                the outputs)
 //   ctl[P_NEXEC] / ctl[P_ERR]  executed count and status after those rows
 //   ctl[P_RUN]   1 while the kernel is resident
 // rows: a ring of PR rows of PRW words (dot, hdr, up to 14 deps), row i in slot
@@ -523,8 +526,12 @@ __global__ __launch_bounds__(64 * WPB) void k_graph_wave(KArgs a) {
 // kernel outlives an idle or vanished host (a device-wide synchronisation
 // waits for it at most that long).
 namespace persist {
-enum : uint32_t { P_PUB = 0, P_EXIT = 1, P_DONE = 2, P_NEXEC = 3, P_ERR = 4, P_RUN = 5, P_WORDS = 16 };
+// control words (host-mapped, fine-grained): line 0 host -> device, line 1 the
+// mailbox (the row of a one-Add flush), line 2 device -> host
+enum : uint32_t { P_PUB = 0, P_EXIT = 1, P_MB = 16, P_DONE = 32, P_NEXEC = 33, P_ERR = 34, P_TCOMP = 35,
+                  P_TFENCE = 36, P_TPOLLS = 37, P_TRTT = 38, P_TCYC = 39, P_RUN = 47 };
 constexpr uint32_t PRW = 16;                     // words per published row
+constexpr uint32_t MBD = 13;                     // deps a mailbox row carries (tag, dot, hdr, deps)
 constexpr uint64_t IDLE_TICKS = 25000000ull;     // s_memrealtime runs at 100 MHz: 0.25 s
 
 struct RingOut {
@@ -537,11 +544,12 @@ struct RingOut {
   }
 };
 
+// one lane-parallel load with system coherence (the host's latest writes)
 __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
@@ -577,38 +585,65 @@ __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
     e.epoch = uni(gst[S_SCAL + 6]);
   }
   uint32_t* ctl = a.ctl;
-  if (lane == 0) st_sys(ctl + P_RUN, 1u);
   uint32_t done = a.done0;
   uint64_t idle0 = __builtin_amdgcn_s_memrealtime();
+  // timing words for tools/handle_latency (100 MHz ticks): the last poll's
+  // round trip, the polls before the last doorbell, the last flush's compute
+  // and its release fence
+  uint32_t t_rtt = 0, t_polls = 0, t_fence = 0;
   while (!e.err) {
-    const uint32_t pub = uni(ld_sys(ctl + P_PUB));
-    if (uni(ld_sys(ctl + P_EXIT))) break;
+    // one round trip: the doorbell line and the mailbox line (lane w: word w)
+    const uint64_t tp0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t v = lane < 32u ? ld_sys(ctl + lane) : 0u;
+    const uint32_t pub = rl(v, P_PUB);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // (timing: the load has returned)
+    const uint64_t tp1 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t cy1 = __builtin_amdgcn_s_memtime();
+    if (rl(v, P_EXIT)) break;
+    ++t_polls;
     if (pub == done) {
-      if (__builtin_amdgcn_s_memrealtime() - idle0 > IDLE_TICKS) break;
+      if (tp1 - idle0 > IDLE_TICKS) break;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    // rows [done, pub), four per load: lane 16 r + w reads word w of row i + r
-    for (uint32_t i = done; i < pub && !e.err; i += 4) {
-      const uint32_t r4 = lane >> 4, w = lane & 15u;
-      const uint32_t row = i + r4;
-      const uint32_t v = row < pub ? a.rows[(size_t)(row & (a.row_slots - 1u)) * PRW + w] : 0u;
-      for (uint32_t r = 0; r < 4 && i + r < pub && !e.err; ++r) {
-        const uint32_t d = rl(v, 16u * r), h = rl(v, 16u * r + 1u);
-        const uint32_t depj = gather(v, (16u * r + 2u + lane) & 63u);
-        e.step_start(i + r, d, h, lane < MAXD ? depj : 0u, MAXD, a.at_commit != 0);
-        if (e.phase != PH_IDLE) e.run_slow();
+    t_rtt = (uint32_t)(tp1 - tp0);
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the rows after the doorbell
+    if (pub == done + 1u && rl(v, P_MB) == pub) {
+      // a one-Add flush: its row came with the doorbell (the host writes the
+      // mailbox line before the doorbell; a load that saw the new doorbell but
+      // an older mailbox tag falls back to the ring)
+      const uint32_t d = rl(v, P_MB + 1u), h = rl(v, P_MB + 2u);
+      const uint32_t depj = gather(v, (P_MB + 3u + lane) & 63u);
+      e.step_start(done, d, h, lane < MBD ? depj : 0u, MBD, a.at_commit != 0);
+      if (e.phase != PH_IDLE) e.run_slow();
+    } else {
+      // rows [done, pub) from the ring, four per load: lane 16 r + w reads word w of row i + r
+      for (uint32_t i = done; i < pub && !e.err; i += 4) {
+        const uint32_t r4 = lane >> 4, w = lane & 15u;
+        const uint32_t row = i + r4;
+        const uint32_t rv = row < pub ? a.rows[(size_t)(row & (a.row_slots - 1u)) * PRW + w] : 0u;
+        for (uint32_t r = 0; r < 4 && i + r < pub && !e.err; ++r) {
+          const uint32_t d = rl(rv, 16u * r), h = rl(rv, 16u * r + 1u);
+          const uint32_t depj = gather(rv, (16u * r + 2u + lane) & 63u);
+          e.step_start(i + r, d, h, lane < MAXD ? depj : 0u, MAXD, a.at_commit != 0);
+          if (e.phase != PH_IDLE) e.run_slow();
+        }
       }
     }
-    // outputs first, then the counters, then the done word (release)
+    // the pairs (plain stores), the counters, then ONE release fence before
+    // the done word (every lane stores the same word to the same address:
+    // one request, and no exec-mask split around the fence)
+    const uint64_t tc = __builtin_amdgcn_s_memrealtime();
+    const uint32_t cyc = (uint32_t)(__builtin_amdgcn_s_memtime() - cy1);
+    if (lane < 7u)
+      ctl[P_NEXEC + lane] = lane == 0 ? e.k : lane == 1 ? e.err : lane == 2 ? (uint32_t)(tc - tp1)
+                          : lane == 3 ? t_fence : lane == 4 ? t_polls : lane == 5 ? t_rtt : cyc;
     __threadfence_system();
-    if (lane == 0) {
-      st_sys(ctl + P_NEXEC, e.k);
-      st_sys(ctl + P_ERR, e.err);
-      st_sys(ctl + P_DONE, pub);
-    }
+    st_sys(ctl + P_DONE, pub);
     done = pub;
     idle0 = __builtin_amdgcn_s_memrealtime();
+    t_fence = (uint32_t)(idle0 - tc);
+    t_polls = 0;
   }
   uint32_t* r = gst + lane * RREGS;
   r[0] = e.sdot;

@@ -493,6 +493,9 @@ struct Sim : GP {
     }
   }
   __device__ __forceinline__ void hist_delay(uint32_t v) {
+#ifdef FX_ABL_HIST  // measurement-only ablation (wrong histograms)
+    return;
+#endif
     if (v < HD_BINS) {
       if (lid == 0) atomicAdd(&lds[g.off_hist + v], 1u);
     } else if (lid == 0) {
@@ -642,6 +645,9 @@ struct Sim : GP {
   }
   __device__ __forceinline__ void note_(uint64_t kind, uint64_t a, uint64_t b, uint64_t c) {
     ++events;
+#ifdef FX_ABL_NOTE  // measurement-only ablation (wrong trace): the cost of the trace hash
+    return;
+#endif
     trace = mix64(trace ^ ((uint64_t)now << 24) ^ (kind << 20) ^ (a << 12) ^ (b << 4)) + c;
   }
 

@@ -1,0 +1,93 @@
+// handle_latency — the drop-in handle's per-Add cost without an interpreter in
+// the loop: the reference simulator's calling pattern (runner.rs:406-424:
+// handle(Add) then drain to_clients, one Add at a time) as a C++ loop over the
+// C-ABI.  Reads a captured commit stream written by bench_handle.py:
+//   u32 n, u32 process_id, u32 count, then per Add:
+//   u32 src, u32 seq, u32 t_ms, u32 ndeps, ndeps x (u32 src, u32 seq)
+// and prints one JSON line: microseconds per Add (median of `reps` passes, each
+// on a fresh handle) and the execution order as packed dots (src << 24 | seq).
+// Measurement helper, not product code.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+
+#include "fantoch_amd.h"
+
+struct Add {
+  fx_dot dot;
+  uint32_t t;
+  std::vector<fx_dot> deps;
+};
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: handle_latency stream.bin [reps]\n");
+    return 2;
+  }
+  const int reps = argc > 2 ? std::atoi(argv[2]) : 5;
+  FILE* f = std::fopen(argv[1], "rb");
+  if (!f) return 2;
+  uint32_t hdr[3];
+  if (std::fread(hdr, 4, 3, f) != 3) return 2;
+  std::vector<Add> adds(hdr[2]);
+  for (auto& a : adds) {
+    uint32_t w[4];
+    if (std::fread(w, 4, 4, f) != 4) return 2;
+    a.dot = fx_dot{w[0], w[1]};
+    a.t = w[2];
+    a.deps.resize(w[3]);
+    for (auto& d : a.deps) {
+      uint32_t x[2];
+      if (std::fread(x, 4, 2, f) != 2) return 2;
+      d = fx_dot{x[0], x[1]};
+    }
+  }
+  std::fclose(f);
+  fx_config cfg{hdr[0], 1, 1, 0, 0};
+  std::vector<double> us;
+  std::vector<uint32_t> order;
+  std::vector<fx_dot> buf(256);
+  std::vector<uint8_t> start(256);
+  const uint32_t key = 0;
+  for (int r = 0; r < reps + 1; ++r) {  // pass 0 warms up (module load, first allocations)
+    fx_graph_executor* ex = fx_graph_executor_new((uint8_t)hdr[1], 0, &cfg);
+    if (!ex) return 3;
+    order.clear();
+    const auto t0 = std::chrono::steady_clock::now();
+    double add_ns = 0;
+    for (const auto& a : adds) {
+      fx_rifl rifl{a.dot.source, a.dot.seq};
+      const auto ta = std::chrono::steady_clock::now();
+      if (fx_graph_executor_handle_add(ex, a.dot, rifl, &key, 1, 0, a.deps.data(), (uint32_t)a.deps.size(), a.t))
+        return 4;
+      add_ns += std::chrono::duration<double, std::nano>(std::chrono::steady_clock::now() - ta).count();
+      uint32_t got = 0;
+      do {
+        if (fx_graph_executor_drain_dots(ex, buf.data(), start.data(), 256, &got)) return 5;
+        for (uint32_t i = 0; i < got; ++i) order.push_back(FX_PACK_DOT(buf[i].source, buf[i].seq));
+      } while (got == 256);
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    uint64_t ps[9];
+    fx_graph_executor_persist_stats(ex, ps);
+    if (r == reps && ps[0]) {
+      const double f = (double)ps[0];
+      std::printf("{\"persist\": {\"flushes\": %llu, \"host_wait_us\": %.3f, \"compute_us\": %.3f, \"fence_us\": %.3f, "
+                  "\"polls_per_flush\": %.2f, \"poll_rtt_us\": %.3f, \"host_prep_us\": %.3f, \"host_convert_us\": %.3f, "
+                  "\"handle_add_us\": %.3f, \"compute_mhz\": %.0f}}\n",
+                  (unsigned long long)ps[0], ps[1] / f / 1e3, ps[2] / f / 100.0, ps[3] / f / 100.0, ps[4] / f,
+                  ps[5] / f / 100.0, ps[6] / f / 1e3, ps[7] / f / 1e3, add_ns / adds.size() / 1e3,
+                  ps[2] ? 100.0 * (double)ps[8] / (double)ps[2] : 0.0);
+    }
+    fx_graph_executor_free(ex);
+    if (r > 0) us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count() / adds.size());
+  }
+  std::sort(us.begin(), us.end());
+  std::printf("{\"adds\": %zu, \"reps\": %d, \"us_per_add_median\": %.3f, \"us_per_add_min\": %.3f, \"order\": [",
+              adds.size(), reps, us[us.size() / 2], us[0]);
+  for (size_t i = 0; i < order.size(); ++i) std::printf(i ? ", %u" : "%u", order[i]);
+  std::printf("]}\n");
+  return 0;
+}

@@ -1,10 +1,6 @@
-# round-4 GPU call: the persistent handle (tests, then bench --mode handle),
-# then the whole measurement (tools/r4_measure.sh)
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/r4
-timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "executor" > gpurun_out/r4/handle_tests.log 2>&1
-rc=$?; echo "handle tests rc=$rc"; tail -3 gpurun_out/r4/handle_tests.log; if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 300 python -u bench.py --mode handle > gpurun_out/r4/handle.log 2>&1
-rc=$?; echo "bench handle rc=$rc"; tail -c 600 gpurun_out/r4/handle.log; if [ $rc -ne 0 ]; then exit $rc; fi
-bash tools/r4_measure.sh
+bash tools/sim_ab.sh base gcu base gcu || exit 1
+FX_LIB=fantoch_amd/build_gcu/libfantoch_amd.so timeout -k 10 400 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_sim_gpu.py tests/test_sim_poison.py > gpurun_out/r4/gcu_tests.log 2>&1
+rc=$?; echo "gcu tests rc=$rc"; tail -2 gpurun_out/r4/gcu_tests.log; exit $rc
