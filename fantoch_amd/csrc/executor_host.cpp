@@ -13,13 +13,16 @@
 
 #include <algorithm>
 #include <atomic>
+#include <emmintrin.h>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
+#include <mutex>
 #include <set>
+#include <string>
 #include <vector>
 
 #include "fantoch_amd.h"
@@ -54,6 +57,10 @@ struct DevBuf {
     return true;
   }
   uint32_t* u32() const { return static_cast<uint32_t*>(p); }
+  void swap(DevBuf& o) {
+    std::swap(p, o.p);
+    std::swap(bytes, o.bytes);
+  }
 };
 
 // pinned host memory mapped into the device's address space: the handle's
@@ -84,7 +91,27 @@ struct HostBuf {
   }
   uint32_t* u32() const { return static_cast<uint32_t*>(p); }
   uint32_t* du32() const { return static_cast<uint32_t*>(dp); }
+  void swap(HostBuf& o) {
+    std::swap(p, o.p);
+    std::swap(dp, o.dp);
+    std::swap(bytes, o.bytes);
+  }
 };
+
+// A persistent handle's resources: its stream (a hardware queue of its own,
+// ~12 ms to make) and its mapped control words, rings and state block.  A
+// freed handle leaves them in a process-wide pool for the next handle, so a
+// program that makes handle after handle (a test per permutation, a simulation
+// per configuration) makes the queue once.  The pool is never destroyed (its
+// buffers would be freed after the HIP runtime at exit).
+struct PersistRes {
+  hipStream_t stream = nullptr;
+  HostBuf ctl, rows, out;
+  DevBuf state;
+};
+std::mutex g_persist_pool_mu;
+std::vector<PersistRes*>* g_persist_pool = new std::vector<PersistRes*>();
+constexpr size_t kPersistPoolMax = 64;
 
 constexpr uint32_t kDmaxDev = 31;
 
@@ -176,7 +203,8 @@ struct fx_graph_executor {
     static constexpr uint32_t ROWS = 4096, OUT = 8192;
     // fx_graph_executor_persist_stats: flushes, host wait (ns), and the
     // kernel's compute / fence ticks, polls and poll round trips (100 MHz)
-    uint64_t stats[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // + host prep / convert (ns), compute shader cycles
+    uint64_t stats[12] = {};  // + host prep / convert (ns), compute shader cycles, flush total / post-wait reads / pre-publish (ns)
+    bool want_stats = false;  // FX_HANDLE_STATS=1: the kernel's fence / poll / cycle words too
   } ps;
   bool persist_ok = true;
 };
@@ -240,6 +268,18 @@ void convert(fx_graph_executor* ex, const std::vector<uint32_t>& order, const st
 
 volatile uint32_t* pctl(fx_graph_executor* ex) { return reinterpret_cast<volatile uint32_t*>(ex->ps.ctl.u32()); }
 
+// Reads of the device-written words: fine-grained host memory is not cached
+// for the host (each load is a memory round trip, ~0.25 us), so they are read
+// 16 bytes per load instead of word by word.  The load is one instruction in
+// inline asm: from a plain intrinsic the compiler may re-read a word from
+// memory instead of taking it from the loaded register, which tears a tagged
+// word pair written by the device (a new tag with an old value).
+inline void ld16(const volatile uint32_t* p, uint32_t out[4]) {
+  __m128i v;
+  asm volatile("movdqu %1, %0" : "=x"(v) : "m"(*reinterpret_cast<const volatile __m128i*>(p)) : "memory");
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(out), v);
+}
+
 // Stops the persistent kernel (its executor state lands in ps.state).
 int persist_stop(fx_graph_executor* ex) {
   if (!ex->ps.launched) return FX_OK;
@@ -249,6 +289,86 @@ int persist_stop(fx_graph_executor* ex) {
   ex->ps.launched = false;
   pctl(ex)[fx::PERSIST_EXIT] = 0u;
   return ok ? FX_OK : FX_ERR_HIP;
+}
+
+// The stream of a handle's persistent kernel.  The kernel stays resident, so
+// whatever else is queued on the same hardware queue waits for it (up to its
+// idle exit): FX_PERSIST_QUEUE picks how the stream is made -- "plain" (a
+// non-blocking stream, sharing the process's hardware queues), "prio" (a
+// non-blocking high-priority stream), "cumask" (a stream with an all-CU mask,
+// which gets a hardware queue of its own).
+hipError_t persist_stream(hipStream_t* s) {
+  const char* q = std::getenv("FX_PERSIST_QUEUE");
+  const std::string kind = q ? q : "cumask";
+  if (kind == "prio") {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return hipErrorUnknown;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+  }
+  if (kind == "cumask") {
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      return hipErrorUnknown;
+    std::vector<uint32_t> mask(((uint32_t)ncu + 31u) / 32u, 0u);
+    for (int c = 0; c < ncu; ++c) mask[(uint32_t)c / 32u] |= 1u << ((uint32_t)c % 32u);
+    return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+  }
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
+// The persistent mode's stream, mapped control words / rings and state block;
+// made when the handle is created (fx_graph_executor_new), so an Add never
+// pays for them.
+int persist_alloc(fx_graph_executor* ex) {
+  auto& P = ex->ps;
+  if (!P.stream) {
+    PersistRes* r = nullptr;
+    {
+      std::lock_guard<std::mutex> g(g_persist_pool_mu);
+      if (!g_persist_pool->empty()) {
+        r = g_persist_pool->back();
+        g_persist_pool->pop_back();
+      }
+    }
+    if (r) {
+      P.stream = r->stream;
+      P.ctl.swap(r->ctl);
+      P.rows.swap(r->rows);
+      P.out.swap(r->out);
+      P.state.swap(r->state);
+      delete r;
+    } else if (persist_stream(&P.stream) != hipSuccess) {
+      P.stream = nullptr;
+      return FX_ERR_HIP;
+    }
+  }
+  if (!P.ctl.ensure(fx::PERSIST_CTL_WORDS * 4, true) ||
+      !P.rows.ensure((size_t)fx_graph_executor::Persist::ROWS * fx::PERSIST_ROW_WORDS * 4, true) ||
+      !P.out.ensure((size_t)fx_graph_executor::Persist::OUT * 8, true) ||
+      !P.state.ensure((size_t)fx::wave_state_words_per_stream() * 4))
+    return FX_ERR_HIP;
+  std::memset(P.ctl.p, 0, fx::PERSIST_CTL_WORDS * 4);
+  return FX_OK;
+}
+
+// A wait that lasts seconds means a lost word: report the control words once.
+void persist_stuck(fx_graph_executor* ex, const char* where, uint32_t hi, uint64_t spin) {
+  if ((spin & 4095u) != 4095u) return;
+  static thread_local std::chrono::steady_clock::time_point t0;
+  static thread_local bool reported = false;
+  const auto now = std::chrono::steady_clock::now();
+  if (spin == 4095u) {
+    t0 = now;
+    reported = false;
+    return;
+  }
+  if (reported || now - t0 < std::chrono::seconds(5)) return;
+  reported = true;
+  std::fprintf(stderr, "fantoch_amd persistent handle: still waiting (%s) hi=%u consumed=%u pub=%u ctl[0..63]:", where,
+               hi, ex->consumed, ex->ps.pub);
+  for (uint32_t i = 0; i < 64; ++i) std::fprintf(stderr, " %u", pctl(ex)[i]);
+  std::fprintf(stderr, "\n");
 }
 
 int persist_launch_now(fx_graph_executor* ex, bool init) {
@@ -274,27 +394,26 @@ int persist_launch_now(fx_graph_executor* ex, bool init) {
 // word, take the new (order word, release step) pairs from the mapped ring.
 // Returns FX_ERR_CAPACITY when the log must move to the batch tiers.
 int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
+  const auto tf0 = std::chrono::steady_clock::now();
   const uint32_t N = (uint32_t)ex->dots.size();
   for (uint32_t i = ex->ps.pub; i < N; ++i)
     if (ex->deps[i].size() > fx::WAVE_MAX_DEPS) return FX_ERR_CAPACITY;
   auto& P = ex->ps;
   if (!P.active) {  // the first flush of the handle
     if (ex->processed != 0) return FX_ERR_CAPACITY;
-    if (!P.stream && hipStreamCreateWithFlags(&P.stream, hipStreamNonBlocking) != hipSuccess) return FX_ERR_HIP;
-    if (!P.ctl.ensure(fx::PERSIST_CTL_WORDS * 4, true) ||
-        !P.rows.ensure((size_t)fx_graph_executor::Persist::ROWS * fx::PERSIST_ROW_WORDS * 4, true) ||
-        !P.out.ensure((size_t)fx_graph_executor::Persist::OUT * 8, true) ||
-        !P.state.ensure((size_t)fx::wave_state_words_per_stream() * 4))
-      return FX_ERR_HIP;
-    std::memset(P.ctl.p, 0, fx::PERSIST_CTL_WORDS * 4);
+    if (!P.ctl.p) {
+      const int st = persist_alloc(ex);
+      if (st) return st;
+    }
     P.pub = 0;
     P.active = true;
     int st = persist_launch_now(ex, true);
     if (st) return st;
   }
-  uint32_t nexec = pctl(ex)[fx::PERSIST_NEXEC];
+  uint32_t nexec = ex->consumed;  // every pair of the earlier flushes was taken
   while (P.pub < N) {
     const auto tp0 = std::chrono::steady_clock::now();
+    P.stats[11] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tp0 - tf0).count();
     // a chunk the rings hold: every published row and pair was consumed
     const uint32_t hi = std::min<uint32_t>(N, P.pub + fx_graph_executor::Persist::ROWS - 128u);
     uint32_t* rows = P.rows.u32();
@@ -326,45 +445,89 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
       int st = persist_launch_now(ex, false);
       if (st) return st;
     }
-    // wait for the done word; a kernel that exited when idle just before the
-    // doorbell (RUN cleared, done short of hi) is relaunched from its state
-    for (uint64_t spin = 0; pctl(ex)[fx::PERSIST_DONE] != hi; ++spin) {
-      if ((spin & 1023u) == 1023u && pctl(ex)[fx::PERSIST_RUN] == 0u && pctl(ex)[fx::PERSIST_DONE] != hi) {
+    // wait for the status word {done, nexec | error bit} (read with its
+    // second word {done, err} as one 16-byte load); a kernel that exited when
+    // idle just before the doorbell (RUN cleared, done short of hi) is
+    // relaunched from its state
+    uint32_t w[4];
+    for (uint64_t spin = 0;; ++spin) {
+      ld16(pctl(ex) + fx::PERSIST_DONE, w);
+      if (w[0] == hi) break;
+      persist_stuck(ex, "status", hi, spin);
+      if ((spin & 1023u) == 1023u && pctl(ex)[fx::PERSIST_RUN] == 0u) {
         if (hipStreamSynchronize(P.stream) != hipSuccess) return FX_ERR_HIP;
         P.launched = false;
-        if (pctl(ex)[fx::PERSIST_DONE] == hi) break;
-        if (pctl(ex)[fx::PERSIST_ERR]) break;
+        ld16(pctl(ex) + fx::PERSIST_DONE, w);
+        if (w[0] == hi) break;
+        if (w[2] == w[0] && w[3]) {  // the kernel stopped on an error before these rows
+          persist_stop(ex);
+          return w[3] == FX_ERR_CAPACITY || w[3] == FX_ERR_ORDER_OVERFLOW ? FX_ERR_CAPACITY : (int)w[3];
+        }
         int st = persist_launch_now(ex, false);
         if (st) return st;
       }
     }
-    std::atomic_thread_fence(std::memory_order_seq_cst);
+    const auto tw1 = std::chrono::steady_clock::now();
     P.stats[0] += 1;
-    P.stats[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tw0)
-                      .count();
-    P.stats[2] += pctl(ex)[fx::PERSIST_TCOMP];
-    P.stats[3] += pctl(ex)[fx::PERSIST_TFENCE];
-    P.stats[4] += pctl(ex)[fx::PERSIST_TPOLLS];
-    P.stats[5] += pctl(ex)[fx::PERSIST_TRTT];
-    P.stats[8] += pctl(ex)[fx::PERSIST_TCYC];
-    const uint32_t err = pctl(ex)[fx::PERSIST_ERR];
-    if (err) {
+    P.stats[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tw1 - tw0).count();
+    if (w[1] & fx::PERSIST_ERR_BIT) {  // {done, err} is written with the status; wait for it
+      for (uint64_t spin = 0; w[2] != hi; ++spin) {
+        ld16(pctl(ex) + fx::PERSIST_DONE, w);
+        persist_stuck(ex, "error word", hi, spin);
+      }
+      const uint32_t err = w[3];
       persist_stop(ex);
       return err == FX_ERR_CAPACITY || err == FX_ERR_ORDER_OVERFLOW ? FX_ERR_CAPACITY : (int)err;
     }
-    nexec = pctl(ex)[fx::PERSIST_NEXEC];
+    if (P.want_stats) {
+      uint32_t t[4];
+      ld16(pctl(ex) + fx::PERSIST_TCOMP, t);
+      P.stats[2] += t[0];
+      P.stats[3] += t[1];
+      P.stats[4] += t[2];
+      P.stats[5] += t[3];
+      P.stats[8] += pctl(ex)[fx::PERSIST_TCYC];
+    }
+    nexec = w[1];
     P.pub = hi;
-    // the new pairs, straight out of the mapped ring
+    // the new pairs: tagged words in the control line, or the mapped ring
     if (nexec > ex->consumed) {
-      if (nexec - ex->consumed > fx_graph_executor::Persist::OUT) return FX_ERR_CAPACITY;
-      const uint32_t* q = P.out.u32();
-      std::vector<uint32_t> order(nexec - ex->consumed), rel(nexec - ex->consumed);
-      for (uint32_t k = ex->consumed; k < nexec; ++k) {
-        order[k - ex->consumed] = q[2 * (k & (fx_graph_executor::Persist::OUT - 1u))];
-        rel[k - ex->consumed] = q[2 * (k & (fx_graph_executor::Persist::OUT - 1u)) + 1];
+      const uint32_t np = nexec - ex->consumed;
+      if (np > fx_graph_executor::Persist::OUT) return FX_ERR_CAPACITY;
+      std::vector<uint32_t> order(np), rel(np);
+      if (np <= fx::PERSIST_INLINE) {
+        for (uint32_t j = 0; j < np; ++j) {
+          uint32_t t[4];
+          for (uint64_t spin = 0;; ++spin) {
+            ld16(pctl(ex) + fx::PERSIST_PAIRS + 4 * j, t);
+            if (t[0] == hi && t[2] == hi) break;
+            persist_stuck(ex, "pairs", hi, spin);
+          }
+          order[j] = t[1];
+          rel[j] = t[3];
+        }
+      } else {
+        const volatile uint32_t* q = reinterpret_cast<volatile uint32_t*>(P.out.u32());
+        constexpr uint32_t M = fx_graph_executor::Persist::OUT - 1u;
+        for (uint32_t k = ex->consumed; k < nexec;) {
+          if ((k & 1u) == 0 && k + 1 < nexec && ((k + 1) & M) != 0) {  // two pairs per read
+            uint32_t t[4];
+            ld16(q + 2 * (k & M), t);
+            order[k - ex->consumed] = t[0];
+            rel[k - ex->consumed] = t[1];
+            order[k + 1 - ex->consumed] = t[2];
+            rel[k + 1 - ex->consumed] = t[3];
+            k += 2;
+          } else {
+            order[k - ex->consumed] = q[2 * (k & M)];
+            rel[k - ex->consumed] = q[2 * (k & M) + 1];
+            k += 1;
+          }
+        }
       }
       ex->bytes_d2h += 12 + (uint64_t)(nexec - ex->consumed) * 8;
       const auto tc0 = std::chrono::steady_clock::now();
+      P.stats[10] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tc0 - tw1).count();
       convert(ex, order, rel, nexec);
       P.stats[7] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                         std::chrono::steady_clock::now() - tc0).count();
@@ -372,6 +535,8 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
   }
   ex->processed = N;
   nexec_out = nexec;
+  P.stats[9] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tf0)
+                    .count();
   return FX_OK;
 }
 
@@ -653,6 +818,10 @@ fx_graph_executor* fx_graph_executor_new(uint8_t process_id, uint64_t shard_id, 
   if (ex->partial) ex->tier = FX_TIER_WIDE_HBM;
   const char* pe = std::getenv("FX_HANDLE_PERSIST");
   ex->persist_ok = !(pe && pe[0] == '0');
+  const char* ps = std::getenv("FX_HANDLE_STATS");
+  ex->ps.want_stats = ps && ps[0] == '1';
+  // the persistent mode's buffers (if they cannot be had, the batch tiers run)
+  if (ex->persist_ok && !ex->partial && persist_alloc(ex) != FX_OK) ex->persist_ok = false;
   if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ex;
     return nullptr;
@@ -662,8 +831,24 @@ fx_graph_executor* fx_graph_executor_new(uint8_t process_id, uint64_t shard_id, 
 
 void fx_graph_executor_free(fx_graph_executor* ex) {
   if (!ex) return;
-  persist_stop(ex);
-  if (ex->ps.stream) (void)hipStreamDestroy(ex->ps.stream);
+  const bool stopped = persist_stop(ex) == FX_OK;
+  if (ex->ps.stream) {
+    bool pooled = false;
+    if (stopped && ex->ps.ctl.p) {  // the kernel has exited: the resources go back to the pool
+      std::lock_guard<std::mutex> g(g_persist_pool_mu);
+      if (g_persist_pool->size() < kPersistPoolMax) {
+        auto* r = new PersistRes();
+        r->stream = ex->ps.stream;
+        r->ctl.swap(ex->ps.ctl);
+        r->rows.swap(ex->ps.rows);
+        r->out.swap(ex->ps.out);
+        r->state.swap(ex->ps.state);
+        g_persist_pool->push_back(r);
+        pooled = true;
+      }
+    }
+    if (!pooled) (void)hipStreamDestroy(ex->ps.stream);
+  }
   hipStream_t s = ex->stream;
   delete ex;  // DevBufs free first
   if (s) (void)hipStreamDestroy(s);
@@ -966,9 +1151,9 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
 
 int fx_graph_executor_parallel(void) { return 1; }
 
-int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out9) {
-  if (!ex || !out9) return FX_ERR_INVALID_ARG;
-  for (int i = 0; i < 9; ++i) out9[i] = ex->ps.stats[i];
+int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out12) {
+  if (!ex || !out12) return FX_ERR_INVALID_ARG;
+  for (int i = 0; i < 12; ++i) out12[i] = ex->ps.stats[i];
   return FX_OK;
 }
 

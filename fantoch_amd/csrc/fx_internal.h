@@ -85,7 +85,7 @@ bool profile_on();
 void split_profile_record(int which, bool end, hipStream_t s);
 // the drop-in handle's persistent executor kernel (graph_wave.hip, persist::)
 struct PersistArgs {
-  uint32_t* ctl;        // host-mapped control words (persist::P_*)
+  uint32_t* ctl;        // host-mapped control words (PERSIST_*)
   const uint32_t* rows; // host-mapped ring of published rows (persist::PRW words each)
   uint32_t* out;        // host-mapped ring of (order word, release step) pairs
   uint32_t* state;      // device: the wave tier's saved state of one stream
@@ -95,9 +95,21 @@ struct PersistArgs {
 constexpr uint32_t PERSIST_ROW_WORDS = 16;  // dot, hdr, 14 deps
 constexpr uint32_t PERSIST_CTL_WORDS = 64;
 constexpr uint32_t PERSIST_MB_DEPS = 13;    // deps a mailbox row carries
+constexpr uint32_t PERSIST_INLINE = 4;      // pairs a flush reports in the control words
+// Control words, four 64-byte lines.  Line 0 host -> device: PUB (rows
+// published), EXIT.  Line 1: the mailbox (tag, dot, hdr, 13 deps).  Line 2
+// device -> host: the status as two tagged 64-bit words {DONE, NEXEC | bit 31 on
+// an error} and {DONE2, ERR}, the timing words, RUN.  Line 3: up to
+// PERSIST_INLINE (order word, release step) pairs as tagged 64-bit words
+// {tag, order} {tag, release}.  Every device -> host word is a system-scope
+// store and the host checks the tags, so a flush with at most PERSIST_INLINE
+// pairs needs no release fence; a larger one goes through the out ring and one
+// fence before the status.
 enum : uint32_t { PERSIST_PUB = 0, PERSIST_EXIT = 1, PERSIST_MB = 16, PERSIST_DONE = 32, PERSIST_NEXEC = 33,
-                  PERSIST_ERR = 34, PERSIST_TCOMP = 35, PERSIST_TFENCE = 36, PERSIST_TPOLLS = 37,
-                  PERSIST_TRTT = 38, PERSIST_TCYC = 39, PERSIST_RUN = 47 };
+                  PERSIST_DONE2 = 34, PERSIST_ERR = 35, PERSIST_TCOMP = 36, PERSIST_TFENCE = 37,
+                  PERSIST_TPOLLS = 38, PERSIST_TRTT = 39, PERSIST_TCYC = 40, PERSIST_RUN = 47,
+                  PERSIST_PAIRS = 48 };
+constexpr uint32_t PERSIST_ERR_BIT = 0x80000000u;
 int persist_launch(const PersistArgs& a, hipStream_t stream);
 // fx_profile_slot_ms: events around one kernel slot's launch (graph_exec.hip)
 void profile_slot_record(uint32_t slot, bool end, hipStream_t s);

@@ -510,37 +510,48 @@ __global__ __launch_bounds__(64 * WPB) void k_graph_wave(KArgs a) {
 // plus a synchronisation per Add costs tens of microseconds, so instead ONE
 // wavefront stays resident and runs the wave tier's executor (the Wave above)
 // over Adds the host publishes in host-mapped memory:
-//   ctl[P_PUB]   rows published by the host (written after the rows)
-//   ctl[P_EXIT]  host asks the kernel to stop
-//   ctl[P_MB..]  mailbox: tag (= row index + 1), dot, hdr, 13 deps of the row of
+//   ctl[PUB]     rows published by the host (written after the rows)
+//   ctl[EXIT]    host asks the kernel to stop
+//   ctl[MB..]    mailbox: tag (= row index + 1), dot, hdr, 13 deps of the row of
 //                a one-Add flush, read in the same round trip as the doorbell
-//   ctl[P_DONE]  rows processed (written after one release fence that follows
-//                the outputs)
-//   ctl[P_NEXEC] / ctl[P_ERR]  executed count and status after those rows
-//   ctl[P_RUN]   1 while the kernel is resident
+//   ctl[DONE..]  rows processed, executed count, status: tagged 64-bit words
+//   ctl[PAIRS..] the flush's pairs when there are at most PERSIST_INLINE of
+//                them (tagged 64-bit words: no fence), else the out ring and
+//                one release fence before the status
+//   ctl[RUN]     1 while the kernel is resident
+// (fx_internal.h has the layout.)
 // rows: a ring of PR rows of PRW words (dot, hdr, up to 14 deps), row i in slot
 // i mod PR; out: a ring of PO (order word, release step) pairs, pair k in slot
-// k mod PO.  The kernel polls; with nothing published for 0.25 s (or on an
+// k mod PO.  The kernel polls; with nothing published for 20 ms (or on an
 // error, or when asked) it saves the executor state in the wave tier's state
 // layout and exits, and the host relaunches it on the next flush, so no
 // kernel outlives an idle or vanished host (a device-wide synchronisation
 // waits for it at most that long).
 namespace persist {
-// control words (host-mapped, fine-grained): line 0 host -> device, line 1 the
-// mailbox (the row of a one-Add flush), line 2 device -> host
-enum : uint32_t { P_PUB = 0, P_EXIT = 1, P_MB = 16, P_DONE = 32, P_NEXEC = 33, P_ERR = 34, P_TCOMP = 35,
-                  P_TFENCE = 36, P_TPOLLS = 37, P_TRTT = 38, P_TCYC = 39, P_RUN = 47 };
+enum : uint32_t { P_PUB = PERSIST_PUB, P_EXIT = PERSIST_EXIT, P_MB = PERSIST_MB, P_DONE = PERSIST_DONE,
+                  P_DONE2 = PERSIST_DONE2, P_TCOMP = PERSIST_TCOMP, P_RUN = PERSIST_RUN, P_PAIRS = PERSIST_PAIRS };
 constexpr uint32_t PRW = 16;                     // words per published row
 constexpr uint32_t MBD = 13;                     // deps a mailbox row carries (tag, dot, hdr, deps)
-constexpr uint64_t IDLE_TICKS = 25000000ull;     // s_memrealtime runs at 100 MHz: 0.25 s
+constexpr uint64_t IDLE_TICKS = 2000000ull;      // s_memrealtime runs at 100 MHz: 20 ms
 
+// The pairs of one flush are staged in LDS (the wave tier's unused input-chunk
+// words) and copied to the host ring by one lane-parallel store before the
+// fence; a flush with more than STAGE pairs writes the rest straight through.
+constexpr uint32_t STAGE = NPL * CH / 2;
 struct RingOut {
   uint32_t* ring = nullptr;  // host-mapped pairs
   uint32_t mask = 0;         // PO - 1
+  uint32_t* stage = nullptr;
+  uint32_t k0 = 0;           // the flush's first pair
   __device__ __forceinline__ void put(uint32_t k, uint32_t word, uint32_t rec, uint32_t cur) const {
-    uint32_t* q = ring + 2u * (k & mask);
-    q[0] = word;
-    q[1] = cur;
+    const uint32_t j = k - k0;
+    if (j < STAGE) {  // separate stores keep the LDS one an LDS store
+      stage[2u * j] = word;
+      stage[2u * j + 1u] = cur;
+    } else {
+      ring[2u * (k & mask)] = word;
+      ring[2u * (k & mask) + 1u] = cur;
+    }
   }
 };
 
@@ -550,6 +561,11 @@ __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
 }
 __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// a tagged 64-bit word {tag, v}: one single-copy-atomic system-scope store
+__device__ __forceinline__ void st_tag(uint32_t* p, uint32_t tag, uint32_t v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), (uint64_t)tag | ((uint64_t)v << 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
@@ -565,6 +581,7 @@ __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
   e.lds = smem;
   e.out.ring = a.out;
   e.out.mask = a.out_slots - 1u;
+  e.out.stage = smem + L_IN;
   uint32_t* gst = a.state;
   if (a.init) {
     for (uint32_t q = lane; q < L_IN; q += 64) e.lds[q] = 0;
@@ -607,7 +624,7 @@ __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
       continue;
     }
     t_rtt = (uint32_t)(tp1 - tp0);
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the rows after the doorbell
+    e.out.k0 = e.k;
     if (pub == done + 1u && rl(v, P_MB) == pub) {
       // a one-Add flush: its row came with the doorbell (the host writes the
       // mailbox line before the doorbell; a load that saw the new doorbell but
@@ -617,6 +634,7 @@ __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
       e.step_start(done, d, h, lane < MBD ? depj : 0u, MBD, a.at_commit != 0);
       if (e.phase != PH_IDLE) e.run_slow();
     } else {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the rows after the doorbell
       // rows [done, pub) from the ring, four per load: lane 16 r + w reads word w of row i + r
       for (uint32_t i = done; i < pub && !e.err; i += 4) {
         const uint32_t r4 = lane >> 4, w = lane & 15u;
@@ -630,16 +648,28 @@ __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
         }
       }
     }
-    // the pairs (plain stores), the counters, then ONE release fence before
-    // the done word (every lane stores the same word to the same address:
-    // one request, and no exec-mask split around the fence)
+    // the flush's pairs: at most PERSIST_INLINE go into the control words as
+    // tagged words (lane 2j: {pub, order word j}, lane 2j + 1: {pub, release
+    // step j}) and need no fence; more go to the out ring (lane j: pair j of
+    // the staged ones) and one release fence orders them before the status
+    const uint32_t np = e.k - e.out.k0;
     const uint64_t tc = __builtin_amdgcn_s_memrealtime();
     const uint32_t cyc = (uint32_t)(__builtin_amdgcn_s_memtime() - cy1);
-    if (lane < 7u)
-      ctl[P_NEXEC + lane] = lane == 0 ? e.k : lane == 1 ? e.err : lane == 2 ? (uint32_t)(tc - tp1)
-                          : lane == 3 ? t_fence : lane == 4 ? t_polls : lane == 5 ? t_rtt : cyc;
-    __threadfence_system();
-    st_sys(ctl + P_DONE, pub);
+    if (np <= PERSIST_INLINE) {
+      if (lane < 2u * np) st_tag(ctl + P_PAIRS + 2u * lane, pub, e.out.stage[lane]);
+    } else {
+      const uint32_t ns = min(np, STAGE);
+      for (uint32_t j = lane; j < ns; j += 64) {
+        const uint2 pr = *reinterpret_cast<const uint2*>(e.out.stage + 2u * j);
+        *reinterpret_cast<uint2*>(a.out + 2u * ((e.out.k0 + j) & e.out.mask)) = pr;
+      }
+      __threadfence_system();
+    }
+    if (lane == 0) st_tag(ctl + P_DONE, pub, e.k | (e.err ? PERSIST_ERR_BIT : 0u));
+    if (lane == 1) st_tag(ctl + P_DONE2, pub, e.err);
+    if (lane >= 2u && lane < 7u)  // timing words (diagnostics)
+      st_sys(ctl + P_TCOMP + lane - 2u, lane == 2 ? (uint32_t)(tc - tp1) : lane == 3 ? t_fence
+                                      : lane == 4 ? t_polls : lane == 5 ? t_rtt : cyc);
     done = pub;
     idle0 = __builtin_amdgcn_s_memrealtime();
     t_fence = (uint32_t)(idle0 - tc);

@@ -24,6 +24,16 @@ class GraphExecutor:
                                else _lib.FX_ERR_INVALID_ARG, "fx_graph_executor_new")
         self._h = h
         self.n = n
+        # per-handle call buffers: the simulator's pattern calls handle_add and
+        # a drain after every commit, so neither allocates ctypes arrays per call
+        self._add = lib.fx_graph_executor_handle_add
+        self._drain = lib.fx_graph_executor_drain_dots
+        self._karr = (ctypes.c_uint32 * 16)()
+        self._darr = (CDot * 64)()
+        self._dbuf = (CDot * 256)()
+        self._dstart = (ctypes.c_uint8 * 256)()
+        self._got = ctypes.c_uint32()
+        self._gotref = ctypes.byref(self._got)
 
     def close(self):
         if self._h:
@@ -46,12 +56,25 @@ class GraphExecutor:
     def handle_add(self, dot, rifl, keys, deps, time_ms, read_only=False):
         """handle(GraphExecutionInfo::Add{dot, cmd, deps}, time)."""
         keys = list(keys)
-        karr = (ctypes.c_uint32 * max(len(keys), 1))(*keys)
         deps = list(deps)
-        darr = (CDot * max(len(deps), 1))(*[CDot(int(s), int(q)) for s, q in deps])
-        check(_lib.load().fx_graph_executor_handle_add(
-            self._h, CDot(*dot), CRifl(*rifl), karr, len(keys), 1 if read_only else 0, darr,
-            len(deps), int(time_ms)), "handle_add")
+        if len(keys) <= 16:
+            karr = self._karr
+            for i, k in enumerate(keys):
+                karr[i] = k
+        else:
+            karr = (ctypes.c_uint32 * len(keys))(*keys)
+        if len(deps) <= 64:
+            darr = self._darr
+            for i, (s, q) in enumerate(deps):
+                d = darr[i]
+                d.source = s
+                d.seq = q
+        else:
+            darr = (CDot * len(deps))(*[CDot(int(s), int(q)) for s, q in deps])
+        st = self._add(self._h, CDot(*dot), CRifl(*rifl), karr, len(keys), 1 if read_only else 0, darr,
+                       len(deps), int(time_ms))
+        if st:
+            check(st, "handle_add")
 
     # ---- partial replication (shard_count > 1, graph/mod.rs:82-406)
     def handle_add_sharded(self, dot, rifl, keys, deps, shards, time_ms, read_only=False, cmd_shards=0):
@@ -131,15 +154,16 @@ class GraphExecutor:
     def drain_dots(self):
         """Executed dots in execution order: list of ((source, seq), scc_start)."""
         out = []
-        buf = (CDot * 256)()
-        start = (ctypes.c_uint8 * 256)()
-        got = ctypes.c_uint32()
+        buf, start, got = self._dbuf, self._dstart, self._got
         while True:
-            check(_lib.load().fx_graph_executor_drain_dots(self._h, buf, start, 256,
-                                                           ctypes.byref(got)), "drain_dots")
-            for i in range(got.value):
-                out.append(((buf[i].source, buf[i].seq), bool(start[i])))
-            if got.value < 256:
+            st = self._drain(self._h, buf, start, 256, self._gotref)
+            if st:
+                check(st, "drain_dots")
+            n = got.value
+            for i in range(n):
+                d = buf[i]
+                out.append(((d.source, d.seq), bool(start[i])))
+            if n < 256:
                 return out
 
     def metrics(self, kind):

@@ -445,12 +445,14 @@ int fx_graph_executor_parallel(void);
 /* Host<->device bytes this handle has moved so far (not in the reference; lets
  * a test check that draining after every Add moves bytes linear in the Adds). */
 int fx_graph_executor_transfer_stats(const fx_graph_executor* ex, uint64_t* h2d, uint64_t* d2h);
-/* Persistent-mode timing (diagnostics, tools/handle_latency): out9 = flushes,
+/* Persistent-mode timing (diagnostics, tools/handle_latency): out12 = flushes,
  * host wait from doorbell to done (ns, summed), the kernel's summed compute and
  * release-fence times, polls and poll round trips (100 MHz ticks), the host's
- * row preparation and order conversion (ns, summed), and the compute in
- * shader-clock cycles (summed). */
-int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out9);
+ * row preparation and order conversion (ns, summed), the compute in
+ * shader-clock cycles (summed), the host's whole flush, its reads of the
+ * done / timing words and pairs after the wait, and its work before the
+ * publish (ns, summed). */
+int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out12);
 
 /* ------------------------------------------------------- quorum sizes */
 #define FX_PROTOCOL_ATLAS 0u
