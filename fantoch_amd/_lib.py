@@ -272,7 +272,7 @@ SIGNATURES = [
       ctypes.c_uint32, u32p]),
     ("fx_graph_executor_parallel", ctypes.c_int, []),
     ("fx_graph_executor_transfer_stats", ctypes.c_int, [ctypes.c_void_p, u64p, u64p]),
-    ("fx_graph_executor_persist_stats", ctypes.c_int, [ctypes.c_void_p, u64p]),
+    ("fx_graph_executor_persist_stats", ctypes.c_int, [ctypes.c_void_p, u64p, ctypes.c_uint32]),
     ("fx_sim_plan", ctypes.c_int,
      [ctypes.POINTER(SimSpec), ctypes.c_uint32, ctypes.c_uint32, u32p]),
     ("fx_sim_plan_large", ctypes.c_int,

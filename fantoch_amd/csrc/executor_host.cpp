@@ -203,7 +203,7 @@ struct fx_graph_executor {
     static constexpr uint32_t ROWS = 4096, OUT = 8192;
     // fx_graph_executor_persist_stats: flushes, host wait (ns), and the
     // kernel's compute / fence ticks, polls and poll round trips (100 MHz)
-    uint64_t stats[12] = {};  // + host prep / convert (ns), compute shader cycles, flush total / post-wait reads / pre-publish (ns)
+    uint64_t stats[FX_PERSIST_STATS] = {};  // + host prep / convert (ns), compute shader cycles, flush total / post-wait reads / pre-publish (ns)
     bool want_stats = false;  // FX_HANDLE_STATS=1: the kernel's fence / poll / cycle words too
   } ps;
   bool persist_ok = true;
@@ -396,6 +396,7 @@ int persist_launch_now(fx_graph_executor* ex, bool init) {
 int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
   const auto tf0 = std::chrono::steady_clock::now();
   const uint32_t N = (uint32_t)ex->dots.size();
+  if (N >= (1u << 28)) return FX_ERR_CAPACITY;  // the kernel's LDS doorbell word holds row counts < 2^29
   for (uint32_t i = ex->ps.pub; i < N; ++i)
     if (ex->deps[i].size() > fx::WAVE_MAX_DEPS) return FX_ERR_CAPACITY;
   auto& P = ex->ps;
@@ -486,7 +487,10 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
       P.stats[3] += t[1];
       P.stats[4] += t[2];
       P.stats[5] += t[3];
-      P.stats[8] += pctl(ex)[fx::PERSIST_TCYC];
+      ld16(pctl(ex) + fx::PERSIST_TCYC, t);
+      P.stats[8] += t[0];
+      P.stats[12] += t[1];
+      P.stats[13] += t[2];
     }
     nexec = w[1];
     P.pub = hi;
@@ -1151,9 +1155,9 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
 
 int fx_graph_executor_parallel(void) { return 1; }
 
-int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out12) {
-  if (!ex || !out12) return FX_ERR_INVALID_ARG;
-  for (int i = 0; i < 12; ++i) out12[i] = ex->ps.stats[i];
+int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out, uint32_t n) {
+  if (!ex || (!out && n)) return FX_ERR_INVALID_ARG;
+  for (uint32_t i = 0; i < n && i < FX_PERSIST_STATS; ++i) out[i] = ex->ps.stats[i];
   return FX_OK;
 }
 

@@ -107,7 +107,8 @@ constexpr uint32_t PERSIST_INLINE = 4;      // pairs a flush reports in the cont
 // fence before the status.
 enum : uint32_t { PERSIST_PUB = 0, PERSIST_EXIT = 1, PERSIST_MB = 16, PERSIST_DONE = 32, PERSIST_NEXEC = 33,
                   PERSIST_DONE2 = 34, PERSIST_ERR = 35, PERSIST_TCOMP = 36, PERSIST_TFENCE = 37,
-                  PERSIST_TPOLLS = 38, PERSIST_TRTT = 39, PERSIST_TCYC = 40, PERSIST_RUN = 47,
+                  PERSIST_TPOLLS = 38, PERSIST_TRTT = 39, PERSIST_TCYC = 40, PERSIST_TITER = 41,
+                  PERSIST_TSTEP = 42, PERSIST_RUN = 47,
                   PERSIST_PAIRS = 48 };
 constexpr uint32_t PERSIST_ERR_BIT = 0x80000000u;
 int persist_launch(const PersistArgs& a, hipStream_t stream);

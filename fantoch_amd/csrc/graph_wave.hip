@@ -533,6 +533,14 @@ enum : uint32_t { P_PUB = PERSIST_PUB, P_EXIT = PERSIST_EXIT, P_MB = PERSIST_MB,
 constexpr uint32_t PRW = 16;                     // words per published row
 constexpr uint32_t MBD = 13;                     // deps a mailbox row carries (tag, dot, hdr, deps)
 constexpr uint64_t IDLE_TICKS = 2000000ull;      // s_memrealtime runs at 100 MHz: 20 ms
+// Poller waves: a poll of host memory takes a round trip (~1.25 us), so one
+// wave that polls and then waits samples the doorbell once per round trip.
+// NPOLL waves of the workgroup poll instead, each in its own time slot of
+// SLOT_TICKS (100 MHz ticks; NPOLL slots > one round trip, so no poller misses
+// its slot), and hand what they read to the executor wave through LDS: the
+// doorbell is sampled every SLOT_TICKS (0.4 us) and the executor waits on LDS.
+constexpr uint32_t NPOLL = 4;
+constexpr uint64_t SLOT_TICKS = 40;
 
 // The pairs of one flush are staged in LDS (the wave tier's unused input-chunk
 // words) and copied to the host ring by one lane-parallel store before the
@@ -568,9 +576,57 @@ __device__ __forceinline__ void st_tag(uint32_t* p, uint32_t tag, uint32_t v) {
                      __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
+// Poller wave i: in each of its slots, one load of the doorbell and mailbox
+// lines; a new doorbell value goes to LDS slot i and then into `latest`
+// (doorbell << 3 | i, an LDS max), an exit request into `stop`.  Leaves when the
+// executor sets `stop`.
+__device__ void poller(uint32_t i, uint32_t lane, const uint32_t* ctl, uint32_t* slot, uint32_t* stamp,
+                       uint32_t* latest, uint32_t* stop) {
+  uint32_t last = 0xFFFFFFFFu;
+  auto slot_of = [](uint64_t t) { return (uint32_t)((t / SLOT_TICKS) % NPOLL); };
+  while (__hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+    uint64_t t = __builtin_amdgcn_s_memrealtime();
+    while (slot_of(t) != i) {
+      __builtin_amdgcn_s_sleep(1);
+      t = __builtin_amdgcn_s_memrealtime();
+    }
+    const uint32_t v = lane < 32u ? ld_sys(ctl + lane) : 0u;
+    const uint32_t pub = rl(v, P_PUB);
+    if (rl(v, P_EXIT)) {
+      __hip_atomic_store(stop, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      break;
+    }
+    if (pub != last) {
+      if (lane < 32u) slot[lane] = v;
+      if (lane == 0) {
+        *stamp = (uint32_t)t;
+        __hip_atomic_fetch_max(latest, (pub << 3) | i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      last = pub;
+    }
+    do {  // one poll per slot
+      __builtin_amdgcn_s_sleep(1);
+      t = __builtin_amdgcn_s_memrealtime();
+    } while (slot_of(t) == i);
+  }
+}
+
+__global__ __launch_bounds__(64 * (1 + NPOLL)) void k_handle_persist(PersistArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t smem[LW];
-  const uint32_t lane = threadIdx.x;
+  __shared__ uint32_t ps_slot[NPOLL * 32], ps_stamp[NPOLL], ps_latest, ps_stop;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = uni(threadIdx.x >> 6);
+  uint32_t* ctl = a.ctl;
+  uint32_t done = a.done0;
+  if (threadIdx.x == 0) {
+    ps_latest = done << 3;
+    ps_stop = 0;
+  }
+  __syncthreads();
+  if (wv != 0) {
+    poller(wv - 1u, lane, ctl, ps_slot + (wv - 1u) * 32u, ps_stamp + (wv - 1u), &ps_latest, &ps_stop);
+    return;
+  }
   Wave<RingOut> e;
   e.lid = lane;
   e.lbit = 1ull << lane;
@@ -601,29 +657,26 @@ __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
     e.err = uni(gst[S_SCAL + 5]);
     e.epoch = uni(gst[S_SCAL + 6]);
   }
-  uint32_t* ctl = a.ctl;
-  uint32_t done = a.done0;
   uint64_t idle0 = __builtin_amdgcn_s_memrealtime();
-  // timing words for tools/handle_latency (100 MHz ticks): the last poll's
-  // round trip, the polls before the last doorbell, the last flush's compute
-  // and its release fence
-  uint32_t t_rtt = 0, t_polls = 0, t_fence = 0;
+  // timing words for tools/handle_latency (100 MHz ticks): the age of the
+  // sample that carried the last doorbell, the LDS checks before it, the last
+  // flush's compute and its publish
+  uint32_t t_rtt = 0, t_polls = 0, t_fence = 0, t_iter = 0, t_step = 0;
   while (!e.err) {
-    // one round trip: the doorbell line and the mailbox line (lane w: word w)
-    const uint64_t tp0 = __builtin_amdgcn_s_memrealtime();
-    const uint32_t v = lane < 32u ? ld_sys(ctl + lane) : 0u;
-    const uint32_t pub = rl(v, P_PUB);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // (timing: the load has returned)
+    const uint32_t lv = __hip_atomic_load(&ps_latest, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t pub = uni(lv) >> 3;
     const uint64_t tp1 = __builtin_amdgcn_s_memrealtime();
     const uint64_t cy1 = __builtin_amdgcn_s_memtime();
-    if (rl(v, P_EXIT)) break;
     ++t_polls;
     if (pub == done) {
+      if (__hip_atomic_load(&ps_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
       if (tp1 - idle0 > IDLE_TICKS) break;
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    t_rtt = (uint32_t)(tp1 - tp0);
+    const uint32_t si = uni(lv) & 7u;
+    const uint32_t v = lane < 32u ? ps_slot[si * 32u + lane] : 0u;
+    t_rtt = (uint32_t)tp1 - ps_stamp[si];
     e.out.k0 = e.k;
     if (pub == done + 1u && rl(v, P_MB) == pub) {
       // a one-Add flush: its row came with the doorbell (the host writes the
@@ -632,7 +685,14 @@ __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
       const uint32_t d = rl(v, P_MB + 1u), h = rl(v, P_MB + 2u);
       const uint32_t depj = gather(v, (P_MB + 3u + lane) & 63u);
       e.step_start(done, d, h, lane < MBD ? depj : 0u, MBD, a.at_commit != 0);
-      if (e.phase != PH_IDLE) e.run_slow();
+      t_step = (uint32_t)(__builtin_amdgcn_s_memtime() - cy1);
+      while (e.phase != PH_IDLE) {  // run_slow, counted
+        if (e.phase == PH_DFS) e.dfs_iter();
+        else if (e.phase == PH_TRY) e.try_iter();
+        else e.check_iter();
+        if (e.err) e.phase = PH_IDLE;
+        ++t_iter;
+      }
     } else {
       __atomic_thread_fence(__ATOMIC_ACQUIRE);  // the rows after the doorbell
       // rows [done, pub) from the ring, four per load: lane 16 r + w reads word w of row i + r
@@ -655,9 +715,7 @@ __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
     const uint32_t np = e.k - e.out.k0;
     const uint64_t tc = __builtin_amdgcn_s_memrealtime();
     const uint32_t cyc = (uint32_t)(__builtin_amdgcn_s_memtime() - cy1);
-    if (np <= PERSIST_INLINE) {
-      if (lane < 2u * np) st_tag(ctl + P_PAIRS + 2u * lane, pub, e.out.stage[lane]);
-    } else {
+    if (np > PERSIST_INLINE) {
       const uint32_t ns = min(np, STAGE);
       for (uint32_t j = lane; j < ns; j += 64) {
         const uint2 pr = *reinterpret_cast<const uint2*>(e.out.stage + 2u * j);
@@ -665,11 +723,20 @@ __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
       }
       __threadfence_system();
     }
-    if (lane == 0) st_tag(ctl + P_DONE, pub, e.k | (e.err ? PERSIST_ERR_BIT : 0u));
-    if (lane == 1) st_tag(ctl + P_DONE2, pub, e.err);
-    if (lane >= 2u && lane < 7u)  // timing words (diagnostics)
+    {  // one store: lane 0 the status, lane 1 the error word, lanes 2.. the inline pairs
+      const uint32_t m = lane - 2u;
+      const bool pair = lane >= 2u && np <= PERSIST_INLINE && m < 2u * np;
+      const uint32_t val = lane == 0 ? (e.k | (e.err ? PERSIST_ERR_BIT : 0u)) : lane == 1 ? e.err
+                         : pair ? e.out.stage[m] : 0u;
+      uint32_t* dst = lane == 0 ? ctl + P_DONE : lane == 1 ? ctl + P_DONE2 : ctl + P_PAIRS + 2u * m;
+      if (lane < 2u || pair) st_tag(dst, pub, val);
+    }
+    if (lane >= 2u && lane < 9u)  // timing words (diagnostics)
       st_sys(ctl + P_TCOMP + lane - 2u, lane == 2 ? (uint32_t)(tc - tp1) : lane == 3 ? t_fence
-                                      : lane == 4 ? t_polls : lane == 5 ? t_rtt : cyc);
+                                      : lane == 4 ? t_polls : lane == 5 ? t_rtt : lane == 6 ? cyc
+                                      : lane == 7 ? t_iter : t_step);
+    t_iter = 0;
+    t_step = 0;
     done = pub;
     idle0 = __builtin_amdgcn_s_memrealtime();
     t_fence = (uint32_t)(idle0 - tc);
@@ -693,6 +760,7 @@ __global__ __launch_bounds__(64) void k_handle_persist(PersistArgs a) {
     gst[S_SCAL + 5] = e.err;
     gst[S_SCAL + 6] = e.epoch;
   }
+  __hip_atomic_store(&ps_stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // the pollers leave
   __threadfence_system();
   if (lane == 0) st_sys(ctl + P_RUN, 0u);
 }
@@ -704,7 +772,7 @@ int persist_launch(const PersistArgs& a, hipStream_t stream) {
   if ((a.row_slots & (a.row_slots - 1u)) || (a.out_slots & (a.out_slots - 1u)) || !a.ctl || !a.rows || !a.out ||
       !a.state)
     return FX_ERR_INVALID_ARG;
-  hipLaunchKernelGGL(wav::persist::k_handle_persist, dim3(1), dim3(64), 0, stream, a);
+  hipLaunchKernelGGL(wav::persist::k_handle_persist, dim3(1), dim3(64 * (1 + wav::persist::NPOLL)), 0, stream, a);
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 

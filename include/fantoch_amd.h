@@ -445,14 +445,17 @@ int fx_graph_executor_parallel(void);
 /* Host<->device bytes this handle has moved so far (not in the reference; lets
  * a test check that draining after every Add moves bytes linear in the Adds). */
 int fx_graph_executor_transfer_stats(const fx_graph_executor* ex, uint64_t* h2d, uint64_t* d2h);
-/* Persistent-mode timing (diagnostics, tools/handle_latency): out12 = flushes,
- * host wait from doorbell to done (ns, summed), the kernel's summed compute and
- * release-fence times, polls and poll round trips (100 MHz ticks), the host's
- * row preparation and order conversion (ns, summed), the compute in
- * shader-clock cycles (summed), the host's whole flush, its reads of the
- * done / timing words and pairs after the wait, and its work before the
- * publish (ns, summed). */
-int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out12);
+/* Persistent-mode timing (diagnostics, tools/handle_latency): the first n of
+ * FX_PERSIST_STATS counters, summed over the flushes: [0] flushes, [1] host wait
+ * from doorbell to status (ns), [2] the kernel's compute, [3] its publish, [4]
+ * polls, [5] poll round trips (100 MHz ticks), [6] the host's row preparation,
+ * [7] order conversion (ns), [8] the compute in shader-clock cycles, [9] the
+ * host's whole flush, [10] its reads after the wait, [11] its work before the
+ * publish (ns), [12] executor iterations (DFS edges / frame pops, try and
+ * check steps), [13] cycles in the Add's first step. The kernel's words are
+ * read only with FX_HANDLE_STATS=1 in the environment. */
+#define FX_PERSIST_STATS 14
+int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out, uint32_t n);
 
 /* ------------------------------------------------------- quorum sizes */
 #define FX_PROTOCOL_ATLAS 0u

@@ -86,18 +86,19 @@ int main(int argc, char** argv) {
       }
     }
     const auto t1 = std::chrono::steady_clock::now();
-    uint64_t ps[12];
-    fx_graph_executor_persist_stats(ex, ps);
+    uint64_t ps[FX_PERSIST_STATS];
+    fx_graph_executor_persist_stats(ex, ps, FX_PERSIST_STATS);
     if (r == reps && ps[0]) {
       const double f = (double)ps[0];
       std::printf("{\"persist\": {\"flushes\": %llu, \"host_wait_us\": %.3f, \"compute_us\": %.3f, \"fence_us\": %.3f, "
                   "\"polls_per_flush\": %.2f, \"poll_rtt_us\": %.3f, \"host_prep_us\": %.3f, \"host_convert_us\": %.3f, "
                   "\"handle_add_us\": %.3f, \"compute_mhz\": %.0f, \"flush_us\": %.3f, \"drain_call_us\": %.3f, "
-                  "\"post_wait_reads_us\": %.3f, \"pre_publish_us\": %.3f}}\n",
+                  "\"post_wait_reads_us\": %.3f, \"pre_publish_us\": %.3f, \"iters_per_flush\": %.2f, "
+                  "\"step_cycles\": %.0f, \"compute_cycles\": %.0f}}\n",
                   (unsigned long long)ps[0], ps[1] / f / 1e3, ps[2] / f / 100.0, ps[3] / f / 100.0, ps[4] / f,
                   ps[5] / f / 100.0, ps[6] / f / 1e3, ps[7] / f / 1e3, add_ns / adds.size() / H / 1e3,
                   ps[2] ? 100.0 * (double)ps[8] / (double)ps[2] : 0.0, ps[9] / f / 1e3, drain_ns / adds.size() / H / 1e3,
-                  ps[10] / f / 1e3, ps[11] / f / 1e3);
+                  ps[10] / f / 1e3, ps[11] / f / 1e3, ps[12] / f, ps[13] / f, ps[8] / f);
     }
     for (auto h : hs) fx_graph_executor_free(h);
     if (r > 0) us.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count() / adds.size() / H);
