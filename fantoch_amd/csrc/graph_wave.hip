@@ -92,6 +92,7 @@ struct Wave {
   // lane-owned slot fields (slot = lid), DFS frame (depth = lid), clock (source = lid + 1)
   uint32_t sdot = 0, srec = 0, swait = 0, stl = 0, sfr = 0;
   uint32_t cf = 0, cw = 0;
+  uint32_t fdep = 0;  // lane j < C: cached dep j of the DFS's current vertex fv
   // wave-uniform state
   uint64_t occ = 0, wmask = 0, tmask = 0;
   uint32_t k = 0, err = 0, epoch = 1, nwl = 0, cur = 0;
@@ -190,6 +191,10 @@ struct Wave {
     clk_add(d);
   }
 
+  // the current vertex's cached deps into lanes 0..C-1 (one LDS read per
+  // vertex entered or returned to; its latency overlaps the rest of the step)
+  __device__ __forceinline__ void load_fdep() { fdep = lid < C ? cache(fv, lid) : 0u; }
+
   __device__ __forceinline__ void dfs_start(uint32_t r, bool intry) {
     root = r;
     in_try = intry;
@@ -200,6 +205,7 @@ struct Wave {
     if (lid == r) stl = tmk(1, 1, tep(tr));
     nfr = 0;
     fv = r;
+    load_fdep();
     fdi = 0;
     fnc = rl(srec, r) >> 26;
     phase = PH_DFS;
@@ -265,7 +271,7 @@ struct Wave {
   // one DFS edge or one frame pop (TarjanSCCFinder::strong_connect, iterative)
   __device__ __forceinline__ void dfs_iter() {
     if (fdi < fnc) {
-      const uint32_t dep = uni(cache(fv, fdi));
+      const uint32_t dep = rl(fdep, fdi);
       ++fdi;
       if (contains_u(dep)) return;  // executed (tarjan.rs:128-145)
       const int x = find(dep);
@@ -281,6 +287,7 @@ struct Wave {
         if (lid == nfr) sfr = fv | (fdi << 8);
         ++nfr;
         fv = (uint32_t)x;
+        load_fdep();
         fdi = 0;
         fnc = rl(srec, fv) >> 26;
       } else {  // visited and on the stack (tarjan.rs:215-225)
@@ -301,6 +308,7 @@ struct Wave {
       --nfr;
       const uint32_t f = rl(sfr, nfr);  // back in the parent (tarjan.rs:211)
       fv = f & 0xFFu;
+      load_fdep();
       fdi = f >> 8;
       fnc = rl(srec, fv) >> 26;
       const uint32_t tp = rl(stl, fv);
@@ -355,11 +363,13 @@ struct Wave {
       ++k;
       return;
     }
+    // the clock lookups (two ds_bpermute) are issued first so that their LDS
+    // latency overlaps the checks; lane j - 1's dep comes by DPP (wave_shr:1)
+    const bool exd = contains_v(depj);  // every lane active: ds_bpermute reads 0 from inactive lanes
+    const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)depj, 0x138, 0xF, 0xF, false);
     if (occ && find(d) >= 0) { err = FX_ERR_DOUBLE_INDEX; return; }  // mod.rs:233-237
     const bool valid = lid < nd;
-    const uint32_t prev = gather(depj, (lid - 1u) & 63u);
     if (bal(valid && lid > 0 && depj <= prev)) { err = FX_ERR_DEPS_UNSORTED; return; }
-    const bool exd = contains_v(depj);  // every lane active: ds_bpermute reads 0 from inactive lanes
     const bool keep = valid && depj != d && !exd;
     if (kind == FX_KIND_INDEX_ONLY) {
       insert_vertex(i, d, keep, depj);
