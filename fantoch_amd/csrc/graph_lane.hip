@@ -791,7 +791,7 @@ static uint32_t decode(const uint32_t* block, uint32_t lane, uint32_t* dots, uin
 }
 
 // drift bound of k_graph_lane in blocks (FX_LANE_DRIFT overrides; 0 = unbounded)
-constexpr uint32_t DEFAULT_DRIFT = 4;
+constexpr uint32_t DEFAULT_DRIFT = 3;
 
 // instantiation for a batch: sources rounded to 5 / 8, deps to 3 / 5 / 8
 #define FX_LANE_DISPATCH(F, ...)                                         \
