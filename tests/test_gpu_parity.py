@@ -514,6 +514,64 @@ def _drain_run(stream, n, every, env=None, sleep_at=None):
     return out
 
 
+def test_executor_persistent_handles_interleaved_one_thread(gpu):
+    """The simulator drives one executor per process from one thread
+    (runner.rs:406-424): six persistent handles fed in turn, each drained after
+    every Add.  Each handle's kernel has a hardware queue of its own; on shared
+    queues a resident kernel holds back the next handle's until its idle exit
+    (20 ms per switch here).  Orders equal the oracle's, and quickly."""
+    import time
+    streams = []
+    for seed in range(6):
+        p = fs.synth_params(seed=40 + seed, n=5, instances=1, cmds=120, window=8, cycle_pct=30, conflicts=(50,))
+        streams.append(fs.synth_host(p).stream(0)[:500])
+    exps = []
+    for st in streams:
+        g = oracle_lib.Graph(1, 5)
+        for (dot, deps, t, _kind) in st:
+            g.handle_add(dot, deps, t)
+        exps.append([d for d, _, _ in g.drain()])
+    hs = [GraphExecutor(1, 0, 5, monitor=False) for _ in streams]
+    got = [[] for _ in streams]
+    t0 = time.perf_counter()
+    for i in range(max(len(st) for st in streams)):
+        for h, st, out in zip(hs, streams, got):
+            if i < len(st):
+                dot, deps, t, _kind = st[i]
+                h.handle_add(dot, dot, [0], deps, t)
+                out += [d for d, _ in h.drain_dots()]
+    dt = time.perf_counter() - t0
+    for h, out in zip(hs, got):
+        out += [d for d, _ in h.drain_dots()]
+        h.close()
+    assert got == exps
+    assert dt < 5.0, dt
+
+
+def test_executor_handles_made_one_after_another(gpu):
+    """A freed handle's persistent resources (its hardware queue, mapped
+    buffers, state block) go to a pool the next handle takes from: a program
+    that makes a handle per case (the reference's shuffle tests,
+    graph/mod.rs:1045-1113) pays for the queue once."""
+    import time
+    p = fs.synth_params(seed=5, n=3, instances=1, cmds=20, window=4, cycle_pct=30, conflicts=(50,))
+    st = fs.synth_host(p).stream(0)[:40]
+    g = oracle_lib.Graph(1, 3)
+    for (dot, deps, t, _kind) in st:
+        g.handle_add(dot, deps, t)
+    exp = [d for d, _, _ in g.drain()]
+    t0 = time.perf_counter()
+    for _ in range(60):
+        h = GraphExecutor(1, 0, 3, monitor=False)
+        out = []
+        for (dot, deps, t, _kind) in st:
+            h.handle_add(dot, dot, [0], deps, t)
+            out += [d for d, _ in h.drain_dots()]
+        h.close()
+        assert out == exp
+    assert time.perf_counter() - t0 < 10.0
+
+
 def test_executor_persistent_mode_equals_batch_tiers_and_oracle(gpu):
     """The handle's persistent mode (one resident wavefront running the wave
     tier over Adds published in host-mapped memory, drained after every Add as
