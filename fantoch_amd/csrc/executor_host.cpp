@@ -1133,7 +1133,10 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
   if (ex->ps.active) {  // the persistent kernel's state, saved when it stops
     if (persist_stop(ex)) return FX_ERR_HIP;
     std::vector<uint32_t> block(fx::wave_state_words_per_stream());
-    if (hipMemcpy(block.data(), ex->ps.state.p, block.size() * 4, hipMemcpyDeviceToHost) != hipSuccess)
+    // on the handle's own stream: a null-stream copy would also wait for other
+    // handles' resident kernels (their streams are blocking ones)
+    if (hipMemcpyAsync(block.data(), ex->ps.state.p, block.size() * 4, hipMemcpyDeviceToHost, ex->ps.stream) ||
+        hipStreamSynchronize(ex->ps.stream))
       return FX_ERR_HIP;
     std::vector<uint32_t> d(64), w(64);
     const uint32_t c = fx::decode_pending(FX_TIER_WAVE, block.data(), 0, d.data(), w.data(), 64);
