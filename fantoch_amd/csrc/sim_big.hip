@@ -328,7 +328,9 @@ struct Big {
     return e;
   }
   // removes the minimum event; returns its entry (NONE if the queue is empty)
-  __device__ __forceinline__ uint32_t pop_event(uint32_t& hi_out) {
+  // and its info / arg words, read with the group's keys (one round trip: the
+  // event loop's next loads depend on them)
+  __device__ __forceinline__ uint32_t pop_event(uint32_t& hi_out, uint32_t& info_out, uint32_t& arg_out) {
     uint32_t bh = gh[0], bl = gl[0], bk = 0;
 #pragma unroll
     for (uint32_t k = 1; k < NG; ++k) {
@@ -345,7 +347,10 @@ struct Big {
     const uint32_t grp = rl(bk, ln) * 64u + ln;
     const uint32_t e0 = grp * 64u + lid;
     uint32_t kh = W(g.o_kh, e0), kl = W(g.o_kl, e0);
+    const uint32_t vi = W(g.o_inf, e0), va = W(g.o_arg, e0);
     const uint32_t j = ctz64(bal(kh == th && kl == tl));
+    info_out = rl(vi, j);
+    arg_out = rl(va, j);
     if (lid == j) {
       kh = NONE;
       kl = NONE;
@@ -1540,7 +1545,8 @@ __global__ __launch_bounds__(64, 3) void k_simx(ArgsX a) {
 #ifdef FX_SIM_PROFILE
     const uint64_t pt0 = __builtin_amdgcn_s_memtime();
 #endif
-    const uint32_t e = s.pop_event(hi);
+    uint32_t info = 0, arg = 0;
+    const uint32_t e = s.pop_event(hi, info, arg);
 #ifdef FX_SIM_PROFILE
     const uint64_t pt1 = __builtin_amdgcn_s_memtime();
     s.prof[PF_POP] += pt1 - pt0;
@@ -1556,7 +1562,6 @@ __global__ __launch_bounds__(64, 3) void k_simx(ArgsX a) {
       break;
     }
     s.now = t;
-    const uint32_t info = s.rd(M[g.o_inf + e]), arg = s.rd(M[g.o_arg + e]);
     const uint32_t kind = info & 15u, from = (info >> 4) & 15u, to = (info >> 8) & 15u;
     const uint32_t gcv = kind == M_GC && s.lid < n ? M[g.o_gp + e * n + s.lid] : 0u;
     s.free_event(e);
