@@ -103,9 +103,11 @@ MODE_DEFAULTS = {
     # instance, k_simx runs 3 waves per SIMD (164 VGPRs): 12 per CU x 256 CUs
     # = 3,072 (4,096 adds a second, one-third-occupied round: 99 -> 72 M)
     "dense-sim": dict(seeds=3072, conflicts="100", protocol="both", f=2),
-    # configs[3] on the batched executor: 768 instances = 3,840 streams, 5
-    # rounds of 768 workgroups (3 per CU)
-    "dense": dict(seeds=768, conflicts="100", protocol="epaxos", f=2),
+    # configs[3] on the batched executor: 3,072 instances = 15,360 streams,
+    # one wavefront each, 5 per CU (LDS tables): 12 rounds, so the last
+    # round's tail weighs less than at 768 instances (68.3 M; 1,536: 73.2 M;
+    # 3,072: 77.2 M; 6,144: 79.5 M, tools/dense_scale.sh)
+    "dense": dict(seeds=3072, conflicts="100", protocol="epaxos", f=2),
 }
 
 
