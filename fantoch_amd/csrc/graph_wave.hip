@@ -389,8 +389,30 @@ struct Wave {
     if (sl >= 0) dfs_start((uint32_t)sl, false);
   }
 
+  // the wave-uniform state back into scalar registers (readfirstlane of a
+  // value the compiler keeps in a VGPR; a no-op for one already scalar), so the
+  // step loop's branches are scalar compares and its state is not copied
+  // between VGPR versions on every iteration
+  __device__ __forceinline__ void canon() {
+    phase = uni(phase);
+    root = uni(root);
+    idc = uni(idc);
+    nfr = uni(nfr);
+    missing = uni(missing);
+    fv = uni(fv);
+    fdi = uni(fdi);
+    fnc = uni(fnc);
+    in_try = uni(in_try);
+    emitted = uni(emitted);
+    k = uni(k);
+    err = uni(err);
+    epoch = uni(epoch);
+    nwl = uni(nwl);
+  }
+
   __device__ __forceinline__ void run_slow() {
     while (phase != PH_IDLE) {
+      canon();
       if (phase == PH_DFS) dfs_iter();
       else if (phase == PH_TRY) try_iter();
       else check_iter();
@@ -697,6 +719,7 @@ __global__ __launch_bounds__(64 * (1 + NPOLL)) void k_handle_persist(PersistArgs
       e.step_start(done, d, h, lane < MBD ? depj : 0u, MBD, a.at_commit != 0);
       t_step = (uint32_t)(__builtin_amdgcn_s_memtime() - cy1);
       while (e.phase != PH_IDLE) {  // run_slow, counted
+        e.canon();
         if (e.phase == PH_DFS) e.dfs_iter();
         else if (e.phase == PH_TRY) e.try_iter();
         else e.check_iter();
