@@ -13,3 +13,5 @@ timeout -k 10 300 python -u bench.py --mode handle > $M/handle.log 2>&1 || { ech
 tail -1 $M/handle.log | cut -c1-300
 timeout -k 10 300 python -u bench.py --mode executor > $M/executor.log 2>&1 || { echo "executor rc=$?"; tail -20 $M/executor.log; exit 1; }
 tail -1 $M/executor.log | cut -c1-300
+timeout -k 10 400 python -u bench.py --mode dense-sim > $M/dense_sim.log 2>&1 || { echo "dense-sim rc=$?"; tail -20 $M/dense_sim.log; exit 1; }
+tail -1 $M/dense_sim.log | cut -c1-300
