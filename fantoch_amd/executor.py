@@ -30,6 +30,7 @@ class GraphExecutor:
         self._drain = lib.fx_graph_executor_drain_dots
         self._karr = (ctypes.c_uint32 * 16)()
         self._darr = (CDot * 64)()
+        self._du32 = (ctypes.c_uint32 * 128).from_buffer(self._darr)  # the same words, flat
         self._dbuf = (CDot * 256)()
         self._dstart = (ctypes.c_uint8 * 256)()
         self._got = ctypes.c_uint32()
@@ -65,10 +66,7 @@ class GraphExecutor:
             karr = (ctypes.c_uint32 * len(keys))(*keys)
         if len(deps) <= 64:
             darr = self._darr
-            for i, (s, q) in enumerate(deps):
-                d = darr[i]
-                d.source = s
-                d.seq = q
+            self._du32[0:2 * len(deps)] = [int(x) for d in deps for x in d]
         else:
             darr = (CDot * len(deps))(*[CDot(int(s), int(q)) for s, q in deps])
         st = self._add(self._h, CDot(*dot), CRifl(*rifl), karr, len(keys), 1 if read_only else 0, darr,
