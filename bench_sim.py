@@ -285,8 +285,12 @@ def main_sim(args):
                 roof["issue"].update(bound="salu-issue", frac=roof["issue"].get("salu_per_cu_cycle"))
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline_sim(args, specs, rates, executed, executed_len, st, lat_hist, n, exec_cap,
-                                   planet)
+            def run_subset(idx):
+                return _subset_hists(torch, lib, _lib, [specs[i] for i in idx], planet, ping, rank_m, dev, hs,
+                                     sim_flags, exec_cap, args, (LAT_BINS, CHAIN_BINS, DELAY_BINS), n)
+            timed = (lat_hist.view(planet.R, LAT_BINS).cpu().numpy(), chain.cpu().numpy(), delay.cpu().numpy())
+            cpu = cpu_baseline_sim(args, specs, rates, executed, executed_len, st, timed, n, exec_cap,
+                                   planet, run_subset)
         lat = lat_hist.view(planet.R, LAT_BINS).cpu().numpy()
         regions = S.GCP5[:n]
         hist_stats = {"client_latency_ms": {r: fm.dense_stats(lat[planet.index[r]]) for r in regions},
@@ -345,12 +349,74 @@ def sim_key(args):
         "" if (args.clients_per_region or 1) == 1 else "_k%d" % args.clients_per_region)
 
 
-def cpu_baseline_sim(args, specs, rates, executed, executed_len, st, lat_hist, n, exec_cap, planet):
+def _subset_hists(torch, lib, _lib, sub, planet, ping, rank_m, dev, hs, sim_flags, exec_cap, args, bins, n):
+    """Histograms (client latency [R, bins], ChainSize, ExecutionDelay) of a
+    GPU run over a subset of the bench's instances (same specs, so the same
+    C6 RNG streams): the kernel is deterministic per instance, so the sample's
+    run and the rest's run add up to the timed batch's histograms exactly."""
+    import ctypes as ct
+    LAT_BINS, CHAIN_BINS, DELAY_BINS = bins
+    N = len(sub)
+    if N == 0:
+        return (np.zeros((planet.R, LAT_BINS), np.int64), np.zeros(CHAIN_BINS, np.int64),
+                np.zeros(DELAY_BINS, np.int64))
+    host = (_lib.SimSpec * N)(*sub)
+    spec_dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev)
+    executed = torch.empty(N * n * exec_cap, dtype=torch.int32, device=dev)
+    executed_len = torch.zeros(N * n, dtype=torch.int32, device=dev)
+    lat = torch.zeros(planet.R * LAT_BINS, dtype=torch.int64, device=dev)
+    chain = torch.zeros(CHAIN_BINS, dtype=torch.int64, device=dev)
+    delay = torch.zeros(DELAY_BINS, dtype=torch.int64, device=dev)
+    stats = torch.zeros(N * _lib.FX_SIM_STATS, dtype=torch.int64, device=dev)
+    err = torch.zeros(N, dtype=torch.int32, device=dev)
+    batch = _lib.SimBatch(spec_dev.data_ptr(), ct.addressof(host), N, sim_flags, ping.data_ptr(),
+                          rank_m.data_ptr(), planet.R, planet.STRIDE, exec_cap, 0, 0,
+                          args.ring_entries, args.dot_slots, 0)
+    out = _lib.SimOutput(executed.data_ptr(), executed_len.data_ptr(), None, lat.data_ptr(),
+                         chain.data_ptr(), delay.data_ptr(), stats.data_ptr(), err.data_ptr(),
+                         LAT_BINS, CHAIN_BINS, DELAY_BINS, 0, None)
+    _lib.check(lib.fx_sim_run_tiered(ct.byref(batch), ct.byref(out), hs, None), "fx_sim_run_tiered (subset)")
+    torch.cuda.synchronize(dev)
+    if int((err != 0).sum().item()):
+        raise SystemExit("subset rerun: simulated instances failed")
+    return (lat.view(planet.R, LAT_BINS).cpu().numpy(), chain.cpu().numpy(), delay.cpu().numpy())
+
+
+def hist_parity(timed, gpu_sample, gpu_rest, oracle_res):
+    """(ok, detail) of the histogram check on the bench's sample:
+    the GPU's sample histograms (client latency per region, ChainSize,
+    ExecutionDelay) equal the oracle's summed over the sample, and the timed
+    batch's histograms equal the sample's plus the rest's, bin for bin
+    (runner.rs:619-634 clients_latencies, histogram.rs:55-59 increment;
+    graph/mod.rs:492-518 ChainSize / ExecutionDelay)."""
+    names = ("client_latency", "chain_size", "execution_delay")
+    keys = ("latency", "chain", "delay")
+    detail = {}
+    ok = True
+    for nm, k, t, s, r in zip(names, keys, timed, gpu_sample, gpu_rest):
+        o = np.zeros(s.shape, np.int64)
+        for res in oracle_res:
+            a = res[k].astype(np.int64)
+            o[tuple(slice(0, m) for m in a.shape)] += a[tuple(slice(0, m) for m in o.shape)]
+        same_oracle = bool(np.array_equal(s, o))
+        adds_up = bool(np.array_equal(t, s + r))
+        detail[nm] = {"sample_equals_oracle": same_oracle, "timed_equals_sample_plus_rest": adds_up,
+                      "sample_samples": int(o.sum())}
+        ok = ok and same_oracle and adds_up
+    return ok, detail
+
+
+def cpu_baseline_sim(args, specs, rates, executed, executed_len, st, timed_hists, n, exec_cap, planet,
+                     run_subset=None):
     """The simulator oracle (oracle/sim_oracle.cpp, the C++ restatement of the
     reference simulator) on a bounded sample of the same instances, one
     instance per std::thread task like the reference binary's rayon par_iter,
     on every usable host core; the GPU's outputs for the sample are checked
-    against it bit for bit (execution orders, counters, latency histograms)."""
+    against it bit for bit: execution orders, fast / slow / stable counters,
+    action trace and end time per instance, and the three histograms
+    (client latency per region, ChainSize, ExecutionDelay) through
+    `hist_parity` — the timed batch's histograms = the sample's GPU rerun + the
+    rest's GPU rerun, and the sample's = the oracle's sum over the sample."""
     import torch
     from bench import host_cpus
     from oracle import oracle_lib as O
@@ -390,15 +456,26 @@ def cpu_baseline_sim(args, specs, rates, executed, executed_len, st, lat_hist, n
             ok = False
         if not ok:
             break
+    orders_ok = ok
+    hist_detail = None
+    if run_subset is not None:
+        rest = np.setdiff1d(np.arange(len(specs)), pick)
+        hok, hist_detail = hist_parity(timed_hists, run_subset(pick), run_subset(rest), res)
+        ok = ok and hok
+    else:
+        ok = False  # histograms unchecked: no parity claim
     return {"value": round(executed_cpu / dt, 1), "unit": "cmds/s", "cores": threads, "kind": "port",
             "host": host,
             "sample": "%d of %d instances spread over every conflict rate, simulated end to end by the "
                       "C++ simulator oracle in %.2f s on %d threads (%d executed commands); GPU output "
                       "on the sample %s the oracle bit-for-bit (execution orders, fast/slow/stable "
-                      "counters, action trace, end time)"
+                      "counters, action trace, end time, and the client-latency / ChainSize / "
+                      "ExecutionDelay histograms: the sample's GPU histograms equal the oracle's, and the "
+                      "timed batch's equal the sample's plus the other instances' GPU rerun)"
                       % (len(pick), len(specs), dt, threads, executed_cpu,
                          "matches" if ok else "DIFFERS FROM"),
-            "sample_parity": ok}
+            "sample_parity": ok, "sample_orders_counters_parity": orders_ok,
+            "sample_histogram_parity": hist_detail}
 
 
 def _to_oracle(_lib, O, s):

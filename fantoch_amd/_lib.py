@@ -29,6 +29,7 @@ FX_ERR_LOG_FORMAT = 11
 FX_ERR_SIM_CAPACITY = 12
 FX_ERR_SIM_LATE = 13
 FX_ERR_SIM_EVENTS = 14
+FX_ERR_TIMEOUT = 15
 FX_PROTOCOL_ATLAS = 0
 FX_PROTOCOL_EPAXOS = 1
 FX_PROTOCOL_BASIC = 2

@@ -17,12 +17,14 @@
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <map>
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fantoch_amd.h"
@@ -196,6 +198,8 @@ struct fx_graph_executor {
   struct Persist {
     bool active = false;    // the log is executed by the persistent kernel
     bool launched = false;  // a launch is outstanding on `stream` (it may have exited when idle)
+    bool dead = false;      // a stop request went unanswered past the deadline: the stream is abandoned
+    uint64_t timeout_ns = 0;  // every host wait's deadline (FX_HANDLE_TIMEOUT_MS at creation, default 2 s)
     hipStream_t stream = nullptr;
     HostBuf ctl, rows, out;
     DevBuf state;
@@ -280,17 +284,6 @@ inline void ld16(const volatile uint32_t* p, uint32_t out[4]) {
   _mm_storeu_si128(reinterpret_cast<__m128i*>(out), v);
 }
 
-// Stops the persistent kernel (its executor state lands in ps.state).
-int persist_stop(fx_graph_executor* ex) {
-  if (!ex->ps.launched) return FX_OK;
-  pctl(ex)[fx::PERSIST_EXIT] = 1u;
-  std::atomic_thread_fence(std::memory_order_seq_cst);
-  const bool ok = hipStreamSynchronize(ex->ps.stream) == hipSuccess;
-  ex->ps.launched = false;
-  pctl(ex)[fx::PERSIST_EXIT] = 0u;
-  return ok ? FX_OK : FX_ERR_HIP;
-}
-
 // The stream of a handle's persistent kernel.  The kernel stays resident, so
 // whatever else is queued on the same hardware queue waits for it (up to its
 // idle exit): FX_PERSIST_QUEUE picks how the stream is made -- "plain" (a
@@ -352,23 +345,79 @@ int persist_alloc(fx_graph_executor* ex) {
   return FX_OK;
 }
 
-// A wait that lasts seconds means a lost word: report the control words once.
-void persist_stuck(fx_graph_executor* ex, const char* where, uint32_t hi, uint64_t spin) {
-  if ((spin & 4095u) != 4095u) return;
-  static thread_local std::chrono::steady_clock::time_point t0;
-  static thread_local bool reported = false;
-  const auto now = std::chrono::steady_clock::now();
-  if (spin == 4095u) {
-    t0 = now;
-    reported = false;
-    return;
+// Every host wait on the resident kernel is bounded (status
+// codes replace panics; the reference's Executor never blocks,
+// fantoch/src/executor/mod.rs:27-89).  A Wait checks, every 1024 spins, the
+// deadline (FX_HANDLE_TIMEOUT_MS, default 2000 ms from the start of the wait)
+// and the stream: an error there (a faulted kernel) ends the wait with
+// FX_ERR_HIP.  On expiry the handle asks the kernel to stop, waits for the
+// stream at most one more deadline, and the flush returns FX_ERR_TIMEOUT,
+// sticky for the handle.
+uint64_t persist_timeout_ns() {
+  const char* e = std::getenv("FX_HANDLE_TIMEOUT_MS");
+  const long ms = e ? std::atol(e) : 0;
+  return (uint64_t)(ms > 0 ? ms : 2000) * 1000000ull;
+}
+
+struct Wait {
+  std::chrono::steady_clock::time_point end;
+  explicit Wait(uint64_t ns)
+      : end(std::chrono::steady_clock::now() + std::chrono::nanoseconds(ns)) {}
+  // FX_OK: keep spinning; FX_ERR_TIMEOUT: the deadline passed; FX_ERR_HIP: the
+  // stream reported an error
+  int check(hipStream_t s, uint64_t spin) const {
+    if ((spin & 1023u) != 1023u) return FX_OK;
+    const hipError_t q = hipStreamQuery(s);
+    if (q != hipSuccess && q != hipErrorNotReady) return FX_ERR_HIP;
+    return std::chrono::steady_clock::now() > end ? FX_ERR_TIMEOUT : FX_OK;
   }
-  if (reported || now - t0 < std::chrono::seconds(5)) return;
-  reported = true;
-  std::fprintf(stderr, "fantoch_amd persistent handle: still waiting (%s) hi=%u consumed=%u pub=%u ctl[0..63]:", where,
-               hi, ex->consumed, ex->ps.pub);
-  for (uint32_t i = 0; i < 64; ++i) std::fprintf(stderr, " %u", pctl(ex)[i]);
-  std::fprintf(stderr, "\n");
+};
+
+// The end of a failed wait: ask the kernel to stop and give its stream one
+// more deadline to drain.  A stream that drains is reusable; one that does not
+// is abandoned (never synchronised again, never pooled).
+int persist_abort(fx_graph_executor* ex, int st, const char* where, uint32_t hi) {
+  auto& P = ex->ps;
+  std::fprintf(stderr, "fantoch_amd persistent handle: %s while waiting for the %s (rows %u, consumed %u)\n",
+               st == FX_ERR_TIMEOUT ? "deadline passed" : "stream error", where, hi, ex->consumed);
+  pctl(ex)[fx::PERSIST_EXIT] = 1u;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  const Wait w(ex->ps.timeout_ns);
+  for (;;) {
+    const hipError_t q = hipStreamQuery(P.stream);
+    if (q == hipSuccess) {
+      P.launched = false;
+      pctl(ex)[fx::PERSIST_EXIT] = 0u;
+      break;
+    }
+    if (q != hipErrorNotReady || std::chrono::steady_clock::now() > w.end) {
+      P.dead = true;  // the kernel did not stop: leave its stream alone
+      break;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  ex->persist_ok = false;
+  return ex->sticky = st;
+}
+
+// Stops the persistent kernel (its executor state lands in ps.state); the
+// wait for its stream is bounded like every other (persist_abort on expiry).
+int persist_stop(fx_graph_executor* ex) {
+  if (ex->ps.dead) return FX_ERR_TIMEOUT;
+  if (!ex->ps.launched) return FX_OK;
+  pctl(ex)[fx::PERSIST_EXIT] = 1u;
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  const Wait w(ex->ps.timeout_ns);
+  for (uint64_t spin = 0;; ++spin) {
+    const hipError_t q = hipStreamQuery(ex->ps.stream);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) return persist_abort(ex, FX_ERR_HIP, "stop", ex->ps.pub);
+    if (std::chrono::steady_clock::now() > w.end) return persist_abort(ex, FX_ERR_TIMEOUT, "stop", ex->ps.pub);
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  ex->ps.launched = false;
+  pctl(ex)[fx::PERSIST_EXIT] = 0u;
+  return FX_OK;
 }
 
 int persist_launch_now(fx_graph_executor* ex, bool init) {
@@ -383,6 +432,10 @@ int persist_launch_now(fx_graph_executor* ex, bool init) {
   a.at_commit = ex->cfg.execute_at_commit ? 1u : 0u;
   a.init = init ? 1u : 0u;
   a.done0 = pctl(ex)[fx::PERSIST_DONE];
+  {
+    const char* e = std::getenv("FX_HANDLE_DEBUG_SKIP_STATUS");
+    a.debug_skip_status = e ? (uint32_t)std::atol(e) : 0u;
+  }
   pctl(ex)[fx::PERSIST_RUN] = 1u;  // the kernel clears it when it exits
   std::atomic_thread_fence(std::memory_order_seq_cst);
   if (fx::persist_launch(a, ex->ps.stream) != FX_OK) return FX_ERR_HIP;
@@ -428,12 +481,21 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
     ex->bytes_h2d += (uint64_t)(hi - P.pub) * fx::PERSIST_ROW_WORDS * 4;
     if (hi == P.pub + 1u && ex->deps[P.pub].size() <= fx::PERSIST_MB_DEPS) {
       // a one-Add flush: the row also goes into the mailbox line, which the
-      // kernel reads with the doorbell (tag last: the line is read as a unit)
+      // kernel reads with the doorbell.  Its 32 lanes load the line word by
+      // word, so a read can mix two flushes' words: the checksum word (the
+      // tag mixed in, fx::persist_mb_mix) rejects such a line and the kernel
+      // takes the row from the ring
       volatile uint32_t* mb = pctl(ex) + fx::PERSIST_MB;
       const auto& dv = ex->deps[P.pub];
-      mb[1] = ex->dots[P.pub];
-      mb[2] = ex->hdrs[P.pub];
-      for (uint32_t j = 0; j < fx::PERSIST_MB_DEPS; ++j) mb[3 + j] = j < dv.size() ? dv[j] : 0u;
+      uint32_t w15[15];
+      w15[0] = hi;
+      w15[1] = ex->dots[P.pub];
+      w15[2] = ex->hdrs[P.pub];
+      for (uint32_t j = 0; j < fx::PERSIST_MB_DEPS; ++j) w15[3 + j] = j < dv.size() ? dv[j] : 0u;
+      uint32_t sum = 0;
+      for (uint32_t k = 0; k < 15; ++k) sum ^= fx::persist_mb_mix(w15[k], k);
+      for (uint32_t k = 1; k < 15; ++k) mb[k] = w15[k];
+      mb[15] = sum;
       std::atomic_thread_fence(std::memory_order_release);
       mb[0] = hi;
     }
@@ -451,12 +513,20 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
     // idle just before the doorbell (RUN cleared, done short of hi) is
     // relaunched from its state
     uint32_t w[4];
+    const Wait wt(P.timeout_ns);
     for (uint64_t spin = 0;; ++spin) {
       ld16(pctl(ex) + fx::PERSIST_DONE, w);
       if (w[0] == hi) break;
-      persist_stuck(ex, "status", hi, spin);
+      if (const int ws = wt.check(P.stream, spin)) return persist_abort(ex, ws, "status", hi);
       if ((spin & 1023u) == 1023u && pctl(ex)[fx::PERSIST_RUN] == 0u) {
-        if (hipStreamSynchronize(P.stream) != hipSuccess) return FX_ERR_HIP;
+        // the kernel left (idle exit just before the doorbell): its stream
+        // drains within the deadline, then it is relaunched
+        for (uint64_t s2 = 1023u;; s2 += 1024u) {
+          const hipError_t q = hipStreamQuery(P.stream);
+          if (q == hipSuccess) break;
+          if (const int ws = q != hipErrorNotReady ? FX_ERR_HIP : wt.check(P.stream, s2))
+            return persist_abort(ex, ws, "idle exit", hi);
+        }
         P.launched = false;
         ld16(pctl(ex) + fx::PERSIST_DONE, w);
         if (w[0] == hi) break;
@@ -472,9 +542,10 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
     P.stats[0] += 1;
     P.stats[1] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tw1 - tw0).count();
     if (w[1] & fx::PERSIST_ERR_BIT) {  // {done, err} is written with the status; wait for it
+      const Wait we(P.timeout_ns);
       for (uint64_t spin = 0; w[2] != hi; ++spin) {
         ld16(pctl(ex) + fx::PERSIST_DONE, w);
-        persist_stuck(ex, "error word", hi, spin);
+        if (const int ws = we.check(P.stream, spin)) return persist_abort(ex, ws, "error word", hi);
       }
       const uint32_t err = w[3];
       persist_stop(ex);
@@ -491,6 +562,7 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
       P.stats[8] += t[0];
       P.stats[12] += t[1];
       P.stats[13] += t[2];
+      P.stats[14] += t[3];
     }
     nexec = w[1];
     P.pub = hi;
@@ -500,12 +572,13 @@ int flush_persist(fx_graph_executor* ex, uint32_t& nexec_out) {
       if (np > fx_graph_executor::Persist::OUT) return FX_ERR_CAPACITY;
       std::vector<uint32_t> order(np), rel(np);
       if (np <= fx::PERSIST_INLINE) {
+        const Wait wp(P.timeout_ns);
         for (uint32_t j = 0; j < np; ++j) {
           uint32_t t[4];
           for (uint64_t spin = 0;; ++spin) {
             ld16(pctl(ex) + fx::PERSIST_PAIRS + 4 * j, t);
             if (t[0] == hi && t[2] == hi) break;
-            persist_stuck(ex, "pairs", hi, spin);
+            if (const int ws = wp.check(P.stream, spin)) return persist_abort(ex, ws, "pairs", hi);
           }
           order[j] = t[1];
           rel[j] = t[3];
@@ -555,11 +628,18 @@ int flush(fx_graph_executor* ex) {
     if (st == FX_OK) return FX_OK;
     if (st != FX_ERR_CAPACITY) return ex->sticky = st;
     // to the batch tiers, from the start of the log (the consumed prefix of
-    // the deterministic order is skipped there)
-    persist_stop(ex);
+    // the deterministic order is skipped there), for the rest of the handle's
+    // life.  The first tier follows the cause: an Add wider than the wave
+    // tier's WAVE_MAX_DEPS goes to the LDS slot tier (31 deps), a pending set
+    // or clock window the wave tier cannot hold to the HBM slot tier (64
+    // pending, 1024-bit windows); both escalate on capacity from there
+    if (const int s2 = persist_stop(ex)) return ex->sticky = s2;
+    if (ex->sticky) return ex->sticky;
     ex->persist_ok = false;
     ex->ps.active = false;
-    ex->tier = FX_TIER_GLOBAL;
+    bool wide = false;
+    for (const auto& d : ex->deps) wide = wide || d.size() > fx::WAVE_MAX_DEPS;
+    ex->tier = wide ? FX_TIER_LDS_LARGE : FX_TIER_GLOBAL;
     ex->processed = 0;
     ex->uploaded = 0;
   }
@@ -822,14 +902,16 @@ fx_graph_executor* fx_graph_executor_new(uint8_t process_id, uint64_t shard_id, 
   if (ex->partial) ex->tier = FX_TIER_WIDE_HBM;
   const char* pe = std::getenv("FX_HANDLE_PERSIST");
   ex->persist_ok = !(pe && pe[0] == '0');
+  ex->ps.timeout_ns = persist_timeout_ns();
   const char* ps = std::getenv("FX_HANDLE_STATS");
   ex->ps.want_stats = ps && ps[0] == '1';
-  // the persistent mode's buffers (if they cannot be had, the batch tiers run)
-  if (ex->persist_ok && !ex->partial && persist_alloc(ex) != FX_OK) ex->persist_ok = false;
+  // the handle's own stream first: a failure here has nothing else to undo
   if (hipStreamCreateWithFlags(&ex->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ex;
     return nullptr;
   }
+  // the persistent mode's buffers (if they cannot be had, the batch tiers run)
+  if (ex->persist_ok && !ex->partial && persist_alloc(ex) != FX_OK) ex->persist_ok = false;
   return ex;
 }
 
@@ -851,7 +933,9 @@ void fx_graph_executor_free(fx_graph_executor* ex) {
         pooled = true;
       }
     }
-    if (!pooled) (void)hipStreamDestroy(ex->ps.stream);
+    // an abandoned stream (its kernel never answered the stop request) is
+    // leaked: destroying it would wait for the kernel
+    if (!pooled && !ex->ps.dead) (void)hipStreamDestroy(ex->ps.stream);
   }
   hipStream_t s = ex->stream;
   delete ex;  // DevBufs free first
@@ -1131,7 +1215,7 @@ int fx_graph_executor_pending(fx_graph_executor* ex, fx_dot* dots, fx_dot* waiti
   *n_out = 0;
   if (ex->processed == 0) return FX_OK;
   if (ex->ps.active) {  // the persistent kernel's state, saved when it stops
-    if (persist_stop(ex)) return FX_ERR_HIP;
+    if (const int s2 = persist_stop(ex)) return s2;
     std::vector<uint32_t> block(fx::wave_state_words_per_stream());
     // on the handle's own stream: a null-stream copy would also wait for other
     // handles' resident kernels (their streams are blocking ones)

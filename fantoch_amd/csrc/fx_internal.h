@@ -91,13 +91,17 @@ struct PersistArgs {
   uint32_t* state;      // device: the wave tier's saved state of one stream
   uint32_t row_slots, out_slots;  // powers of two
   uint32_t n, at_commit, init, done0;
+  // test hook (FX_HANDLE_DEBUG_SKIP_STATUS=k): the k-th flush of this launch
+  // publishes no status, so the host's bounded wait must expire (0 = never)
+  uint32_t debug_skip_status;
 };
 constexpr uint32_t PERSIST_ROW_WORDS = 16;  // dot, hdr, 14 deps
 constexpr uint32_t PERSIST_CTL_WORDS = 64;
-constexpr uint32_t PERSIST_MB_DEPS = 13;    // deps a mailbox row carries
+constexpr uint32_t PERSIST_MB_DEPS = 12;    // deps a mailbox row carries (tag, dot, hdr, 12 deps, checksum)
 constexpr uint32_t PERSIST_INLINE = 4;      // pairs a flush reports in the control words
 // Control words, four 64-byte lines.  Line 0 host -> device: PUB (rows
-// published), EXIT.  Line 1: the mailbox (tag, dot, hdr, 13 deps).  Line 2
+// published), EXIT.  Line 1: the mailbox (tag, dot, hdr, 12 deps, a checksum of
+// the other 15 words: persist_mb_sum).  Line 2
 // device -> host: the status as two tagged 64-bit words {DONE, NEXEC | bit 31 on
 // an error} and {DONE2, ERR}, the timing words, RUN.  Line 3: up to
 // PERSIST_INLINE (order word, release step) pairs as tagged 64-bit words
@@ -108,10 +112,24 @@ constexpr uint32_t PERSIST_INLINE = 4;      // pairs a flush reports in the cont
 enum : uint32_t { PERSIST_PUB = 0, PERSIST_EXIT = 1, PERSIST_MB = 16, PERSIST_DONE = 32, PERSIST_NEXEC = 33,
                   PERSIST_DONE2 = 34, PERSIST_ERR = 35, PERSIST_TCOMP = 36, PERSIST_TFENCE = 37,
                   PERSIST_TPOLLS = 38, PERSIST_TRTT = 39, PERSIST_TCYC = 40, PERSIST_TITER = 41,
-                  PERSIST_TSTEP = 42, PERSIST_RUN = 47,
+                  PERSIST_TSTEP = 42, PERSIST_TMB = 43, PERSIST_RUN = 47,
                   PERSIST_PAIRS = 48 };
 constexpr uint32_t PERSIST_ERR_BIT = 0x80000000u;
 int persist_launch(const PersistArgs& a, hipStream_t stream);
+// The mailbox checksum: XOR over k of fmix32(word k ^ (k + 1) * golden) for
+// the tag, dot, hdr and the 12 deps (k = 0..14).  The kernel reads the line with
+// 32 independent 4-byte loads, which a host write can interleave with; a line
+// whose words come from two different one-Add flushes fails this check (the
+// tag is mixed in) and the kernel reads the row from the ring instead.
+__host__ __device__ inline uint32_t persist_mb_mix(uint32_t w, uint32_t k) {
+  uint32_t h = w ^ ((k + 1u) * 0x9E3779B9u);
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
 // fx_profile_slot_ms: events around one kernel slot's launch (graph_exec.hip)
 void profile_slot_record(uint32_t slot, bool end, hipStream_t s);
 

@@ -1044,6 +1044,7 @@ const char* fx_status_string(int s) {
     case FX_ERR_SIM_CAPACITY: return "simulated instance outgrew its launch geometry";
     case FX_ERR_SIM_LATE: return "simulated message found no state for its dot";
     case FX_ERR_SIM_EVENTS: return "simulated instance exceeded its event budget";
+    case FX_ERR_TIMEOUT: return "a drop-in handle's wait for its resident kernel passed the deadline";
     default: return "unknown";
   }
 }

@@ -544,7 +544,7 @@ __global__ __launch_bounds__(64 * WPB) void k_graph_wave(KArgs a) {
 // over Adds the host publishes in host-mapped memory:
 //   ctl[PUB]     rows published by the host (written after the rows)
 //   ctl[EXIT]    host asks the kernel to stop
-//   ctl[MB..]    mailbox: tag (= row index + 1), dot, hdr, 13 deps of the row of
+//   ctl[MB..]    mailbox: tag (= row index + 1), dot, hdr, 12 deps, checksum of the row of
 //                a one-Add flush, read in the same round trip as the doorbell
 //   ctl[DONE..]  rows processed, executed count, status: tagged 64-bit words
 //   ctl[PAIRS..] the flush's pairs when there are at most PERSIST_INLINE of
@@ -563,7 +563,7 @@ namespace persist {
 enum : uint32_t { P_PUB = PERSIST_PUB, P_EXIT = PERSIST_EXIT, P_MB = PERSIST_MB, P_DONE = PERSIST_DONE,
                   P_DONE2 = PERSIST_DONE2, P_TCOMP = PERSIST_TCOMP, P_RUN = PERSIST_RUN, P_PAIRS = PERSIST_PAIRS };
 constexpr uint32_t PRW = 16;                     // words per published row
-constexpr uint32_t MBD = 13;                     // deps a mailbox row carries (tag, dot, hdr, deps)
+constexpr uint32_t MBD = PERSIST_MB_DEPS;        // deps a mailbox row carries (tag, dot, hdr, deps, checksum)
 constexpr uint64_t IDLE_TICKS = 2000000ull;      // s_memrealtime runs at 100 MHz: 20 ms
 // Poller waves: a poll of host memory takes a round trip (~1.25 us), so one
 // wave that polls and then waits samples the doorbell once per round trip.
@@ -696,6 +696,7 @@ __global__ __launch_bounds__(64 * (1 + NPOLL)) void k_handle_persist(PersistArgs
   // sample that carried the last doorbell, the LDS checks before it, the last
   // flush's compute and its publish
   uint32_t t_rtt = 0, t_polls = 0, t_fence = 0, t_iter = 0, t_step = 0;
+  uint32_t nflush = 0, t_mb = 0;
   while (!e.err) {
     const uint32_t lv = __hip_atomic_load(&ps_latest, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t pub = uni(lv) >> 3;
@@ -712,11 +713,24 @@ __global__ __launch_bounds__(64 * (1 + NPOLL)) void k_handle_persist(PersistArgs
     const uint32_t v = lane < 32u ? ps_slot[si * 32u + lane] : 0u;
     t_rtt = (uint32_t)tp1 - ps_stamp[si];
     e.out.k0 = e.k;
+    // the mailbox line's checksum (fx_internal.h persist_mb_mix): lanes
+    // P_MB .. P_MB + 14 mix their word, an XOR over the 16 lanes of the line
+    // compares with word P_MB + 15 (a line mixed from two flushes fails)
+    uint32_t mbx = 0;
     if (pub == done + 1u && rl(v, P_MB) == pub) {
+      const uint32_t k = lane - P_MB;
+      mbx = k < 15u ? persist_mb_mix(v, k) : k == 15u ? v : 0u;
+      mbx ^= __shfl_xor(mbx, 1);
+      mbx ^= __shfl_xor(mbx, 2);
+      mbx ^= __shfl_xor(mbx, 4);
+      mbx ^= __shfl_xor(mbx, 8);
+    }
+    if (pub == done + 1u && rl(v, P_MB) == pub && rl(mbx, P_MB) == 0u) {
       // a one-Add flush: its row came with the doorbell (the host writes the
       // mailbox line before the doorbell; a load that saw the new doorbell but
-      // an older mailbox tag falls back to the ring)
+      // an older mailbox tag, or a torn line, falls back to the ring)
       const uint32_t d = rl(v, P_MB + 1u), h = rl(v, P_MB + 2u);
+      t_mb = 1;
       const uint32_t depj = gather(v, (P_MB + 3u + lane) & 63u);
       e.step_start(done, d, h, lane < MBD ? depj : 0u, MBD, a.at_commit != 0);
       t_step = (uint32_t)(__builtin_amdgcn_s_memtime() - cy1);
@@ -764,14 +778,17 @@ __global__ __launch_bounds__(64 * (1 + NPOLL)) void k_handle_persist(PersistArgs
       const uint32_t val = lane == 0 ? (e.k | (e.err ? PERSIST_ERR_BIT : 0u)) : lane == 1 ? e.err
                          : pair ? e.out.stage[m] : 0u;
       uint32_t* dst = lane == 0 ? ctl + P_DONE : lane == 1 ? ctl + P_DONE2 : ctl + P_PAIRS + 2u * m;
-      if (lane < 2u || pair) st_tag(dst, pub, val);
+      ++nflush;
+      const bool skip = a.debug_skip_status != 0u && nflush == a.debug_skip_status;  // test hook
+      if ((lane < 2u && !skip) || pair) st_tag(dst, pub, val);
     }
-    if (lane >= 2u && lane < 9u)  // timing words (diagnostics)
+    if (lane >= 2u && lane < 10u)  // timing words (diagnostics) and the mailbox flag
       st_sys(ctl + P_TCOMP + lane - 2u, lane == 2 ? (uint32_t)(tc - tp1) : lane == 3 ? t_fence
                                       : lane == 4 ? t_polls : lane == 5 ? t_rtt : lane == 6 ? cyc
-                                      : lane == 7 ? t_iter : t_step);
+                                      : lane == 7 ? t_iter : lane == 8 ? t_step : t_mb);
     t_iter = 0;
     t_step = 0;
+    t_mb = 0;
     done = pub;
     idle0 = __builtin_amdgcn_s_memrealtime();
     t_fence = (uint32_t)(idle0 - tc);

@@ -66,12 +66,15 @@ class BatchResult:
 
 
 def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096, tiered=True,
-              tier=None, init_frontier=None, metrics=True, cut=False):
+              tier=None, init_frontier=None, metrics=True, cut=False, before_launch=None):
     """Runs a host batch on the GPU; returns host outputs (BatchResult).
 
     cut: fx_batch_run_cut (quiescent-cut decomposition, for huge streams);
     tiered: fx_batch_run_tiered starting at `tier` (None = FX_TIER_DEFAULT);
-    otherwise one fx_batch_execute launch at `tier` (None = FX_TIER_DEFAULT)."""
+    otherwise one fx_batch_execute launch at `tier` (None = FX_TIER_DEFAULT).
+    before_launch(stream): called with the launch's stream (None = the null
+    stream) once the inputs are on the device, right before the first
+    executor launch (tests: register poisoning, tests/test_poison_all.py)."""
     lib = _lib.load()
     S, steps, pw = planes.S, planes.steps, planes.plane
     bufs = {}
@@ -97,6 +100,8 @@ def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096,
     flags = _lib.FX_FLAG_EXECUTE_AT_COMMIT if execute_at_commit else 0
     tier_counts = (ctypes.c_uint32 * _lib.FX_NUM_TIERS)()
     cut_stats = None
+    if before_launch is not None:
+        before_launch(None)
     if cut:
         cut_stats = _lib.CutStats()
         status = lib.fx_batch_run_cut(ctypes.byref(inb), ctypes.byref(outb), flags, None,
@@ -136,7 +141,8 @@ def run_batch(planes, execute_at_commit=False, nbins_chain=64, nbins_delay=4096,
     return res
 
 
-def run_pred(planes, clock_lo, clock_hi, ndeps=None, execute_at_commit=False, tier=None, nbins_delay=4096):
+def run_pred(planes, clock_lo, clock_hi, ndeps=None, execute_at_commit=False, tier=None, nbins_delay=4096,
+             before_launch=None):
     """PredecessorsExecutor over a host batch with packed Caesar clock planes:
     fx_pred_run (tier None: the escalation chain) or one fx_pred_execute at
     `tier` (FX_PRED_TIER_*); returns a BatchResult (delay histogram from
@@ -163,6 +169,8 @@ def run_pred(planes, clock_lo, clock_hi, ndeps=None, execute_at_commit=False, ti
     outb = _lib.OrderBatch(order.ptr, release.ptr, nexec.ptr, err.ptr)
     flags = _lib.FX_FLAG_EXECUTE_AT_COMMIT if execute_at_commit else 0
     reruns = ctypes.c_uint32()
+    if before_launch is not None:
+        before_launch(None)
     if tier is not None:
         state = DeviceBuffer(lib.fx_pred_state_bytes(planes.n, planes.dmax, S)) if tier == _lib.FX_PRED_TIER_HBM \
             else None

@@ -203,6 +203,16 @@ class GraphExecutor:
                                                            ctypes.byref(d2h)))
         return h2d.value, d2h.value
 
+    def persist_stats(self):
+        """fx_graph_executor_persist_stats: the persistent mode's counters
+        (include/fantoch_amd.h FX_PERSIST_STATS; the kernel's words only with
+        FX_HANDLE_STATS=1 in the environment when the handle was made)."""
+        lib = _lib.load()
+        n = 15
+        out = (ctypes.c_uint64 * n)()
+        check(lib.fx_graph_executor_persist_stats(self._h, out, n))
+        return [int(x) for x in out]
+
 
 class ExecutorClone:
     """Executor index > 0 of a partial-replication process: GraphExecutionInfo::

@@ -49,6 +49,9 @@ extern "C" {
 #define FX_ERR_SIM_LATE 13     /* a simulated message found no state for its dot, or a
                                   reference assertion failed (runner.rs:239-241, single.rs:346-349) */
 #define FX_ERR_SIM_EVENTS 14   /* a simulated instance exceeded its event budget */
+#define FX_ERR_TIMEOUT 15      /* a drop-in handle's device wait passed its deadline
+                                  (FX_HANDLE_TIMEOUT_MS, default 2000): the resident
+                                  kernel was asked to stop; sticky for the handle */
 
 /* ------------------------------------------------- packed stream format */
 /* A dot (fantoch/src/id.rs:21-27, Id<u8>{source, sequence}, derived Ord) is
@@ -452,9 +455,10 @@ int fx_graph_executor_transfer_stats(const fx_graph_executor* ex, uint64_t* h2d,
  * [7] order conversion (ns), [8] the compute in shader-clock cycles, [9] the
  * host's whole flush, [10] its reads after the wait, [11] its work before the
  * publish (ns), [12] executor iterations (DFS edges / frame pops, try and
- * check steps), [13] cycles in the Add's first step. The kernel's words are
- * read only with FX_HANDLE_STATS=1 in the environment. */
-#define FX_PERSIST_STATS 14
+ * check steps), [13] cycles in the Add's first step, [14] one-Add flushes
+ * whose row the kernel took from the mailbox line (the rest read the ring). The
+ * kernel's words are read only with FX_HANDLE_STATS=1 in the environment. */
+#define FX_PERSIST_STATS 15
 int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out, uint32_t n);
 
 /* ------------------------------------------------------- quorum sizes */

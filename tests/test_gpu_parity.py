@@ -591,3 +591,124 @@ def test_executor_persistent_mode_equals_batch_tiers_and_oracle(gpu):
     assert a[0] == b[0] == c[0]
     assert a[1:] == b[1:] == c[1:]
     assert a[1] == g.metrics(1) and a[2] == g.metrics(0)
+
+
+def _with_env(env, fn):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def test_executor_persistent_wait_is_bounded(gpu):
+    """Every host wait of the persistent handle has a deadline (SURVEY §8(b):
+    status codes replace panics; the reference's Executor never blocks,
+    fantoch/src/executor/mod.rs:27-89).  A test hook makes the kernel skip the
+    status store of its 3rd flush: that pull returns FX_ERR_TIMEOUT within the
+    deadline (300 ms here) instead of hanging, the error is sticky, the handle
+    frees without a hang, and the next handle (from the resource pool) runs
+    normally."""
+    import time
+    p = fs.synth_params(seed=8, n=3, instances=1, cmds=20, window=4, cycle_pct=30, conflicts=(50,))
+    st = fs.synth_host(p).stream(0)[:30]
+    g = oracle_lib.Graph(1, 3)
+    for (dot, deps, t, _kind) in st:
+        g.handle_add(dot, deps, t)
+    exp = [d for d, _, _ in g.drain()]
+
+    h = _with_env({"FX_HANDLE_TIMEOUT_MS": 300, "FX_HANDLE_DEBUG_SKIP_STATUS": 3},
+                  lambda: GraphExecutor(1, 0, 3, monitor=False))
+    import os
+    os.environ["FX_HANDLE_DEBUG_SKIP_STATUS"] = "3"  # read at the kernel's launch
+    try:
+        t0 = time.perf_counter()
+        err = None
+        for i, (dot, deps, t, _kind) in enumerate(st[:5]):
+            h.handle_add(dot, dot, [0], deps, t)
+            try:
+                h.drain_dots()
+            except _lib.FxError as e:
+                err = (i, e.status, time.perf_counter() - t0)
+                break
+    finally:
+        del os.environ["FX_HANDLE_DEBUG_SKIP_STATUS"]
+    assert err is not None and err[0] == 2 and err[1] == _lib.FX_ERR_TIMEOUT, err
+    assert err[2] < 2.0, err
+    with pytest.raises(_lib.FxError) as again:
+        h.drain_dots()
+    assert again.value.status == _lib.FX_ERR_TIMEOUT
+    t1 = time.perf_counter()
+    h.close()
+    assert time.perf_counter() - t1 < 1.0
+    h2 = GraphExecutor(1, 0, 3, monitor=False)
+    out = []
+    for (dot, deps, t, _kind) in st:
+        h2.handle_add(dot, dot, [0], deps, t)
+        out += [d for d, _ in h2.drain_dots()]
+    h2.close()
+    assert out == exp
+
+
+def test_executor_persistent_handle_beside_null_stream_work(gpu):
+    """A resident handle kernel runs on a stream of its own hardware queue,
+    which HIP makes a blocking stream: null-stream work (a synchronous copy,
+    torch's default stream synchronisation) waits for it at most until its
+    idle exit (20 ms).  A program that mixes a live handle with such work
+     stays correct and pays at most that per switch."""
+    import time
+    import torch
+    p = fs.synth_params(seed=9, n=5, instances=1, cmds=40, window=8, cycle_pct=30, conflicts=(50,))
+    st = fs.synth_host(p).stream(0)[:120]
+    g = oracle_lib.Graph(1, 5)
+    for (dot, deps, t, _kind) in st:
+        g.handle_add(dot, deps, t)
+    exp = [d for d, _, _ in g.drain()]
+    h = GraphExecutor(1, 0, 5, monitor=False)
+    out = []
+    x = torch.ones(1024, device="cuda")
+    worst = 0.0
+    for i, (dot, deps, t, _kind) in enumerate(st):
+        h.handle_add(dot, dot, [0], deps, t)
+        out += [d for d, _ in h.drain_dots()]
+        if i % 20 == 0:
+            t0 = time.perf_counter()
+            y = (x * 2).sum().item()  # default-stream work + a synchronising copy
+            worst = max(worst, time.perf_counter() - t0)
+            assert y == 2048.0
+    out += [d for d, _ in h.drain_dots()]
+    h.close()
+    assert out == exp
+    assert worst < 0.5, worst
+
+
+def test_executor_persistent_mailbox_line_is_used(gpu):
+    """One-Add flushes carry their row in the mailbox line next to the
+    doorbell; the line's checksum (fx_internal.h persist_mb_mix) rejects a
+    line read across two flushes, which then takes the ring path.  On an
+    undisturbed drain-after-every-Add loop almost every flush takes the
+    mailbox (a wrong checksum would silently fall back to the ring for all),
+    and the order equals the oracle's."""
+    p = fs.synth_params(seed=10, n=5, instances=1, cmds=60, window=8, cycle_pct=30, conflicts=(10,))
+    st = fs.synth_host(p).stream(0)[:200]
+    g = oracle_lib.Graph(1, 5)
+    for (dot, deps, t, _kind) in st:
+        g.handle_add(dot, deps, t)
+    exp = [d for d, _, _ in g.drain()]
+    h = _with_env({"FX_HANDLE_STATS": 1}, lambda: GraphExecutor(1, 0, 5, monitor=False))
+    out = []
+    for (dot, deps, t, _kind) in st:
+        h.handle_add(dot, dot, [0], deps, t)
+        out += [d for d, _ in h.drain_dots()]
+    s = h.persist_stats()
+    h.close()
+    assert out == exp
+    flushes, mailbox = s[0], s[14]
+    assert flushes == len(st)
+    assert mailbox >= 0.9 * flushes, (mailbox, flushes)
