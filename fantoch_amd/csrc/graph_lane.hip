@@ -597,8 +597,11 @@ struct Lane {
   }
 };
 
+// Two waves per SIMD where the LDS allows it: the 8-cached-deps builds take
+// 35-37 KB of LDS per wavefront, so a CU holds four (one per SIMD) whatever
+// the register count, and they declare one (their 256 VGPRs then cost nothing)
 template <uint32_t NS, uint32_t DC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DC <= 5 ? 2 : 1)))
 void k_graph_lane(KArgs a) {
   using L = Lane<NS, DC>;
   constexpr uint32_t NP = 2 + DC;  // planes per block: dot, hdr, deps

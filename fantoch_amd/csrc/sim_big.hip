@@ -41,6 +41,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "fantoch_amd.h"
@@ -94,7 +95,7 @@ enum : uint32_t { R_PST = 0, R_START = 1, R_WAIT = 2, R_TL = 3, R_MARK = 4, R_NE
 struct GeoX {  // launch-uniform geometry (words)
   uint32_t n, C, K, Q, qlog, NS, R, ncli_keys;
   uint32_t amax, vmax, sl_value, sl_ack, SW;
-  uint32_t o_slot, o_rec, o_kd, o_cl, o_kh, o_kl, o_inf, o_arg, o_gp, o_free, o_gco, o_tstk, o_fv, o_fi, o_wl,
+  uint32_t o_slot, o_rec, o_kd, o_cl, o_kh, o_kl, o_inf, o_arg, o_gp, o_free, o_gco, o_tstk, o_fv, o_fi, o_fp, o_wl,
       o_tmp, o_tl, o_tw, o_rdy;
   uint32_t words;  // per instance
 };
@@ -177,7 +178,15 @@ enum : uint32_t { PF_POP = 0, PF_EVENT = 1, PF_XADD = 2, PF_FIND = 3, PF_CHECK =
                   PC_EVENTS = 22, PC_SEND = 23, PC_CACHE = 11 };
 
 // NG: registers of group minima per lane (message pool <= 4096 NG entries)
-template <uint32_t NG>
+// LX: the Tarjan state of a search in LDS (a u16 id word per dot slot,
+// search-epoch tagged, and the Tarjan stack as u16 slots) instead of the
+// per-(slot, process) HBM records: no HBM store per DFS recursion and no HBM
+// round trip to resume a frame (tarjan.rs:96-316 needs a dep's state only as
+// "unvisited / on the stack (id) / assigned to an SCC", and within one search
+// a visited vertex that is not executed is on the stack).  For slot tables of
+// fewer than 4,096 dots and <= 32 deps per vertex (configs[3]: 2,560 slots,
+// 10 KB of LDS per instance).
+template <uint32_t NG, bool LX = false>
 struct Big {
   // ---------------------------------------------------------------- context
   uint32_t lid;
@@ -185,6 +194,9 @@ struct Big {
   GeoX g;
   uint32_t* M;    // this instance's arena
   uint32_t* lds;  // histogram caches
+  uint16_t* ltl;   // LX: Tarjan word per slot: id (12) | assigned to an SCC << 12 | search epoch (3) << 13
+  uint16_t* lstk;  // LX: Tarjan stack (slots)
+  uint32_t tep = 7;  // LX: the search epoch (1..7; the table is cleared when it wraps to 1)
   uint32_t inst;
   uint64_t seed, rng_inst;
   uint32_t protocol, n, f, synod_f, gc_ms, en_ms, cmds, conflict_, pool, extra, ro_pct;
@@ -255,6 +267,52 @@ struct Big {
     const uint32_t sl = hslot(d);
     return rd(S(sl, SL_DOT)) == d ? sl : NONE;
   }
+
+  // ------------------------------------------------- handler row prefetch
+  // A handler reads many words of one dot slot and of its record at the
+  // handling process, one dependent HBM round trip each.  Instead the slot's
+  // first HR_S words (lanes 0 .. HR_S - 1) and the record (lanes HR_S ..
+  // HR_S + 15) come in ONE lane-parallel load when the handler starts; the
+  // handler reads them with readlanes and writes through sput / rput, which
+  // keep the copy current.  Words past HR_S (the ack deps of high processes
+  // in large geometries) are read from the arena.  x_add, run right after
+  // the handler that committed the slot, reuses the copy.
+  static constexpr uint32_t HR_S = 48;
+  uint32_t hsl = NONE, hpp = NONE, hrow = 0;
+  __device__ __forceinline__ void hload(uint32_t sl, uint32_t p) {
+    hsl = sl;
+    hpp = p;
+    hrow = lid < HR_S ? (lid < g.SW ? S(sl, lid) : 0u) : RC(sl, p, lid - HR_S);
+  }
+  // the slot of a live dot with its row and p's record loaded (always from
+  // the arena: other events wrote it since); NONE if the slot no longer holds
+  // the dot
+  __device__ __forceinline__ uint32_t hslot_of(uint32_t d, uint32_t p) {
+    if (!src_ok(d)) return NONE;
+    const uint32_t sl = hslot(d);
+    hload(sl, p);
+    return rl(hrow, SL_DOT) == d ? sl : NONE;
+  }
+  __device__ __forceinline__ uint32_t sv(uint32_t w) { return w < HR_S ? rl(hrow, w) : rd(S(hsl, w)); }
+  __device__ __forceinline__ void sput(uint32_t w, uint32_t v) {
+    put(S(hsl, w), v);
+    if (w < HR_S) lset(hrow, w, v);
+  }
+  __device__ __forceinline__ uint32_t rv(uint32_t w) { return rl(hrow, HR_S + w); }
+  __device__ __forceinline__ void rput(uint32_t w, uint32_t v) {
+    put(RC(hsl, hpp, w), v);
+    lset(hrow, HR_S + w, v);
+  }
+  // lane-parallel read of slot words w0 + lid for lanes with lid < cnt
+  __device__ __forceinline__ uint32_t svl(uint32_t w0, uint32_t cnt) {
+    const uint32_t w = w0 + lid;
+    const uint32_t gv = gather(hrow, w & 63u);
+    if (lid >= cnt) return 0u;
+    return w < HR_S ? gv : S(hsl, w);
+  }
+  // the copy is valid from a handler's hslot_of to the end of the x_add that
+  // follows it (run_handlers drops it after that)
+  __device__ __forceinline__ void hforget() { hsl = hpp = NONE; }
 
   // ------------------------------------------------------------- histograms
   __device__ __forceinline__ void hist_chain(uint32_t v) {
@@ -514,26 +572,26 @@ struct Big {
   // basic.rs:187-211 handle_mstore: the command arrives; a member of the
   // coordinator's quorum acks; a commit that arrived first is applied now
   __device__ __forceinline__ void h_mstore(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
+    const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
       err = FX_ERR_SIM_LATE;
       return;
     }
-    const uint32_t ps = rd(RC(sl, p, R_PST));
-    put(RC(sl, p, R_PST), (ps & ~(3u | PS_BUF)) | ST_PAYLOAD);
-    if ((rd(S(sl, SL_QUORUM)) >> p) & 1u) act_send(M_STORE_ACK, dot, 1u << from);
+    const uint32_t ps = rv(R_PST);
+    rput(R_PST, (ps & ~(3u | PS_BUF)) | ST_PAYLOAD);
+    if ((sv(SL_QUORUM) >> p) & 1u) act_send(M_STORE_ACK, dot, 1u << from);
     if (ps & PS_BUF) h_bcommit(p, dot);  // buffered_mcommits.remove
   }
   // basic.rs:213-230 handle_mstoreack: f + 1 acks commit
   __device__ __forceinline__ void h_mstoreack(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
+    const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
       err = FX_ERR_SIM_LATE;
       return;
     }
-    const uint32_t masks = rd(S(sl, SL_MASKS));
+    const uint32_t masks = sv(SL_MASKS);
     const uint32_t acks = (masks & 0xFFu) | (1u << from);
-    put(S(sl, SL_MASKS), (masks & ~0xFFu) | acks);
+    sput(SL_MASKS, (masks & ~0xFFu) | acks);
     if (pop32(acks) == f + 1u) act_send(M_COMMIT_BASIC, dot, (1u << n) - 1u);
   }
   // basic.rs:232-257 handle_mcommit, and BasicExecutor::handle for each key at
@@ -541,19 +599,19 @@ struct Big {
   // oracle's execution log), the key results go to AggregatePending; no
   // ExecutionDelay / ChainSize samples
   __device__ __forceinline__ void h_bcommit(uint32_t p, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
+    const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
       err = FX_ERR_SIM_LATE;
       return;
     }
-    const uint32_t ps = rd(RC(sl, p, R_PST));
+    const uint32_t ps = rv(R_PST);
     if ((ps & 3u) == ST_START) {  // buffered_mcommits.insert
-      put(RC(sl, p, R_PST), ps | PS_BUF);
+      rput(R_PST, ps | PS_BUF);
       return;
     }
-    put(RC(sl, p, R_PST), (ps & ~3u) | ST_COMMIT);
-    const uint32_t c = rd(S(sl, SL_CLIENT));
-    const uint32_t nk = (rd(S(sl, SL_CNT)) >> 16) & 3u;
+    rput(R_PST, (ps & ~3u) | ST_COMMIT);
+    const uint32_t c = sv(SL_CLIENT);
+    const uint32_t nk = (sv(SL_CNT) >> 16) & 3u;
     const uint32_t x0 = rl(pexec, p);
     if (lid < nk && A.executed && x0 + lid < A.exec_cap)
       A.executed[((size_t)inst * n + p) * A.exec_cap + x0 + lid] = dot;
@@ -561,48 +619,48 @@ struct Big {
     if ((rd(CL(c, 0)) & 0xFFu) == p) client_result(c, nk);  // pending.wait_for registered this rifl at p
     if (err) return;
     if (gc_ms) gc_commit(p, dot);  // Forward(MCommitDot) (basic.rs:246-251), before the slot can go
-    const uint32_t masks = rd(S(sl, SL_MASKS));
-    if (((masks >> 24) & 0xFFu) + 1u == n) put(S(sl, SL_DOT), 0u);  // executed everywhere: free the slot
-    else put(S(sl, SL_MASKS), masks + (1u << 24));
+    const uint32_t masks = sv(SL_MASKS);
+    if (((masks >> 24) & 0xFFu) + 1u == n) sput(SL_DOT, 0u);  // executed everywhere: free the slot
+    else sput(SL_MASKS, masks + (1u << 24));
   }
 
   // atlas.rs:251-325 / epaxos.rs:223-301
   __device__ __forceinline__ void h_mcollect(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
+    const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
       err = FX_ERR_SIM_LATE;
       return;
     }
-    const uint32_t ps = rd(RC(sl, p, R_PST));
+    const uint32_t ps = rv(R_PST);
     if ((ps & 3u) != ST_START) return;
-    const uint32_t qm = rd(S(sl, SL_QUORUM)) & 0xFFu;
+    const uint32_t qm = sv(SL_QUORUM) & 0xFFu;
     if (!((qm >> p) & 1u)) {
       const uint32_t ps2 = (ps & ~3u) | ST_PAYLOAD;
       if (ps & PS_BUF) {  // buffered commit (atlas.rs:288-292)
-        put(RC(sl, p, R_PST), ps2 & ~PS_BUF);
+        rput(R_PST, ps2 & ~PS_BUF);
         h_mcommit(p, (ps >> 4) & 15u, dot);
       } else {
-        put(RC(sl, p, R_PST), ps2);
+        rput(R_PST, ps2);
       }
       return;
     }
     const bool from_self = from == p;
-    const uint32_t cnt = rd(S(sl, SL_CNT));
+    const uint32_t cnt = sv(SL_CNT);
     const uint32_t ncol = cnt & 0xFFu, nk = (cnt >> 16) & 3u;
     const bool ro = (cnt >> 18) & 1u;
-    const uint32_t colv = lid < ncol ? S(sl, SL_COLLECT + lid) : 0u;
+    const uint32_t colv = svl(SL_COLLECT, ncol);
     uint32_t depv = 0, nd = 0;
     if (from_self) {
       depv = colv;
       nd = ncol;
     } else {
-      nd = add_cmd(p, dot, rd(S(sl, SL_KEYS)), nk, ro, colv, ncol, depv);
+      nd = add_cmd(p, dot, sv(SL_KEYS), nk, ro, colv, ncol, depv);
     }
     if (nd > g.amax) {
       fail_cap(__LINE__);
       return;
     }
-    put(RC(sl, p, R_PST), (ps & ~3u) | ST_COLLECT);
+    rput(R_PST, (ps & ~3u) | ST_COLLECT);
     if (lid < g.amax) S(sl, g.sl_ack + p * g.amax + lid) = lid < nd ? depv : 0u;
     if (protocol == FX_PROTOCOL_EPAXOS && from_self) return;  // epaxos.rs:290-300
     act_send(M_COLLECT_ACK, dot, 1u << from);
@@ -610,23 +668,25 @@ struct Big {
 
   // atlas.rs:327-402 / epaxos.rs:303-368
   __device__ __forceinline__ void h_mcollectack(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
+    const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
       err = FX_ERR_SIM_LATE;
       return;
     }
-    if ((rd(RC(sl, p, R_PST)) & 3u) != ST_COLLECT) return;
-    const uint32_t masks = rd(S(sl, SL_MASKS));
+    if ((rv(R_PST) & 3u) != ST_COLLECT) return;
+    const uint32_t masks = sv(SL_MASKS);
     const uint32_t part = (masks & 0xFFu) | (1u << from);
-    put(S(sl, SL_MASKS), (masks & ~0xFFu) | part);
-    const uint32_t qs = rd(S(sl, SL_QUORUM)) >> 8;
+    sput(SL_MASKS, (masks & ~0xFFu) | part);
+    const uint32_t qs = sv(SL_QUORUM) >> 8;
     const uint32_t fq_eff = protocol == FX_PROTOCOL_EPAXOS ? qs - 1u : qs;  // EPaxosInfo (epaxos.rs:650-662)
     if (pop32(part) != fq_eff) return;
     // QuorumDeps: union + per-dep report counts; lanes [q amax, (q + 1) amax)
     // hold process q's reported deps
     const uint32_t q = lid / g.amax, j = lid % g.amax;
+    const uint32_t aw = g.sl_ack + q * g.amax + j;
+    const uint32_t ag = gather(hrow, aw & 63u);
     uint32_t v = 0;
-    if (q < n && ((part >> q) & 1u)) v = S(sl, g.sl_ack + q * g.amax + j);
+    if (q < n && ((part >> q) & 1u)) v = aw < HR_S ? ag : S(sl, aw);
     const bool valid = v != 0;
     uint32_t cnt = 0;
     bool first = valid;
@@ -654,9 +714,9 @@ struct Big {
     }
     uint32_t rank = 0;
     for (uint64_t m = um; m; m &= m - 1) rank += rl(v, ctz64(m)) < v ? 1u : 0u;
-    if (first) S(sl, g.sl_value + rank) = v;
-    const uint32_t c0 = rd(S(sl, SL_CNT));
-    put(S(sl, SL_CNT), (c0 & ~0xFF00u) | (nu << 8) | (fast ? 0u : (1u << 19)));
+    if (first) S(sl, g.sl_value + rank) = v;  // (the copy's value words go stale: not read again here)
+    const uint32_t c0 = sv(SL_CNT);
+    sput(SL_CNT, (c0 & ~0xFF00u) | (nu << 8) | (fast ? 0u : (1u << 19)));
     const bool ro = (c0 >> 18) & 1u;
     if (lid == p) {  // BaseProcess::path (base.rs:229-243)
       if (fast) {
@@ -692,59 +752,59 @@ struct Big {
 
   // atlas.rs:404-475 / epaxos.rs:370-428
   __device__ __forceinline__ void h_mcommit(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
+    const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
       err = FX_ERR_SIM_LATE;
       return;
     }
-    const uint32_t ps = rd(RC(sl, p, R_PST));
+    const uint32_t ps = rv(R_PST);
     if ((ps & 3u) == ST_START) {  // buffered_commits.insert
-      put(RC(sl, p, R_PST), (ps & ~0xF4u) | PS_BUF | (from << 4));
+      rput(R_PST, (ps & ~0xF4u) | PS_BUF | (from << 4));
       return;
     }
     if ((ps & 3u) == ST_COMMIT) return;
     xinfo = sl;  // to_executors.push(GraphExecutionInfo::add(dot, cmd, value.deps))
-    put(RC(sl, p, R_PST), (ps & ~3u) | ST_COMMIT);
-    const uint32_t masks = rd(S(sl, SL_MASKS));
-    put(S(sl, SL_MASKS), masks + (1u << 16));
+    rput(R_PST, (ps & ~3u) | ST_COMMIT);
+    const uint32_t masks = sv(SL_MASKS);
+    sput(SL_MASKS, masks + (1u << 16));
     if (gc_ms) gc_commit(p, dot);  // Forward(MCommitDot) to self
   }
 
   // atlas.rs:477-524 / epaxos.rs:430-477
   __device__ __forceinline__ void h_mconsensus(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
+    const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
       err = FX_ERR_SIM_LATE;
       return;
     }
-    const uint32_t ps = rd(RC(sl, p, R_PST));
+    const uint32_t ps = rv(R_PST);
     if ((ps & 3u) == ST_COMMIT) {  // chosen: reply with the chosen value
       act_send(M_COMMIT, dot, 1u << from);
       return;
     }
-    put(RC(sl, p, R_PST), ps | PS_ACC);
+    rput(R_PST, ps | PS_ACC);
     act_send(M_CONSENSUS_ACK, dot, 1u << from);
   }
 
   // atlas.rs:526-558 / epaxos.rs:479-517
   __device__ __forceinline__ void h_mconsensusack(uint32_t p, uint32_t from, uint32_t dot) {
-    const uint32_t sl = slot_of(dot);
+    const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
       err = FX_ERR_SIM_LATE;
       return;
     }
-    if (!((rd(S(sl, SL_CNT)) >> 19) & 1u)) return;  // proposer ballot != b
-    const uint32_t masks = rd(S(sl, SL_MASKS));
+    if (!((sv(SL_CNT) >> 19) & 1u)) return;  // proposer ballot != b
+    const uint32_t masks = sv(SL_MASKS);
     const uint32_t acc = ((masks >> 8) & 0xFFu) | (1u << from);
     if (pop32(acc) == synod_f + 1u) {
-      put(S(sl, SL_MASKS), masks & ~0xFF00u);  // reset_state
-      if (!(rd(RC(sl, p, R_PST)) & PS_ACC)) {  // single.rs:346-349 panic
+      sput(SL_MASKS, masks & ~0xFF00u);  // reset_state
+      if (!(rv(R_PST) & PS_ACC)) {  // single.rs:346-349 panic
         err = FX_ERR_SIM_LATE;
         return;
       }
       act_send(M_COMMIT, dot, (1u << n) - 1u);
     } else {
-      put(S(sl, SL_MASKS), (masks & ~0xFF00u) | (acc << 8));
+      sput(SL_MASKS, (masks & ~0xFF00u) | (acc << 8));
     }
   }
 
@@ -975,7 +1035,9 @@ struct Big {
   __device__ __forceinline__ uint32_t find_scc(uint32_t rsl, uint32_t* missing, uint32_t mark_epoch, bool* saved) {
     XPROF_T0();
     XPROF_CNT(PC_FIND, 1);
-    const uint32_t r = find_scc_(rsl, missing, mark_epoch, saved);
+    uint32_t r;
+    if constexpr (LX) r = find_scc_lx_(rsl, missing, mark_epoch, saved);
+    else r = find_scc_(rsl, missing, mark_epoch, saved);
     XPROF_ADD(PF_FIND);
     return r;
   }
@@ -1102,6 +1164,227 @@ struct Big {
     return result;
   }
 
+  // ====================================================== LX search
+  static constexpr uint32_t LT_ID = 0xFFFu, LT_SCC = 0x1000u;
+  __device__ __forceinline__ uint32_t lt_get(uint32_t sl) { return uni(ltl[sl]); }
+  __device__ __forceinline__ void lt_set(uint32_t sl, uint32_t v) { ltl[sl] = (uint16_t)v; }  // every lane, same word
+  // the id of a vertex visited by this search (0: not visited)
+  __device__ __forceinline__ uint32_t lt_id(uint32_t e) const { return (e >> 13) == tep ? e & LT_ID : 0u; }
+
+  // the static state of a frame's deps (lanes [0, cnd)): a dep that is the
+  // vertex itself, of a freed slot or executed at xp is skipped (tarjan.rs:
+  // 128-145); one not in xp's graph is missing (148-157); the others are
+  // pending.  None of these change during the search (no vertex is added, and
+  // an SCC member executes only through the search, which the LDS word
+  // records), so a resumed frame needs no reload.  Returns the pending mask;
+  // *jm = the first missing dep (the search stops there), 63 if none.
+  __device__ __forceinline__ uint32_t dep_status(uint32_t drow, uint32_t cnd, uint32_t cdot, uint32_t& jm) {
+    uint32_t tag = 0, ps = 0;
+    const bool live = lid < cnd && drow != cdot && src_ok(drow);
+    if (live) {
+      const uint32_t sl = hslot(drow);
+      tag = S(sl, SL_DOT);
+      ps = RC(sl, xp, R_PST);
+    }
+    const bool act = live && tag == drow && !(ps & PS_EXEC);
+    const uint64_t miss = bal(act && !(ps & PS_INGRAPH));
+    jm = miss ? ctz64(miss) : 63u;
+    return (uint32_t)bal(act && (ps & PS_INGRAPH));
+  }
+
+  // save_scc for the LX search: the members lstk[base, base + cnt) (their LDS
+  // words already say "assigned"); ranks by dot computed lane-parallel and,
+  // for up to 64 members, permuted across lanes with no memory round trip;
+  // the executed-clock bit of each member is set here (tarjan.rs:293).
+  __device__ __forceinline__ void save_scc_lx(uint32_t base, uint32_t cnt) {
+    hist_chain(cnt);
+    ++xe;  // the graph lost vertices: every cached search result of xp is stale
+    if (nwl + cnt > 2u * g.NS) {
+      fail_cap(__LINE__);
+      return;
+    }
+    const uint32_t p = xp;
+    XPROF_T0();
+    // member slots and dots in lanes (chunks of 64), ranked by dot
+    bool direct = cnt <= 64u;
+    uint32_t sorted = 0;
+    for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
+      const uint32_t i = i0 + lid;
+      const uint32_t msl = i < cnt ? (uint32_t)lstk[base + i] : 0u;
+      const uint32_t md = i < cnt ? S(msl, SL_DOT) : NONE;
+      uint32_t rank = 0;
+      for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+        const uint32_t k = k0 + lid;
+        const uint32_t kd = k0 == i0 ? md : (k < cnt ? S((uint32_t)lstk[base + k], SL_DOT) : NONE);
+        const uint32_t m = min(64u, cnt - k0);
+        for (uint32_t j = 0; j < m; ++j) rank += rl(kd, j) < md ? 1u : 0u;
+      }
+      if (direct) {
+        // lane rank <- member i (ds_permute: a forward permutation)
+        sorted = (uint32_t)__builtin_amdgcn_ds_permute((int)((i < cnt ? rank : 63u) << 2), (int)msl);
+      } else if (i < cnt) {
+        W(g.o_tl, rank) = msl;
+      }
+    }
+    XPROF_ADD(PF_SORT);
+    XPROF_T0();
+    for (uint32_t r0 = 0; r0 < cnt && !err; r0 += 64) {
+      const uint32_t r = r0 + lid;
+      const bool act = r < cnt;
+      uint32_t sl = 0, d = 0, st = 0, wt = 0, c = 0, cw = 0, mk = 0, ps = 0;
+      if (act) {
+        sl = direct ? sorted : W(g.o_tl, r);
+        d = S(sl, SL_DOT);
+        st = RC(sl, p, R_START);
+        wt = RC(sl, p, R_WAIT);
+        ps = RC(sl, p, R_PST);
+        c = S(sl, SL_CLIENT);
+        cw = S(sl, SL_CNT);
+        mk = S(sl, SL_MASKS);
+      }
+      const uint32_t cpr = act ? CL(c, 0) : 0u;
+      const uint32_t m = min(64u, cnt - r0);
+      if (act) {
+        RC(sl, p, R_PST) = ps | PS_EXEC;  // executed_clock.add (tarjan.rs:293)
+        if (A.executed && xk + lid < A.exec_cap) A.executed[((size_t)inst * n + p) * A.exec_cap + xk + lid] = d;
+        W(g.o_wl, nwl + lid) = sl;
+        if (A.delay_hist) {  // ExecutionDelay (graph/mod.rs:514-518)
+          const uint32_t bn = min(now - st, A.delay_bins - 1u);
+          if (bn < HD_BINS) atomicAdd(&lds[HC_BINS + bn], 1u);
+          else atomicAdd(&A.delay_hist[bn], 1ull);
+        }
+        if (((mk >> 24) & 0xFFu) + 1u == n) S(sl, SL_DOT) = 0u;  // executed everywhere: free the slot
+        else S(sl, SL_MASKS) = mk + (1u << 24);
+      }
+      xk += m;
+      nwl += m;
+      const uint64_t need = bal(act && (wt != 0 || (cpr & 0xFFu) == p));
+      for (uint64_t mm = need; mm && !err; mm &= mm - 1) {
+        const uint32_t j = ctz64(mm);
+        if (rl(wt, j)) unlink(rl(sl, j));
+        if ((rl(cpr, j) & 0xFFu) == p) client_result(rl(c, j), (rl(cw, j) >> 16) & 3u);
+      }
+    }
+    XPROF_ADD(PF_EMIT);
+  }
+
+  // find_scc + strong_connect + finalize (as find_scc_) over the LDS state.
+  // Frames 0..63 in lanes: slot | next dep << 24; stack position | low << 12 |
+  // first missing dep << 24; the pending-deps mask.  Deeper frames in
+  // W(o_fv / o_fi / o_fp).
+  __device__ __forceinline__ uint32_t find_scc_lx_(uint32_t rsl, uint32_t* missing, uint32_t mark_epoch, bool* saved) {
+    const uint32_t p = xp;
+    *saved = false;
+    tep = tep == 7u ? 1u : tep + 1u;
+    if (tep == 1u) {  // the epoch wrapped: no word of an older search may match
+      uint32_t* w = reinterpret_cast<uint32_t*>(ltl);
+      for (uint32_t i = lid; i < g.NS / 2u; i += 64) w[i] = 0u;
+    }
+    const uint32_t te = tep << 13;
+    idc = 1;
+    tsp = 0;
+    uint32_t frs = 0, frt = 0, frp = 0;
+    lt_set(rsl, 1u | te);
+    lstk[tsp++] = (uint16_t)rsl;
+    fsp = 1;
+    uint32_t cv = rsl, ci = 0, cid = 1, clow = 1, ctp = 0, cdot = 0, cnd = 0, drow = 0, jm = 63u;
+    frame_row(rsl, cdot, cnd, drow);
+    uint32_t pm = dep_status(drow, cnd, cdot, jm);
+    uint32_t result = FOUND;
+    for (uint32_t guard = 0; fsp && !err; ++guard) {
+      if (guard > 64u * g.NS + 64u) {
+        fail_cap(__LINE__);
+        break;
+      }
+      // the next pending dep before the first missing one
+      const uint32_t lim = min(cnd, jm);
+      const uint32_t rest = ci < 32u ? (pm >> ci) << ci : 0u;
+      const uint32_t nx = rest ? (uint32_t)__builtin_ctz(rest) : 32u;
+      XPROF_CNT(PC_EDGES, 1);
+      if (nx < lim) {
+        ci = nx + 1u;
+        const uint32_t d = rl(drow, nx), sl = hslot(d);
+        const uint32_t lw = lt_get(sl), id = lt_id(lw);
+        if (id == 0) {  // recurse (tarjan.rs:172-214)
+          XPROF_CNT(PC_RECURSE, 1);
+          const uint32_t f = fsp - 1u;
+          const uint32_t fw = cv | (ci << 24), tw = ctp | (clow << 12) | (jm << 24);
+          if (f < 64u) {
+            lset(frs, f, fw);
+            lset(frt, f, tw);
+            lset(frp, f, pm);
+          } else {
+            put(W(g.o_fv, f), fw);
+            put(W(g.o_fi, f), tw);
+            put(W(g.o_fp, f), pm);
+          }
+          ++idc;
+          if (idc > LT_ID || tsp >= g.NS || fsp >= g.NS) {
+            fail_cap(__LINE__);
+            break;
+          }
+          lt_set(sl, idc | te);
+          ctp = tsp;
+          lstk[tsp++] = (uint16_t)sl;
+          ++fsp;
+          cv = sl;
+          ci = 0;
+          cid = idc;
+          clow = idc;
+          frame_row(sl, cdot, cnd, drow);
+          pm = dep_status(drow, cnd, cdot, jm);
+        } else if (!(lw & LT_SCC)) {  // on the stack (tarjan.rs:215-225)
+          clow = min(clow, id);
+        }
+        continue;
+      }
+      if (jm < cnd && ci <= jm) {  // missing (tarjan.rs:148-157, shard_count == 1)
+        *missing = rl(drow, jm);
+        result = MISSING;
+        break;
+      }
+      // cv finished
+      const uint32_t lowv = clow;
+      if (cid == lowv) {  // SCC root: the members lstk[ctp, tsp) (tarjan.rs:233-312)
+        for (uint32_t i = ctp + lid; i < tsp; i += 64) {
+          const uint32_t x = lstk[i];
+          ltl[x] = (uint16_t)(ltl[x] | LT_SCC);
+        }
+        save_scc_lx(ctp, tsp - ctp);
+        tsp = ctp;
+        *saved = true;
+        if (err) break;
+      }
+      --fsp;
+      if (fsp) {  // resume the parent frame (tarjan.rs:211: low = min(low, dep low))
+        const uint32_t f = fsp - 1u;
+        uint32_t fw, tw;
+        if (f < 64u) {
+          fw = rl(frs, f);
+          tw = rl(frt, f);
+          pm = rl(frp, f);
+        } else {
+          fw = rd(W(g.o_fv, f));
+          tw = rd(W(g.o_fi, f));
+          pm = rd(W(g.o_fp, f));
+        }
+        cv = fw & 0xFFFFFFu;
+        ci = fw >> 24;
+        ctp = tw & 0xFFFu;
+        jm = tw >> 24;
+        clow = min((tw >> 12) & LT_ID, lowv);
+        cid = lt_id(lt_get(cv));
+        frame_row(cv, cdot, cnd, drow);
+      }
+    }
+    // finalize: a failed search marks the vertices left on the stack visited
+    // (try_pending's skip rule); their LDS words lapse with the epoch
+    if (mark_epoch && result == MISSING)
+      for (uint32_t i = lid; i < tsp; i += 64) RC((uint32_t)lstk[i], p, R_MARK) = mark_epoch << 1;
+    tsp = 0;
+    return result;
+  }
+
   // PendingIndex::remove (index.rs:204-207) of the released dot in slot x:
   // unregisters its waiters and sorts them ascending (C2) into W(o_tw, ..)
   __device__ __forceinline__ uint32_t take_waiters(uint32_t x) {
@@ -1145,27 +1428,42 @@ struct Big {
     xk = rl(pexec, p);
     xe = rl(pxe, p);
     nwl = 0;
-    const uint32_t d = rd(S(sl, SL_DOT));
-    const uint32_t ps = rd(RC(sl, p, R_PST));
+    // the slot's row and p's record: the copy the committing handler loaded
+    // (run_handlers calls x_add right after h_mcommit), else one load
+    if (hsl != sl || hpp != p) hload(sl, p);
+    const uint32_t d = sv(SL_DOT);
+    const uint32_t ps = rv(R_PST);
     if (ps & (PS_INGRAPH | PS_EXEC)) {
       err = FX_ERR_DOUBLE_INDEX;
       return;
     }
-    const uint32_t vc = (rd(S(sl, SL_CNT)) >> 8) & 0xFFu;
+    const uint32_t vc = (sv(SL_CNT) >> 8) & 0xFFu;
     deps_total += vc;
-    const uint32_t depj = lid < vc ? S(sl, g.sl_value + lid) : 0u;
+    const uint32_t depj = svl(g.sl_value, vc);
+    // every dep's slot tag and record at p in one round trip (lane j: dep j):
+    // AEClock::contains (tarjan.rs:131-132: a freed slot was executed
+    // everywhere) and the search-result cache words below
+    uint32_t dtag = 0, dps = 0, dcm = 0, dce = 0;
+    const bool dl = lid < vc && depj != d && src_ok(depj);
+    if (dl) {
+      const uint32_t dsl = hslot(depj);
+      dtag = S(dsl, SL_DOT);
+      dps = RC(dsl, p, R_PST);
+      dcm = RC(dsl, p, R_CMISS);
+      dce = RC(dsl, p, R_CEPOCH);
+    }
     bool keep = false;
-    if (lid < vc && depj != d) keep = !contains_v(depj);
+    if (lid < vc && depj != d) keep = !src_ok(depj) || (dtag == depj && !(dps & PS_EXEC));
     bool first = bal(keep) != 0;
     if (!first) {  // every dep executed: a singleton SCC
       XPROF_CNT(PC_FAST, 1);
-      put(RC(sl, p, R_PST), ps | PS_EXEC);
+      rput(R_PST, ps | PS_EXEC);
       ++xe;
       hist_chain(1u);
       put(W(g.o_wl, nwl++), sl);
       on_execute(sl, d, now);
     } else {
-      put(RC(sl, p, R_PST), ps | PS_INGRAPH);
+      rput(R_PST, ps | PS_INGRAPH);
       put(RC(sl, p, R_START), now);  // Vertex::start_time_ms (tarjan.rs:332-348)
       // The first search from the new vertex v enters its first dep u that is
       // neither v nor executed (deps ascend, C1).  If u is pending and the last
@@ -1178,23 +1476,30 @@ struct Big {
       // missing then).  So v just waits on m (index_pending) — no walk; and
       // v's own result is the same cache entry.
       const uint32_t j0 = ctz64(bal(keep));
-      const uint32_t u = rl(depj, j0), usl = hslot(u);
-      const uint32_t ut = S(usl, SL_DOT), ups = RC(usl, p, R_PST), ucm = RC(usl, p, R_CMISS),
-                     uce = RC(usl, p, R_CEPOCH);
-      const uint32_t cm = uni(ucm);
-      if (uni(ut) == u && (uni(ups) & (PS_INGRAPH | PS_EXEC)) == PS_INGRAPH && cm && cm != d &&
-          uni(uce) == xe && src_ok(cm)) {
+      const uint32_t u = rl(depj, j0);
+      const uint32_t ut = rl(dtag, j0), ups = rl(dps, j0), cm = rl(dcm, j0), uce = rl(dce, j0);
+      if (src_ok(u) && ut == u && (ups & (PS_INGRAPH | PS_EXEC)) == PS_INGRAPH && cm && cm != d && uce == xe &&
+          src_ok(cm)) {
+        // m's tag, its record at p and the head of its waiter list together
         const uint32_t msl = hslot(cm);
-        const uint32_t mt = S(msl, SL_DOT), mps = RC(msl, p, R_PST);
+        const uint32_t mt = S(msl, SL_DOT), mps = RC(msl, p, R_PST), mh = RC(msl, p, R_HEAD);
         if (uni(mt) == cm && !(uni(mps) & (PS_INGRAPH | PS_EXEC))) {
           XPROF_CNT(PC_CACHE, 1);
-          index_pending(sl, cm);
+          // index_pending (mod.rs:525-554) of the fresh vertex (it waits on
+          // nothing yet: its record was zeroed when its dot was proposed)
+          const uint32_t h = uni(mh);
+          put(RC(sl, p, R_NEXT), h);
+          put(RC(sl, p, R_PREV), 0u);
+          if (h) put(RC(h - 1u, p, R_PREV), sl + 1u);
+          put(RC(msl, p, R_HEAD), sl + 1u);
+          put(RC(sl, p, R_WAIT), msl + 1u);
           put(RC(sl, p, R_CMISS), cm);
           put(RC(sl, p, R_CEPOCH), xe);
           first = false;
         }
       }
     }
+    hforget();
     XPROF_T0();
     uint32_t wk = 0, wcnt = 0, cur = 0;  // the waiter list being tried
     uint32_t wps = 0, wmk = 0, wbase = NONE;  // lanes: states of waiters [wbase, wbase + 64)
@@ -1312,6 +1617,7 @@ struct Big {
           xinfo = NONE;
           x_add(p, sl);
         }
+        hforget();
         continue;
       }
       if (nfrm == 0) return;
@@ -1417,12 +1723,19 @@ struct Big {
   }
 };
 
-template <uint32_t NG>
-__global__ __launch_bounds__(64, 3) void k_simx(ArgsX a) {
-  __shared__ uint32_t smem[LDS_WORDS];
+// waves per SIMD the register budget is built for (3: 168 VGPRs, no spills)
+#ifndef FX_SIMX_WAVES
+#define FX_SIMX_WAVES 3
+#endif
+template <uint32_t NG, bool LX>
+__global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
+  // LDS_WORDS of histogram caches, then (LX) the Tarjan words and stack: u16[NS] each
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
-  Big<NG> s;
+  Big<NG, LX> s;
+  s.ltl = reinterpret_cast<uint16_t*>(smem + LDS_WORDS);
+  s.lstk = s.ltl + a.g.NS;
   s.lid = threadIdx.x;
   s.A = a;
   s.g = a.g;
@@ -1675,6 +1988,7 @@ bool simx_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t dots, simx::Ge
   take(g.o_tstk, g.NS);
   take(g.o_fv, g.NS);
   take(g.o_fi, g.NS);
+  take(g.o_fp, g.NS);
   take(g.o_wl, 2ull * g.NS);
   take(g.o_tmp, g.NS);
   take(g.o_tl, g.NS);
@@ -1729,9 +2043,23 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
   a.stats = (unsigned long long*)o->stats;
   a.err = o->err;
   const dim3 grid(b->instances), block(64);
-  if (a.g.R <= 4096) hipLaunchKernelGGL(k_simx<1>, grid, block, 0, hs, a);
-  else if (a.g.R <= 8192) hipLaunchKernelGGL(k_simx<2>, grid, block, 0, hs, a);
-  else hipLaunchKernelGGL(k_simx<4>, grid, block, 0, hs, a);
+  // the LDS Tarjan state (LX) when its ids fit 12 bits and a frame's deps a
+  // 32-bit mask; FX_SIMX_LX=0 in the environment forces the HBM records (A/B)
+  static const bool lx_env = [] {
+    const char* e = std::getenv("FX_SIMX_LX");
+    return !(e && e[0] == '0');
+  }();
+  const bool lx = lx_env && a.g.NS < 4096u && a.g.vmax <= 32u;
+  const size_t lds = (size_t)(LDS_WORDS + (lx ? a.g.NS : 0u)) * 4u;
+  if (lx) {
+    if (a.g.R <= 4096) hipLaunchKernelGGL((k_simx<1, true>), grid, block, lds, hs, a);
+    else if (a.g.R <= 8192) hipLaunchKernelGGL((k_simx<2, true>), grid, block, lds, hs, a);
+    else hipLaunchKernelGGL((k_simx<4, true>), grid, block, lds, hs, a);
+  } else {
+    if (a.g.R <= 4096) hipLaunchKernelGGL((k_simx<1, false>), grid, block, lds, hs, a);
+    else if (a.g.R <= 8192) hipLaunchKernelGGL((k_simx<2, false>), grid, block, lds, hs, a);
+    else hipLaunchKernelGGL((k_simx<4, false>), grid, block, lds, hs, a);
+  }
   const hipError_t le = hipGetLastError();
   (void)hipFreeAsync(arena, hs);
   return le == hipSuccess ? FX_OK : FX_ERR_HIP;
