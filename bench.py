@@ -85,7 +85,6 @@ def parse(argv=None):
                     help="placements mode (BASELINE configs[2]): conflict rate of every placement")
     ap.add_argument("--placement-limit", type=int, default=None,
                     help="placements mode: run only the first K placements of the enumeration")
-    ap.add_argument("--traffic-json", type=str, default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     args = ap.parse_args(argv)
     for k, v in MODE_DEFAULTS.get(args.mode, MODE_DEFAULTS["sim"]).items():
         if getattr(args, k) is None:
@@ -337,21 +336,11 @@ def main():
                 kname = max(per_kernel, key=per_kernel.get)
                 dom_ms = per_kernel[kname]
             achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
-            traffic = traffic_raw = traffic_read = traffic_write = None
-            if os.path.exists(args.traffic_json):
-                try:
-                    tj = json.load(open(args.traffic_json))
-                    if tj.get("workload_key") == workload_key(args) and \
-                            tj.get("kernel") == KERNEL_NAMES.get(tier):
-                        traffic = tj.get("hbm_bytes_per_launch")
-                        traffic_raw = int(tj["fetch_size_kb"] * 1024 + tj["write_size_kb"] * 1024)
-                        traffic_read = tj.get("read_bytes_per_launch")
-                        traffic_write = tj.get("write_bytes_per_launch")
-                except Exception:
-                    traffic = None
+            # the counters come from this exact workload's PMC record
+            # (tools/mode_pmc.sh executor k_graph_lane -> profiles/pmc_executor.json)
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                    "traffic": traffic, "kernel": kname,
+                    "traffic": None, "kernel": kname,
                     "kernel_ms_avg": round(dom_ms, 4), "per_kernel_ms_avg": per_kernel,
                     "launch_ms_avg": round(kavg, 4),
                     "alg_bytes_per_launch": alg_bytes,
@@ -359,10 +348,13 @@ def main():
                     "alg_bytes_definition": "SURVEY.md 8(d): 32 + 4k + 8d per command, k = 1",
                     "plane_bytes_per_launch": plane_bytes,
                     "plane_bytes_per_cmd": round(plane_bytes / n_adds, 3),
-                    "plane_frac_of_launch": round(plane_bytes / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                    "traffic_fetch_plus_write_raw": traffic_raw,
-                    "traffic_read_corrected_x2": traffic_read,
-                    "traffic_write": traffic_write}
+                    "plane_frac_of_launch": round(plane_bytes / (kavg * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+            import bench_pmc
+            pm = bench_pmc.load("executor", args)
+            bench_pmc.attach(roof, pm, alg_bytes)
+            if pm and pm.get("kernel_pattern") and pm["kernel_pattern"] not in kname:
+                roof["traffic_note"] = ("counters of %s, the dominant kernel by rocprofv3 time; the HIP-event "
+                                        "dominant kernel here is %s" % (pm["kernel_pattern"], kname))
             copy = measured_copy_gbps(torch, dev)
             roof["measured_copy_gbps"] = copy
             roof["frac_of_measured_copy"] = round(achieved / copy, 4)

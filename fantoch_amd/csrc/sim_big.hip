@@ -109,6 +109,7 @@ struct ArgsX {
   const uint8_t* rank;
   uint32_t RP;
   uint32_t exec_cap, lat_cap, max_events, sim_exec_notif;
+  uint32_t row_prefetch;  // LX search: prefetch the first deps' rows (vmax <= 15; FX_SIMX_PF=0 turns it off)
   uint32_t* executed;
   uint32_t* executed_len;
   uint32_t* latency_log;
@@ -173,7 +174,8 @@ enum : uint32_t { FOUND = 0, MISSING = 1 };
 #define XPROF_CNT(cat, v) (void)0
 #endif
 enum : uint32_t { PF_POP = 0, PF_EVENT = 1, PF_XADD = 2, PF_FIND = 3, PF_CHECK = 4, PF_SORT = 5, PF_EMIT = 6,
-                  PF_HANDLER = 7, PF_SEND = 8, PF_GC = 9, PF_CLIENT = 10,
+                  PF_HANDLER = 7, PF_SEND = 8, PF_GC = 9, PF_CLIENT = 10, PF_READY = 12, PF_HLOAD = 13,
+                  PF_PUSH = 14, PF_DEPST = 15,
                   PC_EDGES = 16, PC_RECURSE = 17, PC_XADD = 18, PC_FIND = 19, PC_WAITERS = 20, PC_FAST = 21,
                   PC_EVENTS = 22, PC_SEND = 23, PC_CACHE = 11 };
 
@@ -207,6 +209,11 @@ struct Big {
     if (!err) err_site = line;
     err = FX_ERR_SIM_CAPACITY;
   }
+  // FX_ERR_SIM_LATE with its source line in the stats row (as capacity failures)
+  __device__ __forceinline__ void fail_late(uint32_t line) {
+    if (!err) err_site = line;
+    err = FX_ERR_SIM_LATE;
+  }
   uint32_t now = 0;  // ms
   uint32_t seq = 0;  // insertion counter (C3)
   uint64_t rdraws = 0;
@@ -220,15 +227,18 @@ struct Big {
   uint32_t nfree = 0;
   // lane p: proposal seq, Fast / Slow (and their read-only shares), executed
   // count, Stable, quorums (fast | write << 8 | majority << 16), GC reporters
-  uint32_t pseq = 0, pfast = 0, pslow = 0, pfr = 0, psr = 0, pexec = 0, pstab = 0, pq = 0, prep = 0;
+  // (packed into two VGPRs, 8 lanes a field: pa lane A_x + p, pb lane B_x + p)
+  uint32_t pa = 0, pb = 0;
+  enum : uint32_t { A_SEQ = 0, A_FAST = 8, A_SLOW = 16, A_FR = 24, A_SR = 32, A_EXEC = 40, A_STAB = 48, A_Q = 56 };
+  enum : uint32_t { B_REP = 0, B_XE = 8, B_FRW = 16, B_FRD = 32, B_FRB = 48 };  // frames: lanes B_FR* + fi (fi < 16)
   // lane p: executions so far at p, in SCCs (the epoch of the search-result cache)
-  uint32_t pxe = 0;
+
   // lane 8 p + s: p's committed frontier of source s + 1 (GC track), its
   // previous stable frontier, and the link delay p -> s
   uint32_t gcf = 0, gps = 0, dpq = 0;
   // handler frames, frame fi in lane fi: action (0 none, 1 ToSend) | kind << 2 |
   // targets << 8 | next target << 16; dot; base of its ready results
-  uint32_t frw = 0, frd = 0, frb = 0;
+
   uint32_t nfrm = 0, xinfo = NONE, rtop = 0;
   // executor (the process being run)
   uint32_t xp = 0, xk = 0, xe = 0, epoch = 0, nwl = 0, idc = 0, tsp = 0, fsp = 0;
@@ -280,9 +290,14 @@ struct Big {
   static constexpr uint32_t HR_S = 48;
   uint32_t hsl = NONE, hpp = NONE, hrow = 0;
   __device__ __forceinline__ void hload(uint32_t sl, uint32_t p) {
+    XPROF_T0();
     hsl = sl;
     hpp = p;
     hrow = lid < HR_S ? (lid < g.SW ? S(sl, lid) : 0u) : RC(sl, p, lid - HR_S);
+#ifdef FX_SIM_PROFILE
+    hrow = uni(hrow) == 0xFFFFFFFFu ? hrow + 1u : hrow;  // (waits for the load inside the bracket)
+#endif
+    XPROF_ADD(PF_HLOAD);
   }
   // the slot of a live dot with its row and p's record loaded (always from
   // the arena: other events wrote it since); NONE if the slot no longer holds
@@ -360,6 +375,12 @@ struct Big {
   // executed notification; 1 the GC event of process a; 2 the GC delivery
   // a -> b), key lo = insertion seq: the oracle's (time, class, seq) order
   __device__ __forceinline__ uint32_t push_event(uint32_t t, uint32_t cls, uint32_t info, uint32_t arg) {
+    XPROF_T0();
+    const uint32_t e = push_event_(t, cls, info, arg);
+    XPROF_ADD(PF_PUSH);
+    return e;
+  }
+  __device__ __forceinline__ uint32_t push_event_(uint32_t t, uint32_t cls, uint32_t info, uint32_t arg) {
     if (t >= TIME_LIMIT) {
       err = FX_ERR_TIME_RANGE;
       return NONE;
@@ -478,8 +499,8 @@ struct Big {
   // ------------------------------------------------------- frame stack
   __device__ __forceinline__ void act_send(uint32_t kind, uint32_t dot, uint32_t tgt) {
     const uint32_t fi = nfrm - 1;
-    lset(frw, fi, 1u | (kind << 2) | (tgt << 8));
-    lset(frd, fi, dot);
+    lset(pb, B_FRW + fi, 1u | (kind << 2) | (tgt << 8));
+    lset(pb, B_FRD + fi, dot);
   }
 
   // ============================================================ protocol
@@ -527,8 +548,8 @@ struct Big {
 
   // Protocol::submit (atlas.rs:210-249, epaxos.rs:199-221)
   __device__ __forceinline__ void h_submit(uint32_t p, uint32_t c) {
-    const uint32_t s = rl(pseq, p) + 1u;
-    lset(pseq, p, s);
+    const uint32_t s = rl(pa, A_SEQ + p) + 1u;
+    lset(pa, A_SEQ + p, s);
     if (s > FX_SEQ_MASK) {
       err = FX_ERR_DOT_RANGE;
       return;
@@ -547,7 +568,7 @@ struct Big {
     uint32_t depv = 0;
     const uint32_t nd = basic ? 0u : add_cmd(p, dot, keys, nk, ro, 0, 0, depv);
     // maybe_adjust_fast_quorum: a single-key read under NFR goes to a majority
-    const uint32_t qw = rl(pq, p);
+    const uint32_t qw = rl(pa, A_Q + p);
     const uint32_t qm = (nfr && ro && nk == 1) ? (qw >> 16) & 0xFFu : qw & 0xFFu;
     // the fresh slot in one lane-parallel pass, and its per-process records
     const uint32_t dv = gather(depv, (lid - SL_COLLECT) & 63u);
@@ -574,7 +595,7 @@ struct Big {
   __device__ __forceinline__ void h_mstore(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
-      err = FX_ERR_SIM_LATE;
+      fail_late(__LINE__);
       return;
     }
     const uint32_t ps = rv(R_PST);
@@ -586,7 +607,7 @@ struct Big {
   __device__ __forceinline__ void h_mstoreack(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
-      err = FX_ERR_SIM_LATE;
+      fail_late(__LINE__);
       return;
     }
     const uint32_t masks = sv(SL_MASKS);
@@ -601,7 +622,7 @@ struct Big {
   __device__ __forceinline__ void h_bcommit(uint32_t p, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
-      err = FX_ERR_SIM_LATE;
+      fail_late(__LINE__);
       return;
     }
     const uint32_t ps = rv(R_PST);
@@ -612,10 +633,10 @@ struct Big {
     rput(R_PST, (ps & ~3u) | ST_COMMIT);
     const uint32_t c = sv(SL_CLIENT);
     const uint32_t nk = (sv(SL_CNT) >> 16) & 3u;
-    const uint32_t x0 = rl(pexec, p);
+    const uint32_t x0 = rl(pa, A_EXEC + p);
     if (lid < nk && A.executed && x0 + lid < A.exec_cap)
       A.executed[((size_t)inst * n + p) * A.exec_cap + x0 + lid] = dot;
-    lset(pexec, p, x0 + nk);
+    lset(pa, A_EXEC + p, x0 + nk);
     if ((rd(CL(c, 0)) & 0xFFu) == p) client_result(c, nk);  // pending.wait_for registered this rifl at p
     if (err) return;
     if (gc_ms) gc_commit(p, dot);  // Forward(MCommitDot) (basic.rs:246-251), before the slot can go
@@ -628,7 +649,7 @@ struct Big {
   __device__ __forceinline__ void h_mcollect(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
-      err = FX_ERR_SIM_LATE;
+      fail_late(__LINE__);
       return;
     }
     const uint32_t ps = rv(R_PST);
@@ -670,7 +691,7 @@ struct Big {
   __device__ __forceinline__ void h_mcollectack(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
-      err = FX_ERR_SIM_LATE;
+      fail_late(__LINE__);
       return;
     }
     if ((rv(R_PST) & 3u) != ST_COLLECT) return;
@@ -718,17 +739,10 @@ struct Big {
     const uint32_t c0 = sv(SL_CNT);
     sput(SL_CNT, (c0 & ~0xFF00u) | (nu << 8) | (fast ? 0u : (1u << 19)));
     const bool ro = (c0 >> 18) & 1u;
-    if (lid == p) {  // BaseProcess::path (base.rs:229-243)
-      if (fast) {
-        ++pfast;
-        if (ro) ++pfr;
-      } else {
-        ++pslow;
-        if (ro) ++psr;
-      }
-    }
+    // BaseProcess::path (base.rs:229-243): Fast / Slow at p, and their read-only shares
+    if (lid == (fast ? A_FAST : A_SLOW) + p || (ro && lid == (fast ? A_FR : A_SR) + p)) ++pa;
     if (fast) act_send(M_COMMIT, dot, (1u << n) - 1u);
-    else act_send(M_CONSENSUS, dot, (rl(pq, p) >> 8) & 0xFFu);  // skip_prepare: ballot = coordinator
+    else act_send(M_CONSENSUS, dot, (rl(pa, A_Q + p) >> 8) & 0xFFu);  // skip_prepare: ballot = coordinator
   }
 
   // the GC track's committed clock at p (MCommitDot, gc/clock.rs:43-48): the
@@ -738,7 +752,7 @@ struct Big {
     const uint32_t si = FX_DOT_SRC(dot) - 1u, sq = FX_DOT_SEQ(dot);
     uint32_t fr = rl(gcf, p * 8u + si);
     if (sq != fr + 1u) return;
-    const uint32_t top = rl(pseq, si);
+    const uint32_t top = rl(pa, A_SEQ + si);
     for (uint32_t guard = 0; guard <= g.NS; ++guard) {
       const uint32_t nx = fr + 1u;
       if (nx > top) break;
@@ -754,7 +768,7 @@ struct Big {
   __device__ __forceinline__ void h_mcommit(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
-      err = FX_ERR_SIM_LATE;
+      fail_late(__LINE__);
       return;
     }
     const uint32_t ps = rv(R_PST);
@@ -774,7 +788,7 @@ struct Big {
   __device__ __forceinline__ void h_mconsensus(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
-      err = FX_ERR_SIM_LATE;
+      fail_late(__LINE__);
       return;
     }
     const uint32_t ps = rv(R_PST);
@@ -790,7 +804,7 @@ struct Big {
   __device__ __forceinline__ void h_mconsensusack(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
-      err = FX_ERR_SIM_LATE;
+      fail_late(__LINE__);
       return;
     }
     if (!((sv(SL_CNT) >> 19) & 1u)) return;  // proposer ballot != b
@@ -799,7 +813,7 @@ struct Big {
     if (pop32(acc) == synod_f + 1u) {
       sput(SL_MASKS, masks & ~0xFF00u);  // reset_state
       if (!(rv(R_PST) & PS_ACC)) {  // single.rs:346-349 panic
-        err = FX_ERR_SIM_LATE;
+        fail_late(__LINE__);
         return;
       }
       act_send(M_COMMIT, dot, (1u << n) - 1u);
@@ -826,21 +840,27 @@ struct Big {
   // each source is (previous stable, min over all frontiers]; MStable to self
   // erases those dots (all committed at q), counted as Stable
   __device__ __forceinline__ void gc_deliver(uint32_t q, uint32_t from, uint32_t v) {
-    const uint32_t ob = g.o_gco + (q * n + from) * n;
-    if (lid < n) {
-      const uint32_t o = W(ob, lid);
-      W(ob, lid) = max(o, v);
+    // q's table of reported frontiers (row r = the last report from r, lane
+    // r n + s = source s + 1) in one lane-parallel load; the report from
+    // `from` is merged in registers and written back
+    const uint32_t nn = n * n, base = g.o_gco + q * nn;
+    uint32_t blk = lid < nn ? W(base, lid) : 0u;
+    const uint32_t row = lid / n, src = lid - row * n;
+    const uint32_t vs = gather(v, src & 63u);
+    if (lid < nn && row == from) {
+      blk = max(blk, vs);
+      W(base, lid) = blk;
     }
-    const uint32_t rep = rl(prep, q) | (1u << from);
-    lset(prep, q, rep);
+    const uint32_t rep = rl(pb, B_REP + q) | (1u << from);
+    lset(pb, B_REP + q, rep);
     uint32_t cur = 0;
     const uint32_t mine = gather(gcf, (q * 8u + lid) & 63u);
     if (pop32(rep) == n - 1u) {
-      cur = mine;
+      cur = lid < n ? mine : 0u;
       for (uint32_t r = 0; r < n; ++r) {
         if (r == q) continue;
-        const uint32_t o = lid < n ? W(g.o_gco + (q * n + r) * n, lid) : 0u;
-        cur = min(cur, o);
+        const uint32_t o = gather(blk, (r * n + lid) & 63u);
+        if (lid < n) cur = min(cur, o);
       }
     }
     const uint32_t prev = gather(gps, (q * 8u + lid) & 63u);
@@ -850,7 +870,7 @@ struct Big {
     if ((lid >> 3) == q && (lid & 7u) < n) gps = t;
     uint32_t total = 0;
     for (uint32_t s = 0; s < n; ++s) total += rl(cnt, s);
-    if (lid == q) pstab += total;
+    if (lid == A_STAB + q) pa += total;
   }
 
   // ===================================================== GraphExecutor
@@ -884,7 +904,7 @@ struct Big {
   __device__ __forceinline__ void client_result(uint32_t c, uint32_t nk) {
     const uint32_t pend = rd(CL(c, 3));
     if (pend < nk) {
-      err = FX_ERR_SIM_LATE;
+      fail_late(__LINE__);
       return;
     }
     put(CL(c, 3), pend - nk);
@@ -913,7 +933,7 @@ struct Big {
     if (rd(RC(v, p, R_WAIT))) unlink(v);
     const uint32_t m = slot_of(missing);
     if (m == NONE) {  // a missing dep is never executed at p, so its slot is live
-      err = FX_ERR_SIM_LATE;
+      fail_late(__LINE__);
       return;
     }
     const uint32_t h = rd(RC(m, p, R_HEAD));
@@ -1178,9 +1198,19 @@ struct Big {
   // an SCC member executes only through the search, which the LDS word
   // records), so a resumed frame needs no reload.  Returns the pending mask;
   // *jm = the first missing dep (the search stops there), 63 if none.
-  __device__ __forceinline__ uint32_t dep_status(uint32_t drow, uint32_t cnd, uint32_t cdot, uint32_t& jm) {
+  // With pf (vmax <= 15), the same round trip prefetches the dep rows of the
+  // frame's first four deps (lanes 16 g + w: value word w of dep g, lane
+  // 16 g + 15 its count word; the words share the cache lines of the tags
+  // read anyway), so descending into one of them needs no row load.
+  __device__ __forceinline__ uint32_t dep_status(uint32_t drow, uint32_t cnd, uint32_t cdot, uint32_t& jm, bool pf,
+                                                 uint32_t& prow) {
     uint32_t tag = 0, ps = 0;
     const bool live = lid < cnd && drow != cdot && src_ok(drow);
+    XPROF_T0();
+    const uint32_t grp = lid >> 4, w = lid & 15u;
+    const uint32_t dg = gather(drow, grp);
+    prow = 0;
+    if (pf && grp < cnd && dg != cdot && src_ok(dg)) prow = S(hslot(dg), w == 15u ? SL_CNT : g.sl_value + w);
     if (live) {
       const uint32_t sl = hslot(drow);
       tag = S(sl, SL_DOT);
@@ -1189,7 +1219,9 @@ struct Big {
     const bool act = live && tag == drow && !(ps & PS_EXEC);
     const uint64_t miss = bal(act && !(ps & PS_INGRAPH));
     jm = miss ? ctz64(miss) : 63u;
-    return (uint32_t)bal(act && (ps & PS_INGRAPH));
+    const uint32_t pmask = (uint32_t)bal(act && (ps & PS_INGRAPH));
+    XPROF_ADD(PF_DEPST);
+    return pmask;
   }
 
   // save_scc for the LX search: the members lstk[base, base + cnt) (their LDS
@@ -1204,10 +1236,11 @@ struct Big {
       return;
     }
     const uint32_t p = xp;
-    XPROF_T0();
     // member slots and dots in lanes (chunks of 64), ranked by dot
-    bool direct = cnt <= 64u;
+    const bool direct = cnt <= 64u;
     uint32_t sorted = 0;
+    {
+    XPROF_T0();
     for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
       const uint32_t i = i0 + lid;
       const uint32_t msl = i < cnt ? (uint32_t)lstk[base + i] : 0u;
@@ -1227,6 +1260,7 @@ struct Big {
       }
     }
     XPROF_ADD(PF_SORT);
+    }
     XPROF_T0();
     for (uint32_t r0 = 0; r0 < cnt && !err; r0 += 64) {
       const uint32_t r = r0 + lid;
@@ -1289,7 +1323,10 @@ struct Big {
     fsp = 1;
     uint32_t cv = rsl, ci = 0, cid = 1, clow = 1, ctp = 0, cdot = 0, cnd = 0, drow = 0, jm = 63u;
     frame_row(rsl, cdot, cnd, drow);
-    uint32_t pm = dep_status(drow, cnd, cdot, jm);
+    const bool pf = A.row_prefetch != 0;
+    bool pv = pf;  // prow holds the current frame's first deps' rows
+    uint32_t prow = 0;
+    uint32_t pm = dep_status(drow, cnd, cdot, jm, pf, prow);
     uint32_t result = FOUND;
     for (uint32_t guard = 0; fsp && !err; ++guard) {
       if (guard > 64u * g.NS + 64u) {
@@ -1331,8 +1368,17 @@ struct Big {
           ci = 0;
           cid = idc;
           clow = idc;
-          frame_row(sl, cdot, cnd, drow);
-          pm = dep_status(drow, cnd, cdot, jm);
+          if (pv && nx < 4u) {  // the row came with the parent's dep states
+            const uint32_t cw = rl(prow, 16u * nx + 15u);
+            const uint32_t rw = gather(prow, (16u * nx + lid) & 63u);
+            cdot = d;
+            cnd = (cw >> 8) & 0xFFu;
+            drow = lid < cnd ? rw : 0u;
+          } else {
+            frame_row(sl, cdot, cnd, drow);
+          }
+          pm = dep_status(drow, cnd, cdot, jm, pf, prow);
+          pv = pf;
         } else if (!(lw & LT_SCC)) {  // on the stack (tarjan.rs:215-225)
           clow = min(clow, id);
         }
@@ -1375,6 +1421,7 @@ struct Big {
         clow = min((tw >> 12) & LT_ID, lowv);
         cid = lt_id(lt_get(cv));
         frame_row(cv, cdot, cnd, drow);
+        pv = false;  // (the resumed frame's deps' rows are loaded when descended into)
       }
     }
     // finalize: a failed search marks the vertices left on the stack visited
@@ -1425,8 +1472,8 @@ struct Big {
   // find_scc call site.
   __device__ __forceinline__ void x_add_(uint32_t p, uint32_t sl) {
     xp = p;
-    xk = rl(pexec, p);
-    xe = rl(pxe, p);
+    xk = rl(pa, A_EXEC + p);
+    xe = rl(pb, B_XE + p);
     nwl = 0;
     // the slot's row and p's record: the copy the committing handler loaded
     // (run_handlers calls x_add right after h_mcommit), else one load
@@ -1561,8 +1608,8 @@ struct Big {
       }
     }
     XPROF_ADD(PF_CHECK);
-    lset(pexec, p, xk);
-    lset(pxe, p, xe);
+    lset(pa, A_EXEC + p, xk);
+    lset(pb, B_XE + p, xe);
   }
 
   // =========================================== send_to_processes_and_executors
@@ -1572,8 +1619,8 @@ struct Big {
       return;
     }
     const uint32_t fi = nfrm++;
-    lset(frw, fi, 0);
-    lset(frb, fi, rtop);
+    lset(pb, B_FRW + fi, 0);
+    lset(pb, B_FRB + fi, rtop);
     xinfo = NONE;
   }
   __device__ __forceinline__ void send_p(uint32_t from, uint32_t to, uint32_t kind, uint32_t dot) {
@@ -1622,15 +1669,15 @@ struct Big {
       }
       if (nfrm == 0) return;
       const uint32_t fi = nfrm - 1;
-      const uint32_t w = rl(frw, fi);
+      const uint32_t w = rl(pb, B_FRW + fi);
       if (w & 3u) {  // ToSend: targets ascending (C4), self recurses in place
-        const uint32_t tgt = (w >> 8) & 0xFFu, k2 = (w >> 2) & 15u, dot = rl(frd, fi);
+        const uint32_t tgt = (w >> 8) & 0xFFu, k2 = (w >> 2) & 15u, dot = rl(pb, B_FRD + fi);
         uint32_t nx = (w >> 16) & 15u;
         while (nx < n) {
           const uint32_t to = nx++;
           if (!((tgt >> to) & 1u)) continue;
           if (to == p) {
-            lset(frw, fi, (w & ~(15u << 16)) | (nx << 16));
+            lset(pb, B_FRW + fi, (w & ~(15u << 16)) | (nx << 16));
             from = p;
             kind = k2;
             w2 = dot;
@@ -1641,10 +1688,11 @@ struct Big {
           if (err) return;
         }
         if (pend) continue;
-        lset(frw, fi, 0);
+        lset(pb, B_FRW + fi, 0);
       }
       // ready results -> schedule_to_client (runner.rs:434-440, 491-504)
-      const uint32_t b = rl(frb, fi);
+      XPROF_T0();
+      const uint32_t b = rl(pb, B_FRB + fi);
       for (uint32_t r = b; r < rtop && !err; ++r) {
         const uint32_t c = rd(W(g.o_rdy, r));
         const uint32_t d = msg_delay(rd(CL(c, 5)));
@@ -1652,6 +1700,7 @@ struct Big {
       }
       rtop = b;
       --nfrm;
+      XPROF_ADD(PF_READY);
     }
   }
 
@@ -1808,7 +1857,7 @@ __global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
     const uint32_t fqm = (uint32_t)bal(s.lid < n && pos < fq);
     const uint32_t wqm = (uint32_t)bal(s.lid < n && pos < wq);
     const uint32_t mqm = (uint32_t)bal(s.lid < n && pos < maj);
-    s.lset(s.pq, p, fqm | (wqm << 8) | (mqm << 16));
+    s.lset(s.pa, s.A_Q + p, fqm | (wqm << 8) | (mqm << 16));
     if (s.lid >= p * 8u && s.lid < p * 8u + n) s.dpq = a.ping[rp * RP + sp.process_regions[s.lid - p * 8u]] / 2u;
   }
   // clients: for region in client_regions, clients_per_region each (runner.rs:143-163)
@@ -1866,7 +1915,7 @@ __global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
     s.prof[PC_EVENTS] += 1;
 #endif
     if (e == NONE) {
-      s.err = FX_ERR_SIM_LATE;  // "there should be a new action"
+      s.fail_late(__LINE__);  // "there should be a new action"
       break;
     }
     const uint32_t t = hi >> 8;
@@ -1887,16 +1936,19 @@ __global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
   }
   // ----------------------------------------------------------- outputs
   __syncthreads();
-  if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = s.pexec;
+  const uint32_t o_exec = gather(s.pa, (s.A_EXEC + s.lid) & 63u), o_fast = gather(s.pa, (s.A_FAST + s.lid) & 63u),
+                 o_slow = gather(s.pa, (s.A_SLOW + s.lid) & 63u), o_stab = gather(s.pa, (s.A_STAB + s.lid) & 63u),
+                 o_fr = gather(s.pa, (s.A_FR + s.lid) & 63u), o_sr = gather(s.pa, (s.A_SR + s.lid) & 63u);
+  if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = o_exec;
   if (a.stats) {
     unsigned long long* st = a.stats + (size_t)inst * FX_SIM_STATS;
     if (s.lid < NMAX) {
       const bool v = s.lid < n;
-      st[FX_SIM_STAT_FAST + s.lid] = v ? s.pfast : 0u;
-      st[FX_SIM_STAT_SLOW + s.lid] = v ? s.pslow : 0u;
-      st[FX_SIM_STAT_STABLE + s.lid] = v ? s.pstab : 0u;
-      st[FX_SIM_STAT_FAST_READS + s.lid] = v ? s.pfr : 0u;
-      st[FX_SIM_STAT_SLOW_READS + s.lid] = v ? s.psr : 0u;
+      st[FX_SIM_STAT_FAST + s.lid] = v ? o_fast : 0u;
+      st[FX_SIM_STAT_SLOW + s.lid] = v ? o_slow : 0u;
+      st[FX_SIM_STAT_STABLE + s.lid] = v ? o_stab : 0u;
+      st[FX_SIM_STAT_FAST_READS + s.lid] = v ? o_fr : 0u;
+      st[FX_SIM_STAT_SLOW_READS + s.lid] = v ? o_sr : 0u;
     }
     if (s.lid == 0) {
       st[FX_SIM_STAT_EVENTS] = s.events;
@@ -2050,6 +2102,11 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
     return !(e && e[0] == '0');
   }();
   const bool lx = lx_env && a.g.NS < 4096u && a.g.vmax <= 32u;
+  static const bool pf_env = [] {
+    const char* e = std::getenv("FX_SIMX_PF");
+    return !(e && e[0] == '0');
+  }();
+  a.row_prefetch = pf_env && a.g.vmax <= 15u ? 1u : 0u;
   const size_t lds = (size_t)(LDS_WORDS + (lx ? a.g.NS : 0u)) * 4u;
   if (lx) {
     if (a.g.R <= 4096) hipLaunchKernelGGL((k_simx<1, true>), grid, block, lds, hs, a);

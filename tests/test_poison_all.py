@@ -70,7 +70,9 @@ _SIM_CASES = {
 def test_poisoned_k_simx(case, fill):
     specs, orc = _oracle_sim(case)
     res = S.run(specs, planet(), large=True, before_launch=poisoner(*fill))
-    assert not [int(e) for e in res.err if e], "instances failed under fill %s" % (fill,)
+    bad = ["instance %d err %d site %d events %d" % (i, int(e), int(res.stats[i, _lib.FX_SIM_STAT_ERR_SITE]),
+                                                    res.events(i)) for i, e in enumerate(res.err) if e]
+    assert not bad, "instances failed under fill %s: %s" % (fill, "; ".join(bad))
     for i, (s, o) in enumerate(zip(specs, orc)):
         assert_instance_parity(res, i, s, o)
     assert np.array_equal(res.chain, sum(o["chain"] for o in orc)[:res.chain.shape[0]])

@@ -21,11 +21,14 @@ sys.path.insert(0, ROOT)
 
 
 def per_dispatch(path, pat):
+    """pat: a substring of the kernel names, optionally followed by
+    !excluded substrings (fx::!k_synth)."""
+    inc, *exc = pat.split("!")
     d = collections.defaultdict(lambda: collections.defaultdict(float))
     names = set()
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if pat not in r["Kernel_Name"]:
+            if inc not in r["Kernel_Name"] or any(x in r["Kernel_Name"] for x in exc):
                 continue
             names.add(r["Kernel_Name"])
             d[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
@@ -40,10 +43,24 @@ def main():
     res = {"mode": mode, "kernel_pattern": pat, "workload_key": args.pmc_key}
     c = {}
     kernels = set()
+    # "sum:PATTERN:STEPS": a multi-kernel step (bench.py --mode huge, the
+    # quiescent-cut driver): the counters of every matching dispatch summed
+    # and divided by the steps the profiled run executed (warmup + timed)
+    summed = pat.startswith("sum:")
+    if summed:
+        _, pat, nsteps = pat.split(":")
+        nsteps = float(nsteps)
+        res["kernel_pattern"] = pat
+        res["per"] = "step (%g steps profiled, every matching dispatch summed)" % nsteps
     for name in ("fetch", "write", "insts", "lds"):
         d, names = per_dispatch(os.path.join(M, name), pat)
         kernels |= names
-        if d:
+        if d and summed:
+            res["dispatches_" + name] = "%d summed" % len(d)
+            for k in d:
+                for ctr, v in d[k].items():
+                    c[ctr] = c.get(ctr, 0.0) + v / nsteps
+        elif d:
             # the main launches only: a tiered driver's rerun dispatches of the
             # same kernel over a few streams are far smaller (kept: dispatches
             # within 2x of the largest in this pass)

@@ -37,6 +37,9 @@ print("events %d, cycles/event %.0f" % (ev, tot / ev))
 for i, nm in enumerate(names):
     print("%-16s %9.0f cycles/event  %5.1f %%" % (nm, st[:, i].sum() / ev, 100 * st[:, i].sum() / tot))
     out[nm] = st[:, i].sum() / ev
+for i, nm in ((12, "ready results"), (13, "handler row load"), (14, "push_event"), (15, "dep states (LX)")):
+    print("%-16s %9.0f cycles/event  %5.1f %%" % (nm, st[:, i].sum() / ev, 100 * st[:, i].sum() / tot))
+    out[nm] = st[:, i].sum() / ev
 for k, nm in counts.items():
     print("%-16s %12.0f per instance  %.3f per event" % (nm, st[:, k].sum() / len(specs), st[:, k].sum() / ev))
     out[nm] = st[:, k].sum() / len(specs)
