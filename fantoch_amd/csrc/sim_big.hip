@@ -427,7 +427,13 @@ struct Big {
     const uint32_t e0 = grp * 64u + lid;
     uint32_t kh = W(g.o_kh, e0), kl = W(g.o_kl, e0);
     const uint32_t vi = W(g.o_inf, e0), va = W(g.o_arg, e0);
-    const uint32_t j = ctz64(bal(kh == th && kl == tl));
+    const uint64_t hit = bal(kh == th && kl == tl);
+    if (!hit) {  // the group's minimum is not among its leaves: a broken event tree
+      fail_late(__LINE__);
+      hi_out = NONE;
+      return NONE;
+    }
+    const uint32_t j = ctz64(hit);
     info_out = rl(vi, j);
     arg_out = rl(va, j);
     if (lid == j) {
@@ -1135,14 +1141,23 @@ struct Big {
       // cv finished
       const uint32_t lowv = clow;
       if (cid == lowv) {  // SCC root: pop the members tstk[ctp, tsp) (tarjan.rs:233-312)
+        bool broken = false;
         for (uint32_t i0 = ctp; i0 < tsp; i0 += 64) {
           const uint32_t i = i0 + lid;
+          uint32_t psx = PS_INGRAPH;
           if (i < tsp) {
             const uint32_t x = W(g.o_tstk, i);
-            const uint32_t mkx = RC(x, p, R_MARK), psx = RC(x, p, R_PST);
+            const uint32_t mkx = RC(x, p, R_MARK);
+            psx = RC(x, p, R_PST);
             RC(x, p, R_MARK) = mkx & ~1u;
             RC(x, p, R_PST) = psx | PS_EXEC;  // executed_clock.add (tarjan.rs:293)
           }
+          // a member in xp's graph and not executed yet (tarjan.rs:245-255 expects)
+          broken = broken || bal((psx & (PS_INGRAPH | PS_EXEC)) != PS_INGRAPH);
+        }
+        if (broken) {
+          fail_late(__LINE__);
+          break;
         }
         save_scc(ctp, tsp - ctp);
         tsp = ctp;
@@ -1254,7 +1269,15 @@ struct Big {
       }
       if (direct) {
         // lane rank <- member i (ds_permute: a forward permutation)
-        sorted = (uint32_t)__builtin_amdgcn_ds_permute((int)((i < cnt ? rank : 63u) << 2), (int)msl);
+        const int addr = (int)((i < cnt ? rank : 63u) << 2);
+        sorted = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)msl);
+        // the permuted dots must ascend over lanes [0, cnt) (every lane written once)
+        const uint32_t sd = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)md);
+        const uint32_t pd = gather(sd, (lid - 1u) & 63u);
+        if (bal(lid < cnt && ((lid > 0 && sd <= pd) || sd == 0u || sd == NONE))) {
+          fail_late(__LINE__);
+          return;
+        }
       } else if (i < cnt) {
         W(g.o_tl, rank) = msl;
       }
@@ -1278,6 +1301,12 @@ struct Big {
       }
       const uint32_t cpr = act ? CL(c, 0) : 0u;
       const uint32_t m = min(64u, cnt - r0);
+      // an SCC member must be in xp's graph and not executed yet (the
+      // reference's expects, tarjan.rs:245-255): anything else is a broken table
+      if (bal(act && ((ps & (PS_INGRAPH | PS_EXEC)) != PS_INGRAPH || d == 0u))) {
+        fail_late(__LINE__);
+        return;
+      }
       if (act) {
         RC(sl, p, R_PST) = ps | PS_EXEC;  // executed_clock.add (tarjan.rs:293)
         if (A.executed && xk + lid < A.exec_cap) A.executed[((size_t)inst * n + p) * A.exec_cap + xk + lid] = d;
@@ -1732,8 +1761,10 @@ struct Big {
         note(4, c + 1, 0, issued);
         const uint32_t lat = now - rd(CL(c, 2));  // latency.as_millis()
         lat_sum += lat;
+#ifndef FX_SIMX_EVLOG
         if (lid == 0 && A.latency_log && issued - 1u < A.lat_cap)
           A.latency_log[((size_t)inst * g.C + c) * A.lat_cap + issued - 1u] = lat;
+#endif
         hist_lat(rd(CL(c, 0)) >> 8, lat);
         if (!client_send(c)) {
           ++clients_done;
@@ -1902,6 +1933,9 @@ __global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
   }
   // ------------------------------------------------------------ loop
   const uint64_t max_events = a.max_events ? a.max_events : 0xFFFFFFFFull;
+#ifdef FX_SIMX_EVLOG
+  uint32_t evn = 0;
+#endif
   while (!s.done && !s.err) {
     uint32_t hi = 0;
 #ifdef FX_SIM_PROFILE
@@ -1915,7 +1949,7 @@ __global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
     s.prof[PC_EVENTS] += 1;
 #endif
     if (e == NONE) {
-      s.fail_late(__LINE__);  // "there should be a new action"
+      if (!s.err) s.fail_late(__LINE__);  // "there should be a new action"
       break;
     }
     const uint32_t t = hi >> 8;
@@ -1928,6 +1962,18 @@ __global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
     const uint32_t gcv = kind == M_GC && s.lid < n ? M[g.o_gp + e * n + s.lid] : 0u;
     s.free_event(e);
     s.run_event(kind, from, to, arg, gcv);
+#ifdef FX_SIMX_EVLOG
+    // debug build (tools/simx_repro.py): every event's key, info, argument and
+    // the trace hash after it, into the instance's latency-log region
+    if (s.lid == 0 && a.latency_log && 4ull * evn + 3ull < (uint64_t)g.C * a.lat_cap) {
+      uint32_t* lg = a.latency_log + (size_t)inst * g.C * a.lat_cap + 4ull * evn;
+      lg[0] = hi;
+      lg[1] = info;
+      lg[2] = arg;
+      lg[3] = (uint32_t)s.trace ^ (uint32_t)(s.trace >> 32);
+    }
+    ++evn;
+#endif
 #ifdef FX_SIM_PROFILE
     s.prof[PF_EVENT] += __builtin_amdgcn_s_memtime() - pt1;
 #endif
@@ -2096,10 +2142,11 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
   a.err = o->err;
   const dim3 grid(b->instances), block(64);
   // the LDS Tarjan state (LX) when its ids fit 12 bits and a frame's deps a
-  // 32-bit mask; FX_SIMX_LX=0 in the environment forces the HBM records (A/B)
+  // 32-bit mask: opt-in (FX_SIMX_LX=1) until an intermittent failure under
+  // register poisoning is explained; the HBM records otherwise
   static const bool lx_env = [] {
     const char* e = std::getenv("FX_SIMX_LX");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   const bool lx = lx_env && a.g.NS < 4096u && a.g.vmax <= 32u;
   static const bool pf_env = [] {

@@ -15,12 +15,14 @@ import test_poison_all as T
 from test_sim_large import assert_instance_parity, planet
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+cases = sys.argv[2].split(",") if len(sys.argv) > 2 else ["config3_atlas", "config3_epaxos", "sim_epaxos_5_2"]
+fills = list(T.FILLS) + [None]  # None: no fill
 fails = 0
 for rep in range(reps):
-    for case in ("config3_atlas", "config3_epaxos", "sim_epaxos_5_2"):
+    for case in cases:
         specs, orc = T._oracle_sim(case)
-        for fill in T.FILLS:
-            res = S.run(specs, planet(), large=True, before_launch=T.poisoner(*fill))
+        for fill in fills:
+            res = S.run(specs, planet(), large=True, before_launch=T.poisoner(*fill) if fill else None)
             for i, e in enumerate(res.err):
                 if e:
                     fails += 1
