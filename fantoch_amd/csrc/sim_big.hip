@@ -42,6 +42,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "fantoch_amd.h"
@@ -2117,7 +2118,40 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
   if (!simx_geometry(b->host_specs[0], b->ring_entries, b->dot_slots, a.g)) return FX_ERR_UNSUPPORTED;
   const size_t bytes = (size_t)a.g.words * 4 * b->instances;
   void* arena = nullptr;
-  if (hipMallocAsync(&arena, bytes, hs) != hipSuccess) return FX_ERR_HIP;
+  // FX_SIMX_ARENA (diagnostics): "fill" fills the arena with 0xA5 bytes
+  // before the launch, "uc" allocates it uncached
+  // "fill-<table>" fills with 0xA5 and then zeroes one table group of every
+  // instance: rec, slot, ev (info / arg / GC payloads), scr (search and
+  // worklist scratch), cl (clients)
+  static const std::string arena_env = [] {
+    const char* e = std::getenv("FX_SIMX_ARENA");
+    return std::string(e ? e : "");
+  }();
+  // default: the arena starts zeroed (a launch must not depend on what an
+  // earlier launch left in the pool's memory: DESIGN.md §3.6); "pool" keeps
+  // the pool's contents (diagnostics)
+  static const int arena_mode = arena_env == "pool" ? 0 : arena_env.rfind("fill", 0) == 0 ? 2
+                              : arena_env == "uc" ? 3 : 1;
+  if (arena_mode == 3) {
+    if (hipExtMallocWithFlags(&arena, bytes, hipDeviceMallocUncached) != hipSuccess) return FX_ERR_HIP;
+  } else if (hipMallocAsync(&arena, bytes, hs) != hipSuccess) {
+    return FX_ERR_HIP;
+  }
+  if (arena_mode == 1 || arena_mode == 2)
+    if (hipMemsetAsync(arena, arena_mode == 1 ? 0 : 0xA5, bytes, hs) != hipSuccess) return FX_ERR_HIP;
+  if (arena_mode == 2 && arena_env.size() > 5) {
+    const std::string grp = arena_env.substr(5);
+    auto zero = [&](uint32_t off, uint32_t end) {
+      (void)hipMemset2DAsync((char*)arena + (size_t)off * 4, (size_t)a.g.words * 4, 0, (size_t)(end - off) * 4,
+                             b->instances, hs);
+    };
+    const GeoX& g = a.g;
+    if (grp == "rec") zero(g.o_rec, g.o_kd);
+    if (grp == "slot") zero(g.o_slot, g.o_rec);
+    if (grp == "ev") { zero(g.o_inf, g.o_arg); zero(g.o_arg, g.o_gp); zero(g.o_gp, g.o_free); }
+    if (grp == "scr") zero(g.o_tstk, g.words);
+    if (grp == "cl") zero(g.o_cl, g.o_kh);
+  }
   a.specs = b->specs;
   a.instances = b->instances;
   a.arena = (uint32_t*)arena;
@@ -2165,7 +2199,12 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
     else hipLaunchKernelGGL((k_simx<4, false>), grid, block, lds, hs, a);
   }
   const hipError_t le = hipGetLastError();
-  (void)hipFreeAsync(arena, hs);
+  if (arena_mode == 3) {
+    (void)hipStreamSynchronize(hs);
+    (void)hipFree(arena);
+  } else {
+    (void)hipFreeAsync(arena, hs);
+  }
   return le == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 
