@@ -37,6 +37,19 @@ struct KArgs {
   uint32_t req_cap;
 };
 
+// One workgroup per stream, streams read from the plane tiles (fx_index: 16
+// bytes per stream and tile row, so 8 consecutive streams share a 128-byte
+// line).  Hardware deals workgroups round-robin to the 8 XCDs, whose L2s are
+// separate: with the identity mapping the 8 streams of a line run on 8 XCDs
+// and each fetches the line.  A launch whose grid is a multiple of 64 maps
+// workgroup 64g + 8i + x (XCD x) to stream slot 64g + 8x + i, so a line's
+// streams share one L2; xcd_grid pads launches of >= 256 slots to that shape
+// (slots >= the lane count exit at once).
+__device__ __forceinline__ uint32_t xcd_slot(uint32_t b) {
+  return (gridDim.x & 63u) ? b : (b & ~63u) | ((b & 7u) << 3) | ((b >> 3) & 7u);
+}
+inline uint32_t xcd_grid(uint32_t lanes) { return lanes >= 256u ? (lanes + 63u) & ~63u : lanes; }
+
 // Lane-per-stream executor tiers (graph_exec.hip) and the 16-lanes-per-stream
 // group tier (graph_group.hip).
 int launch_group(const KArgs& a, hipStream_t stream);

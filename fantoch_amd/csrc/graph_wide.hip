@@ -105,7 +105,7 @@ struct W {
   KArgs a;
   Lay L;
   uint32_t* m;  // table memory (LDS or this stream's HBM block)
-  uint32_t lid, s;
+  uint32_t lid, s, slot = 0;  // slot: the launch's lane index (partial: this lane's request ring)
   uint32_t err = 0;
   uint32_t nfree = 0, tsp = 0, fsp = 0, nwl = 0, idc = 0, epoch = 1, nexec = 0, step = 0;
   uint32_t t_now = 0;
@@ -536,7 +536,7 @@ struct W {
       seen = __ballot(hit) != 0;
     }
     if (!seen) {
-      uint32_t* ring = a.req + (size_t)blockIdx.x * (1 + 2 * (size_t)a.req_cap);
+      uint32_t* ring = a.req + (size_t)slot * (1 + 2 * (size_t)a.req_cap);
       const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)ring[0]);
       if (k >= a.req_cap) { err = FX_ERR_CAPACITY; return; }
       if (lid == 0) {
@@ -741,7 +741,7 @@ struct W {
 template <bool HBM, uint32_t FN = 0, uint32_t FD = 0>
 __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay Lrt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t lane_idx = blockIdx.x;
+  const uint32_t lane_idx = xcd_slot(blockIdx.x);
   if (lane_idx >= a.num_lanes) return;
   Lay L = Lrt;
   if constexpr (FN != 0) L.make(512, 256, 32, FN, FD, false, true);
@@ -749,6 +749,7 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay Lrt) {
   w.a = a;
   w.L = L;
   w.lid = threadIdx.x;
+  w.slot = lane_idx;
   w.s = a.stream_map ? a.stream_map[lane_idx] : lane_idx;
   w.partial = HBM && (a.flags & FX_FLAG_PARTIAL);
   w.m = HBM ? a.state + (size_t)lane_idx * L.words : smem;
@@ -762,7 +763,7 @@ __global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay Lrt) {
     if (a.init_frontier && w.lid < L.n) w.m[L.front + w.lid] = a.init_frontier[(size_t)w.s * 8 + w.lid];
     __syncthreads();
     w.nfree = L.P;
-    if (w.partial && w.lid == 0) a.req[(size_t)blockIdx.x * (1 + 2 * (size_t)a.req_cap)] = 0;
+    if (w.partial && w.lid == 0) a.req[(size_t)lane_idx * (1 + 2 * (size_t)a.req_cap)] = 0;
   } else {  // resume (HBM tables only): the tables are in place, the scalars saved
     w.nfree = w.rd(L.sc, 0);
     w.nexec = w.rd(L.sc, 1);
@@ -855,9 +856,10 @@ int launch_wide(const KArgs& a, bool hbm, hipStream_t hs) {
   if (partial && (!hbm || !a.req || a.stream_map)) return FX_ERR_INVALID_ARG;
   const wide::Lay L = wide_layout(hbm, a.n, a.dmax, partial);
   if (!hbm && (size_t)L.words * 4 > 160 * 1024) return FX_ERR_UNSUPPORTED;
+  const uint32_t grid = xcd_grid(a.num_lanes);
   if (hbm) {
     if (!a.state) return FX_ERR_INVALID_ARG;
-    hipLaunchKernelGGL(wide::k_graph_wide<true>, dim3(a.num_lanes), dim3(64), 0, hs, a, L);
+    hipLaunchKernelGGL(wide::k_graph_wide<true>, dim3(grid), dim3(64), 0, hs, a, L);
   } else {
     static bool configured = false;
     if (!configured) {
@@ -868,9 +870,9 @@ int launch_wide(const KArgs& a, bool hbm, hipStream_t hs) {
       configured = true;
     }
     if (a.n == 5 && std::max(a.dmax, 1u) == 5)
-      hipLaunchKernelGGL((wide::k_graph_wide<false, 5, 5>), dim3(a.num_lanes), dim3(64), (size_t)L.words * 4, hs, a, L);
+      hipLaunchKernelGGL((wide::k_graph_wide<false, 5, 5>), dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
     else
-      hipLaunchKernelGGL(wide::k_graph_wide<false>, dim3(a.num_lanes), dim3(64), (size_t)L.words * 4, hs, a, L);
+      hipLaunchKernelGGL(wide::k_graph_wide<false>, dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
   }
   return hipGetLastError() == hipSuccess ? FX_OK : FX_ERR_HIP;
 }

@@ -291,10 +291,30 @@ struct Pr {
     }
   }
 
-  // add (mod.rs:104-152)
-  __device__ void add(uint32_t r) {
+  // the inputs of the 4-step tile row holding step r0 (fx_index: 16 bytes per
+  // plane): lane 4q + k holds step r0 + k of plane q -- 0 dot, 1 ndeps (or
+  // hdr), 2 clock lo, 3 clock hi, 4 + j dep j (j < 12) -- so a row is one
+  // load, issued one row ahead of its use.  r0 + 3 stays inside the padded
+  // plane (steps rounded up to 4).
+  __device__ __forceinline__ uint32_t row_load(uint32_t r0) const {
+    const uint32_t q = lid >> 2, r = r0 + (lid & 3u);
+    const size_t at = fx_index(r, s, a.k.steps);
+    if (q == 0) return a.k.dot[at];
+    if (q == 1) return a.ndeps ? a.ndeps[at] : a.k.hdr[at];
+    if (q == 2) return a.clo[at];
+    if (q == 3) return a.chi[at];
+    const uint32_t j = q - 4;
+    return j < a.k.dmax ? a.k.deps[(size_t)j * a.k.plane + at] : 0u;
+  }
+  __device__ __forceinline__ uint32_t row_at(uint32_t row, uint32_t q, uint32_t k) const {
+    return (uint32_t)__builtin_amdgcn_readlane((int)row, (int)(4u * q + k));
+  }
+
+  // add (mod.rs:104-152); `row` = row_load(r & ~3)
+  __device__ void add(uint32_t r, uint32_t row) {
     const size_t at = ix(r);
-    const uint32_t d = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.k.dot[at]);
+    const uint32_t k = r & 3u;
+    const uint32_t d = row_at(row, 0, k);
     const uint32_t src = FX_DOT_SRC(d);
     if (src < 1 || src > L.n || FX_DOT_SEQ(d) == 0) { err = FX_ERR_DOT_RANGE; return; }
     // assert!(self.committed_clock.add(..)) (mod.rs:123): a dot commits once,
@@ -312,15 +332,21 @@ struct Pr {
     }
     if (!nfree) { err = FX_ERR_CAPACITY; return; }
     const uint32_t v = rd(L.vfree, --nfree);
-    const uint32_t nd = min(a.ndeps ? a.ndeps[at] : FX_HDR_ND(a.k.hdr[at]), a.k.dmax);
+    const uint32_t ndw = row_at(row, 1, k);
+    const uint32_t nd = min(a.ndeps ? ndw : FX_HDR_ND(ndw), a.k.dmax);
     put(L.vdot, v, d);
     put(L.vrec, v, r);
-    put(L.vclo, v, a.clo[at]);
-    put(L.vchi, v, a.chi[at]);
+    put(L.vclo, v, row_at(row, 2, k));
+    put(L.vchi, v, row_at(row, 3, k));
     put(L.vmiss, v, 0);
     put(L.vnd, v, nd);
     reg_clear(v);
-    for (uint32_t j = lid; j < nd; j += 64) m[L.vdeps + v * L.D + j] = a.k.deps[(size_t)j * a.k.plane + at];
+    {  // deps 0..11 from the row (every lane takes part in the permute), the rest from HBM
+      const uint32_t src = 16u + 4u * min(lid, 11u) + k;
+      const uint32_t dj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)row);
+      if (lid < nd) m[L.vdeps + v * L.D + lid] = lid < 12u ? dj : a.k.deps[(size_t)lid * a.k.plane + at];
+      for (uint32_t j = lid + 64; j < nd; j += 64) m[L.vdeps + v * L.D + j] = a.k.deps[(size_t)j * a.k.plane + at];
+    }
     put(L.hidx, h, v + 1);
     __syncthreads();
     push_removed(0, d);  // try_phase_one_pending(dot)
@@ -334,7 +360,7 @@ struct Pr {
 template <bool HBM>
 __global__ __launch_bounds__(64) void k_pred(PArgs a, Lay L) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t li = blockIdx.x;
+  const uint32_t li = xcd_slot(blockIdx.x);
   if (li >= a.k.num_lanes) return;
   Pr w;
   w.a = a;
@@ -348,9 +374,14 @@ __global__ __launch_bounds__(64) void k_pred(PArgs a, Lay L) {
   __syncthreads();
   w.nfree = L.P;
   const uint32_t len = a.k.lengths ? min(a.k.lengths[w.s], a.k.steps) : a.k.steps;
+  uint32_t row = len ? w.row_load(0) : 0u, next = len > 4 ? w.row_load(4) : 0u;
   for (uint32_t r = 0; r < len && !w.err; ++r) {
+    if (r && !(r & 3u)) {
+      row = next;
+      if (r + 4 < len) next = w.row_load(r + 4);
+    }
     w.step = r;
-    w.add(r);
+    w.add(r, row);
   }
   if (w.lid == 0) {
     a.k.nexec[w.s] = w.nexec;
@@ -431,9 +462,10 @@ extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* ou
   const pred::Lay L = pred_layout(tier, in->base.n, in->base.dmax);
   hipStream_t hs = (hipStream_t)hip_stream;
   if (!hbm && L.words == 0) return FX_ERR_UNSUPPORTED;
+  const uint32_t grid = xcd_grid(num_lanes);
   fx::profile_slot_record(FX_PROFILE_SLOT_PRED + tier, false, hs);
   if (hbm) {
-    hipLaunchKernelGGL(pred::k_pred<true>, dim3(num_lanes), dim3(64), 0, hs, a, L);
+    hipLaunchKernelGGL(pred::k_pred<true>, dim3(grid), dim3(64), 0, hs, a, L);
   } else {
     static bool configured = false;
     if (!configured) {
@@ -441,7 +473,7 @@ extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* ou
                                 160 * 1024);
       configured = true;
     }
-    hipLaunchKernelGGL(pred::k_pred<false>, dim3(num_lanes), dim3(64), (size_t)L.words * 4, hs, a, L);
+    hipLaunchKernelGGL(pred::k_pred<false>, dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
   }
   if (hipGetLastError() != hipSuccess) return FX_ERR_HIP;
   fx::profile_slot_record(FX_PROFILE_SLOT_PRED + tier, true, hs);

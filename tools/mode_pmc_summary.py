@@ -48,7 +48,7 @@ def main():
     # and divided by the steps the profiled run executed (warmup + timed)
     summed = pat.startswith("sum:")
     if summed:
-        _, pat, nsteps = pat.split(":")
+        pat, nsteps = pat.split(":", 1)[1].rsplit(":", 1)
         nsteps = float(nsteps)
         res["kernel_pattern"] = pat
         res["per"] = "step (%g steps profiled, every matching dispatch summed)" % nsteps
