@@ -284,14 +284,6 @@ def main_dense(args):
     if roof.get("issue"):
         roof["note"] = ("one wavefront per stream walking the pending graph: latency-bound "
                         "(issue.wait_any_frac_of_wave_cycles, issue.mean_waves_per_cu)")
-    huge_roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                 "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": None,
-                 "kernel": "fx_batch_run_cut (cut analysis + segment executor + scatter)",
-                 "alg_bytes_per_launch": int(alg_bytes), "alg_bytes_per_cmd": round(alg_bytes / n_adds, 3)}
-    # HBM traffic of the whole step (every kernel of the cut driver summed):
-    # tools/mode_pmc.sh huge -> profiles/pmc_huge.json, when it was measured on this workload
-    import bench_pmc
-    bench_pmc.attach(huge_roof, bench_pmc.load("huge", args), alg_bytes)
     line = {
         "metric": "executed cmds/sec (node) for batched Atlas/EPaxos sims; % of HBM roofline",
         "value": round(executed * world * args.steps / elapsed, 1), "unit": "cmds/s", "n_gpus": world,
