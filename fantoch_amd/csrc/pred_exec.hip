@@ -95,13 +95,6 @@ struct Pr {
   __device__ __forceinline__ uint32_t rw(uint32_t ph, uint32_t v, uint32_t j) const {
     return L.vreg + (ph * L.P + v) * L.DW + (j >> 5);
   }
-  // registers dep slot j of vertex v in phase ph's PendingIndex
-  __device__ __forceinline__ void reg_set(uint32_t ph, uint32_t v, uint32_t j) {
-    const uint32_t w = rw(ph, v, j);
-    put(w, 0, rd(w, 0) | (1u << (j & 31u)));
-    if (ph) ++nreg1;
-    else ++nreg0;
-  }
   __device__ __forceinline__ void reg_clear(uint32_t v) {
     for (uint32_t i = lid; i < 2 * L.DW; i += 64) m[L.vreg + ((i / L.DW) * L.P + v) * L.DW + i % L.DW] = 0;
     __syncthreads();
@@ -230,38 +223,72 @@ struct Pr {
     push_removed(1, d);
   }
 
-  // move_to_phase_two (mod.rs:208-275)
+  // per-lane forms of contains / find (each lane asks about its own dot)
+  __device__ __forceinline__ bool contains_v(uint32_t front, uint32_t bits, uint32_t d) const {
+    const uint32_t src = FX_DOT_SRC(d), sq = FX_DOT_SEQ(d);
+    if (src < 1 || src > L.n) return false;
+    const uint32_t f = m[front + src - 1];
+    if (sq <= f) return true;
+    if (sq - f - 1 >= L.WB * 32u) return false;
+    const uint32_t b = sq & (L.WB * 32u - 1u);
+    return (m[bits + (src - 1) * L.WB + (b >> 5)] >> (b & 31u)) & 1u;
+  }
+  __device__ __forceinline__ uint32_t find_v(uint32_t d) const {
+    const uint32_t src = FX_DOT_SRC(d);
+    if (src < 1 || src > L.n) return NONE;
+    const uint32_t v = m[L.hidx + hslot(d)];
+    return (v != 0 && m[L.vdot + v - 1] == d) ? v - 1 : NONE;
+  }
+  // a phase's PendingIndex::index(dot, dep) for the deps j0 .. j0 + 63 of v
+  // whose lanes are set in b: the phase's words of v are still zero (cleared
+  // at commit, each phase registers once), so the ballot is the word pair
+  __device__ __forceinline__ void reg_mask(uint32_t ph, uint32_t v, uint32_t j0, uint64_t b) {
+    if (lid < 2 && j0 / 32 + lid < L.DW) m[rw(ph, v, j0 + 32 * lid)] = (uint32_t)(b >> (32 * lid));
+  }
+
+  // move_to_phase_two (mod.rs:208-275): the deps are checked lane-parallel
+  // (nothing they read changes while they are checked)
   __device__ void phase_two(uint32_t d) {
     const uint32_t v = find(d);
     if (v == NONE) { err = FX_ERR_CAPACITY; return; }
     const uint64_t cv = clock_of(v);
     const uint32_t nd = rd(L.vnd, v);
     uint32_t miss = 0;
-    for (uint32_t j = 0; j < nd; ++j) {
-      const uint32_t dep = rd(L.vdeps, v * L.D + j);
-      if (contains(L.efront, L.ebits, dep)) continue;
-      const uint32_t w = find(dep);
-      if (w == NONE) { err = FX_ERR_CAPACITY; return; }  // "non-executed dependency must exist"
-      if (clock_of(w) < cv) {
-        ++miss;
-        reg_set(1, v, j);  // phase_two_pending_index.index(dot, dep)
+    for (uint32_t j0 = 0; j0 < nd; j0 += 64) {
+      const uint32_t j = j0 + lid;
+      bool lower = false, gone = false;
+      if (j < nd) {
+        const uint32_t dep = m[L.vdeps + v * L.D + j];
+        if (!contains_v(L.efront, L.ebits, dep)) {
+          const uint32_t w = find_v(dep);
+          if (w == NONE) gone = true;
+          else lower = ((((uint64_t)m[L.vchi + w]) << 32) | m[L.vclo + w]) < cv;
+        }
       }
+      if (__ballot(gone)) { err = FX_ERR_CAPACITY; return; }  // "non-executed dependency must exist"
+      const uint64_t b = __ballot(lower);
+      reg_mask(1, v, j0, b);  // phase_two_pending_index.index(dot, dep)
+      miss += (uint32_t)__builtin_popcountll(b);
     }
+    nreg1 += miss;
     if (miss) put(L.vmiss, v, miss);
     else save(d);
   }
 
-  // move_to_phase_one (mod.rs:154-206)
+  // move_to_phase_one (mod.rs:154-206), lane-parallel over the deps
   __device__ void phase_one(uint32_t d) {
     const uint32_t v = find(d);
     if (v == NONE) { err = FX_ERR_CAPACITY; return; }
     const uint32_t nd = rd(L.vnd, v);
     uint32_t miss = 0;
-    for (uint32_t j = 0; j < nd; ++j)
-      if (!contains(L.cfront, L.cbits, rd(L.vdeps, v * L.D + j))) {
-        ++miss;
-        reg_set(0, v, j);
-      }
+    for (uint32_t j0 = 0; j0 < nd; j0 += 64) {
+      const uint32_t j = j0 + lid;
+      const uint64_t b =
+          __ballot(j < nd && !contains_v(L.cfront, L.cbits, m[L.vdeps + v * L.D + min(j, nd - 1)]));
+      reg_mask(0, v, j0, b);  // phase_one_pending_index.index(dot, dep)
+      miss += (uint32_t)__builtin_popcountll(b);
+    }
+    nreg0 += miss;
     if (miss) put(L.vmiss, v, miss);
     else phase_two(d);
   }
