@@ -384,11 +384,21 @@ struct Pr {
   }
 };
 
-template <bool HBM>
-__global__ __launch_bounds__(64) void k_pred(PArgs a, Lay L) {
+// FN / FD != 0: the SMALL tier's layout for n = FN sources and FD dep planes
+// compiled in (the configs[1] shape, n = 5): table offsets become immediates,
+// which frees the scalar registers the layout's fields held (the generic
+// build spills about 50 SGPRs to VGPR lanes)
+template <bool HBM, uint32_t FN = 0, uint32_t FD = 0>
+__global__ __launch_bounds__(64) void k_pred(PArgs a, Lay Lrt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t li = xcd_slot(blockIdx.x);
   if (li >= a.k.num_lanes) return;
+  Lay L = Lrt;
+  if constexpr (FN != 0) {
+    L.make(64, 128, 32, FN, FD, 4 * 64);
+    a.k.n = FN;
+    a.k.dmax = FD;
+  }
   Pr w;
   w.a = a;
   w.L = L;
@@ -498,9 +508,14 @@ extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* ou
     if (!configured) {
       (void)hipFuncSetAttribute((const void*)pred::k_pred<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)pred::k_pred<false, 5, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
       configured = true;
     }
-    hipLaunchKernelGGL(pred::k_pred<false>, dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
+    if (tier == FX_PRED_TIER_SMALL && in->base.n == 5 && std::max(in->base.dmax, 1u) == 5)
+      hipLaunchKernelGGL((pred::k_pred<false, 5, 5>), dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
+    else
+      hipLaunchKernelGGL(pred::k_pred<false>, dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
   }
   if (hipGetLastError() != hipSuccess) return FX_ERR_HIP;
   fx::profile_slot_record(FX_PROFILE_SLOT_PRED + tier, true, hs);

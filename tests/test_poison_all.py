@@ -136,6 +136,20 @@ def test_poisoned_pred(tier, fill):
 
 
 @pytest.mark.parametrize("fill", FILLS, ids=FILL_IDS)
+def test_poisoned_pred_compiled_layout(fill):
+    """The bench's shape (n = 5, dmax = 5): the SMALL tier's compiled-in layout."""
+    from test_pred_gpu import synth_pred_case
+    planes, clo, chi = synth_pred_case(seed=6)
+    res = fd.run_pred(planes, clo, chi, tier=_lib.FX_PRED_TIER_SMALL, before_launch=poisoner(*fill))
+    o_order, o_rel, o_nexec, o_err = O.pred_batch_execute(planes, clo, chi, threads=8)
+    ok = res.err == 0
+    assert np.all(ok | (res.err == _lib.FX_ERR_CAPACITY)) and ok.sum() > planes.S // 2
+    for s in np.flatnonzero(ok):
+        rows = _lib.index(np.arange(int(o_nexec[s])), s, planes.steps)
+        assert res.nexec[s] == o_nexec[s] and np.array_equal(res.order[rows], o_order[rows])
+
+
+@pytest.mark.parametrize("fill", FILLS, ids=FILL_IDS)
 def test_poisoned_persistent_handle_first_launch(fill):
     """The register file is poisoned on the null stream right before the
     handle's first pull; the handle's stream is a blocking one, so its

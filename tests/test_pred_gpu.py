@@ -84,3 +84,35 @@ def test_very_wide_deps():
     streams = P.random_streams(3, 8, 2, 110, keys=3, reverse_pct=80)
     planes, res = check(streams, 2)
     assert planes.dmax > 200 and res.reruns >= 8 and np.all(res.nexec == planes.lengths)
+
+
+def synth_pred_case(seed=5, instances=40, cmds=100):
+    """The pred bench's workload at a small size: configs[1]-shaped synthetic
+    streams (n = 5, so dmax = 5), Caesar clock (seq, process id) of each dot."""
+    from fantoch_amd import streams as fs
+    p = fs.synth_params(seed=seed, instances=instances, n=5, cmds=cmds, window=8, cycle_pct=30,
+                        conflicts=(0, 2, 10, 50, 100), conflict_block=instances // 5)
+    planes = fs.synth_host(p)
+    dot = planes.dot.astype(np.uint32)
+    clo = ((dot & np.uint32(0xFFFFFF)) << np.uint32(8)) | ((dot >> np.uint32(24)) & np.uint32(0xFF))
+    return planes, clo, np.zeros_like(clo)
+
+
+@pytest.mark.parametrize("tier", [None, _lib.FX_PRED_TIER_SMALL])
+def test_synth_streams_bench_shape(tier):
+    """n = 5 and dmax = 5 select the SMALL tier's compiled-in layout
+    (k_pred<false, 5, 5>); bit-exact with the oracle where the tier finished."""
+    planes, clo, chi = synth_pred_case()
+    assert planes.n == 5 and planes.dmax == 5
+    res = fd.run_pred(planes, clo, chi, tier=tier)
+    o_order, o_rel, o_nexec, o_err = O.pred_batch_execute(planes, clo, chi, threads=8)
+    ok = res.err == 0
+    assert np.all(ok | (res.err == _lib.FX_ERR_CAPACITY)) and ok.sum() > planes.S // 2
+    if tier is None:
+        assert np.array_equal(res.err, o_err)
+    for s in np.flatnonzero(ok):
+        assert res.nexec[s] == o_nexec[s]
+        rows = _lib.index(np.arange(int(o_nexec[s])), s, planes.steps)
+        assert np.array_equal(res.order[rows], o_order[rows]), "order differs on stream %d" % s
+        rr = _lib.index(np.arange(planes.steps), s, planes.steps)
+        assert np.array_equal(res.release[rr], o_rel[rr]), "release differs on stream %d" % s
