@@ -130,7 +130,7 @@ def main_pred(args):
         "executed_per_step": executed, "reruns": int(reruns.value),
         "roofline": bench_pmc.attach(
             {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-             "frac": round(achieved / HBM_PEAK_GBPS, 6), "kernel": "k_pred<false> (SMALL tier, every stream)",
+             "frac": round(achieved / HBM_PEAK_GBPS, 6), "kernel": "k_pred<false, 5, 5> (SMALL tier, layout compiled in for n = 5; every stream)",
              "kernel_ms_avg": round(k_main, 3) if k_main else None,
              "rerun_ms_avg": {"lds": round(kms[_lib.FX_PRED_TIER_LDS], 3) if kms[_lib.FX_PRED_TIER_LDS] else None,
                               "hbm": round(kms[_lib.FX_PRED_TIER_HBM], 3) if kms[_lib.FX_PRED_TIER_HBM] else None},

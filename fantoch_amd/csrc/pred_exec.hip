@@ -209,10 +209,8 @@ struct Pr {
   }
 
   // save_to_execute (mod.rs:341-367): remove, execute, then (depth first)
-  // try_phase_two_pending
-  __device__ void save(uint32_t d) {
-    const uint32_t v = find(d);
-    if (v == NONE) { err = FX_ERR_CAPACITY; return; }
+  // try_phase_two_pending.  v = find(d): every caller has just found it
+  __device__ void save(uint32_t d, uint32_t v) {
     const uint32_t rec = rd(L.vrec, v);
     put(L.hidx, hslot(d), 0);
     put(L.vdot, v, 0);
@@ -247,10 +245,8 @@ struct Pr {
   }
 
   // move_to_phase_two (mod.rs:208-275): the deps are checked lane-parallel
-  // (nothing they read changes while they are checked)
-  __device__ void phase_two(uint32_t d) {
-    const uint32_t v = find(d);
-    if (v == NONE) { err = FX_ERR_CAPACITY; return; }
+  // (nothing they read changes while they are checked); v = find(d)
+  __device__ void phase_two(uint32_t d, uint32_t v) {
     const uint64_t cv = clock_of(v);
     const uint32_t nd = rd(L.vnd, v);
     uint32_t miss = 0;
@@ -272,14 +268,12 @@ struct Pr {
     }
     nreg1 += miss;
     if (miss) put(L.vmiss, v, miss);
-    else save(d);
+    else save(d, v);
   }
 
-  // move_to_phase_one (mod.rs:154-206), lane-parallel over the deps
-  __device__ void phase_one(uint32_t d) {
-    const uint32_t v = find(d);
-    if (v == NONE) { err = FX_ERR_CAPACITY; return; }
-    const uint32_t nd = rd(L.vnd, v);
+  // move_to_phase_one (mod.rs:154-206), lane-parallel over the deps; v =
+  // find(d), nd its dep count
+  __device__ void phase_one(uint32_t d, uint32_t v, uint32_t nd) {
     uint32_t miss = 0;
     for (uint32_t j0 = 0; j0 < nd; j0 += 64) {
       const uint32_t j = j0 + lid;
@@ -290,7 +284,7 @@ struct Pr {
     }
     nreg0 += miss;
     if (miss) put(L.vmiss, v, miss);
-    else phase_two(d);
+    else phase_two(d, v);
   }
 
   // the frames: try_phase_one_pending / try_phase_two_pending (mod.rs:295-339)
@@ -312,8 +306,8 @@ struct Pr {
       if (mc == 0) { err = FX_ERR_CAPACITY; return; }
       put(L.vmiss, v, mc - 1);
       if (mc == 1) {
-        if (ph == 0) phase_two(p);
-        else save(p);
+        if (ph == 0) phase_two(p, v);
+        else save(p, v);
       }
     }
   }
@@ -379,7 +373,9 @@ struct Pr {
     push_removed(0, d);  // try_phase_one_pending(dot)
     run();
     if (err) return;
-    phase_one(d);  // move_to_phase_one(dot)
+    // move_to_phase_one(dot): v is still d's vertex (it holds no registration
+    // yet, so nothing run() does can execute and free it)
+    phase_one(d, v, nd);
     run();
   }
 };

@@ -19,7 +19,7 @@ for mode in $MODES; do
     executor) pat="k_graph_lane" ;;
     huge) pat="sum:fx::!k_synth:2" ;;
     dense) pat="k_graph_wide<false" ;;
-    pred) pat="k_pred<false>" ;;
+    pred) pat="k_pred<false" ;;
     placements) pat="k_sim<"; extra="--cmds 100" ;;
     *) echo "unknown mode $mode"; exit 1 ;;
   esac
