@@ -42,6 +42,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -100,6 +101,78 @@ struct GeoX {  // launch-uniform geometry (words)
       o_tmp, o_tl, o_tw, o_rdy;
   uint32_t words;  // per instance
 };
+
+// the geometry of n processes, C clients, K keys per command, a key pool of
+// `pool`, `ring` events in flight and `dots` live dots (0: the defaults); a
+// constant expression, so a kernel can compile one in (GS below)
+__host__ __device__ constexpr bool geo_build(uint32_t n, uint32_t C, uint32_t K, uint32_t pool, uint32_t ring,
+                                             uint32_t dots, GeoX& g) {
+  if (n < 2 || n > NMAX || C < 1 || C > 65535u || K < 1 || K > KMAX) return false;
+  g.n = n;
+  g.C = C;
+  g.K = K;
+  const uint32_t cpr = (C + n - 1) / n;
+  const uint32_t want = dots ? (dots + n - 1) / n : (8u * cpr > 32u ? 8u * cpr : 32u);
+  uint32_t Q = 16, qlog = 4;
+  while (Q < want && Q < (1u << 16)) {
+    Q <<= 1;
+    ++qlog;
+  }
+  if (Q < want) return false;
+  g.Q = Q;
+  g.qlog = qlog;
+  g.NS = n * Q;
+  const uint32_t rdef = 16u * C + 8u * n * n + 256u;
+  uint32_t R = ring ? ring : (rdef < 16384u ? rdef : 16384u);
+  R = (R + 63u) & ~63u;
+  if (R > 16384u) return false;
+  g.R = R;
+  g.ncli_keys = pool + C + 1;
+  // an MCollectAck carries the coordinator's deps (<= 2K: a write and a read
+  // per key) plus the replica's own (<= 2K); a committed value is their union
+  // over the quorum (<= 2K (n + 1))
+  g.amax = 4 * K;
+  g.vmax = 2 * K * (n + 1);
+  if (n * g.amax > 64 || g.vmax > 64) return false;
+  g.sl_value = SL_COLLECT + 2 * K;
+  g.sl_ack = g.sl_value + g.vmax;
+  g.SW = g.sl_ack + n * g.amax;
+  uint64_t o = 0;
+  auto take = [&o](uint32_t& off, uint64_t words) {
+    off = (uint32_t)o;
+    o += (words + 15u) & ~15ull;  // 64-byte aligned tables
+  };
+  take(g.o_slot, (uint64_t)g.NS * g.SW);
+  take(g.o_rec, (uint64_t)g.NS * n * RW);
+  take(g.o_kd, (uint64_t)n * g.ncli_keys * 2u);
+  take(g.o_cl, (uint64_t)C * 8u);
+  take(g.o_kh, R);
+  take(g.o_kl, R);
+  take(g.o_inf, R);
+  take(g.o_arg, R);
+  take(g.o_gp, (uint64_t)R * n);
+  take(g.o_free, R);
+  take(g.o_gco, (uint64_t)n * n * n);
+  take(g.o_tstk, g.NS);
+  take(g.o_fv, g.NS);
+  take(g.o_fi, g.NS);
+  take(g.o_fp, g.NS);
+  take(g.o_wl, 2ull * g.NS);
+  take(g.o_tmp, g.NS);
+  take(g.o_tl, g.NS);
+  take(g.o_tw, g.NS);
+  take(g.o_rdy, C + 64u);
+  if (o > 0x7FFFFFFFull) return false;
+  g.words = (uint32_t)o;
+  return true;
+}
+// GS = 1: BASELINE configs[3] (n = 5, 64 clients per region in the 5 process
+// regions, one key per command, a one-key pool, default ring and dots)
+__host__ __device__ constexpr GeoX geo_compiled(uint32_t gs) {
+  GeoX g{};
+  if (gs == 1) geo_build(5, 320, 1, 1, 0, 0, g);
+  return g;
+}
 
 struct ArgsX {
   const fx_sim_spec* specs;
@@ -1808,29 +1881,38 @@ struct Big {
 #ifndef FX_SIMX_WAVES
 #define FX_SIMX_WAVES 3
 #endif
-template <uint32_t NG, bool LX>
+// GS != 0: the geometry geo_compiled(GS) compiled in (the host launches it
+// when the batch's geometry equals it word for word): its offsets become
+// immediates instead of scalar registers, of which the kernel is short
+template <uint32_t NG, bool LX, uint32_t GS = 0>
 __global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
   // LDS_WORDS of histogram caches, then (LX) the Tarjan words and stack: u16[NS] each
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   const uint32_t inst = blockIdx.x;
   if (inst >= a.instances) return;
   Big<NG, LX> s;
+  if constexpr (GS != 0) {
+    constexpr GeoX gc = geo_compiled(GS);
+    static_assert(gc.words != 0, "compiled geometry");
+    s.g = gc;
+  } else {
+    s.g = a.g;
+  }
   s.ltl = reinterpret_cast<uint16_t*>(smem + LDS_WORDS);
-  s.lstk = s.ltl + a.g.NS;
+  s.lstk = s.ltl + s.g.NS;
   s.lid = threadIdx.x;
   s.A = a;
-  s.g = a.g;
-  s.M = a.arena + (size_t)inst * a.g.words;
+  s.M = a.arena + (size_t)inst * s.g.words;
   s.lds = smem;
   s.inst = inst;
   const fx_sim_spec& sp = a.specs[inst];
   s.seed = sp.seed;
   s.rng_inst = sp.instance;
   s.protocol = sp.protocol;
-  s.n = a.g.n;
+  s.n = s.g.n;
   s.f = sp.f;
-  s.C = a.g.C;
-  s.K = a.g.K;
+  s.C = s.g.C;
+  s.K = s.g.K;
   s.gc_ms = sp.gc_interval_ms;
   s.en_ms = sp.executed_notification_ms;
   s.cmds = sp.commands_per_client;
@@ -2034,68 +2116,9 @@ __global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
 // (per source: the next power of two of dots / n).  Defaults: 16 events per
 // client (plus the GC traffic) and 8 live dots per client per process region.
 bool simx_geometry(const fx_sim_spec& sp, uint32_t ring, uint32_t dots, simx::GeoX& g) {
-  using namespace simx;
-  const uint32_t n = sp.n;
-  if (n < 2 || n > NMAX) return false;
-  const uint32_t C = sp.clients_per_region * sp.num_client_regions;
-  if (C < 1 || C > 65535u) return false;
-  g.n = n;
-  g.C = C;
-  g.K = sp.keys_per_command;
-  if (g.K < 1 || g.K > KMAX) return false;
-  const uint32_t cpr = (C + n - 1) / n;
-  uint32_t want = dots ? (dots + n - 1) / n : std::max<uint32_t>(32u, 8u * cpr);
-  uint32_t Q = 16, qlog = 4;
-  while (Q < want && Q < (1u << 16)) {
-    Q <<= 1;
-    ++qlog;
-  }
-  if (Q < want) return false;
-  g.Q = Q;
-  g.qlog = qlog;
-  g.NS = n * Q;
-  uint32_t R = ring ? ring : std::min<uint32_t>(16384u, 16u * C + 8u * n * n + 256u);
-  R = (R + 63u) & ~63u;
-  if (R > 16384u) return false;
-  g.R = R;
-  g.ncli_keys = sp.pool_size + C + 1;
-  // an MCollectAck carries the coordinator's deps (<= 2K: a write and a read
-  // per key) plus the replica's own (<= 2K); a committed value is their union
-  // over the quorum (<= 2K (n + 1))
-  g.amax = 4 * g.K;
-  g.vmax = 2 * g.K * (n + 1);
-  if (n * g.amax > 64 || g.vmax > 64) return false;
-  g.sl_value = SL_COLLECT + 2 * g.K;
-  g.sl_ack = g.sl_value + g.vmax;
-  g.SW = g.sl_ack + n * g.amax;
-  uint64_t o = 0;
-  auto take = [&](uint32_t& off, uint64_t words) {
-    off = (uint32_t)o;
-    o += (words + 15u) & ~15ull;  // 64-byte aligned tables
-  };
-  take(g.o_slot, (uint64_t)g.NS * g.SW);
-  take(g.o_rec, (uint64_t)g.NS * n * RW);
-  take(g.o_kd, (uint64_t)n * g.ncli_keys * 2u);
-  take(g.o_cl, (uint64_t)C * 8u);
-  take(g.o_kh, R);
-  take(g.o_kl, R);
-  take(g.o_inf, R);
-  take(g.o_arg, R);
-  take(g.o_gp, (uint64_t)R * n);
-  take(g.o_free, R);
-  take(g.o_gco, (uint64_t)n * n * n);
-  take(g.o_tstk, g.NS);
-  take(g.o_fv, g.NS);
-  take(g.o_fi, g.NS);
-  take(g.o_fp, g.NS);
-  take(g.o_wl, 2ull * g.NS);
-  take(g.o_tmp, g.NS);
-  take(g.o_tl, g.NS);
-  take(g.o_tw, g.NS);
-  take(g.o_rdy, C + 64u);
-  if (o > 0x7FFFFFFFull) return false;
-  g.words = (uint32_t)o;
-  return true;
+  g = simx::GeoX{};
+  return simx::geo_build(sp.n, sp.clients_per_region * sp.num_client_regions, sp.keys_per_command, sp.pool_size,
+                         ring, dots, g);
 }
 
 bool simx_table_sizes(const fx_sim_spec& sp, uint32_t ring, uint32_t dots, uint32_t* R, uint32_t* NS) {
@@ -2189,7 +2212,17 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
   }();
   a.row_prefetch = pf_env && a.g.vmax <= 15u ? 1u : 0u;
   const size_t lds = (size_t)(LDS_WORDS + (lx ? a.g.NS : 0u)) * 4u;
-  if (lx) {
+  static const bool gs_env = [] {  // FX_SIMX_GS=0: the generic build only (A/B)
+    const char* e = std::getenv("FX_SIMX_GS");
+    return !(e && e[0] == '0');
+  }();
+  constexpr GeoX gc1 = geo_compiled(1);
+  const bool gs1 = gs_env && std::memcmp(&a.g, &gc1, sizeof(GeoX)) == 0;
+  static_assert(gc1.R > 4096 && gc1.R <= 8192, "configs[3] ring: NG = 2");
+  if (gs1) {
+    if (lx) hipLaunchKernelGGL((k_simx<2, true, 1>), grid, block, lds, hs, a);
+    else hipLaunchKernelGGL((k_simx<2, false, 1>), grid, block, lds, hs, a);
+  } else if (lx) {
     if (a.g.R <= 4096) hipLaunchKernelGGL((k_simx<1, true>), grid, block, lds, hs, a);
     else if (a.g.R <= 8192) hipLaunchKernelGGL((k_simx<2, true>), grid, block, lds, hs, a);
     else hipLaunchKernelGGL((k_simx<4, true>), grid, block, lds, hs, a);
