@@ -198,6 +198,19 @@ struct ArgsX {
   uint32_t* err;
 };
 
+// the kernel's arguments and the instance's spec, read where they are needed
+// (scalar loads through the constant address space, scalar-cache hits); the
+// empty asm makes the pointer opaque so the loads are not hoisted into scalar
+// registers held for the whole run
+typedef __attribute__((address_space(4))) const ArgsX KArgsX;
+typedef __attribute__((address_space(4))) const fx_sim_spec KSpec;
+__device__ __forceinline__ KArgsX* kx() {
+  KArgsX* p = (KArgsX*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+__device__ __forceinline__ KSpec* kspec(uint32_t inst) { return (KSpec*)(kx()->specs + inst); }
+
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t src) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)src);
@@ -266,7 +279,7 @@ template <uint32_t NG, bool LX = false>
 struct Big {
   // ---------------------------------------------------------------- context
   uint32_t lid;
-  ArgsX A;
+
   GeoX g;
   uint32_t* M;    // this instance's arena
   uint32_t* lds;  // histogram caches
@@ -274,8 +287,23 @@ struct Big {
   uint16_t* lstk;  // LX: Tarjan stack (slots)
   uint32_t tep = 7;  // LX: the search epoch (1..7; the table is cleared when it wraps to 1)
   uint32_t inst;
-  uint64_t seed, rng_inst;
-  uint32_t protocol, n, f, synod_f, gc_ms, en_ms, cmds, conflict_, pool, extra, ro_pct;
+  uint32_t protocol, n, f, synod_f;
+  // the instance's other workload parameters are read from its spec where
+  // they are used (scalar loads, scalar-cache hits) instead of being held in
+  // scalar registers for the whole run (the kernel is short of SGPRs)
+  __device__ __forceinline__ KSpec* spec_() const { return kspec(inst); }
+  __device__ __forceinline__ uint64_t seed_() const { return spec_()->seed; }
+  __device__ __forceinline__ uint64_t rng_inst_() const { return spec_()->instance; }
+  __device__ __forceinline__ uint32_t conflict_() const { return spec_()->conflict_rate; }
+  __device__ __forceinline__ uint32_t pool_() const { return spec_()->pool_size; }
+  __device__ __forceinline__ uint32_t ro_pct_() const { return spec_()->read_only_pct; }
+  __device__ __forceinline__ uint32_t cmds_() const { return spec_()->commands_per_client; }
+  __device__ __forceinline__ uint32_t gc_ms_() const { return spec_()->gc_interval_ms; }
+  __device__ __forceinline__ uint32_t en_ms_() const { return spec_()->executed_notification_ms; }
+  __device__ __forceinline__ uint32_t extra_() const {
+    const int32_t e = spec_()->extra_sim_time_ms;
+    return e >= 0 ? (uint32_t)e : 0u;
+  }
   bool has_extra, reorder, nfr;
   uint32_t C, K;
   uint32_t err = 0, err_site = 0;
@@ -405,24 +433,24 @@ struct Big {
 
   // ------------------------------------------------------------- histograms
   __device__ __forceinline__ void hist_chain(uint32_t v) {
-    if (!A.chain_hist) return;
-    const uint32_t b = min(v, A.chain_bins - 1u);
+    if (!kx()->chain_hist) return;
+    const uint32_t b = min(v, kx()->chain_bins - 1u);
     if (lid == 0) {
       if (b < HC_BINS) atomicAdd(&lds[b], 1u);
-      else atomicAdd(&A.chain_hist[b], 1ull);
+      else atomicAdd(&kx()->chain_hist[b], 1ull);
     }
   }
   __device__ __forceinline__ void hist_delay(uint32_t v) {
-    if (!A.delay_hist) return;
-    const uint32_t b = min(v, A.delay_bins - 1u);
+    if (!kx()->delay_hist) return;
+    const uint32_t b = min(v, kx()->delay_bins - 1u);
     if (lid == 0) {
       if (b < HD_BINS) atomicAdd(&lds[HC_BINS + b], 1u);
-      else atomicAdd(&A.delay_hist[b], 1ull);
+      else atomicAdd(&kx()->delay_hist[b], 1ull);
     }
   }
   __device__ __forceinline__ void hist_lat(uint32_t region, uint32_t lat) {
-    if (!A.lat_hist) return;
-    const uint32_t key = region * A.lat_bins + min(lat, A.lat_bins - 1u);
+    if (!kx()->lat_hist) return;
+    const uint32_t key = region * kx()->lat_bins + min(lat, kx()->lat_bins - 1u);
     const uint32_t h = (key * 2654435761u) >> (32 - HL_LOG);
     uint32_t* lc = lds + HC_BINS + HD_BINS;
     const uint32_t k = uni(lc[h]);
@@ -433,7 +461,7 @@ struct Big {
         lc[h] = key + 1u;
         lc[HL_SLOTS + h] = 1u;
       } else {
-        atomicAdd(&A.lat_hist[key], 1ull);
+        atomicAdd(&kx()->lat_hist[key], 1ull);
       }
     }
   }
@@ -533,7 +561,7 @@ struct Big {
   // multiplier in [0, 10) when reordering (one draw per message, in schedule order)
   __device__ __forceinline__ uint32_t msg_delay(uint32_t d) {
     if (!reorder) return d;
-    const uint64_t u = sim_rand(seed, rng_inst, 0, rdraws++, R_REORDER);
+    const uint64_t u = sim_rand(seed_(), rng_inst_(), 0, rdraws++, R_REORDER);
     const double mult = (double)(u >> 11) * (1.0 / 9007199254740992.0) * 10.0;
     return (uint32_t)(uint64_t)((double)d * mult);
   }
@@ -546,14 +574,14 @@ struct Big {
     nk = 0;
     for (uint32_t draw = 0; nk < K && draw < 65536u; ++draw) {  // gen_unique_keys draws until distinct
       bool conflict;
-      if (conflict_ == 0) conflict = false;
-      else if (conflict_ >= 100) conflict = true;
-      else conflict = sim_rand(seed, rng_inst, cid, (uint64_t)idx * 64 + draw, R_CONFLICT) % 100ull < conflict_;
+      if (conflict_() == 0) conflict = false;
+      else if (conflict_() >= 100) conflict = true;
+      else conflict = sim_rand(seed_(), rng_inst_(), cid, (uint64_t)idx * 64 + draw, R_CONFLICT) % 100ull < conflict_();
       uint32_t key;
       if (conflict)
-        key = pool <= 1 ? 0u : (uint32_t)(sim_rand(seed, rng_inst, cid, (uint64_t)idx * 64 + draw, R_POOL) % pool);
+        key = pool_() <= 1 ? 0u : (uint32_t)(sim_rand(seed_(), rng_inst_(), cid, (uint64_t)idx * 64 + draw, R_POOL) % pool_());
       else
-        key = pool + cid;
+        key = pool_() + cid;
       if (nk == 0) {
         k0 = key;
         nk = 1;
@@ -571,9 +599,9 @@ struct Big {
     return k0 | (k1 << 16);
   }
   __device__ __forceinline__ bool gen_read_only(uint32_t cid, uint32_t idx) {  // workload.rs:158-160
-    if (ro_pct == 0) return false;
-    if (ro_pct >= 100) return true;
-    return sim_rand(seed, rng_inst, cid, idx, R_READ_ONLY) % 100ull < ro_pct;
+    if (ro_pct_() == 0) return false;
+    if (ro_pct_() >= 100) return true;
+    return sim_rand(seed_(), rng_inst_(), cid, idx, R_READ_ONLY) % 100ull < ro_pct_();
   }
 
   // ------------------------------------------------------- frame stack
@@ -664,8 +692,8 @@ struct Big {
       S(sl, i) = v;
     }
     for (uint32_t i = lid; i < g.n * RW; i += 64) M[g.o_rec + sl * g.n * RW + i] = 0;
-    if (A.dot_client && s <= A.exec_cap && lid == 0)
-      A.dot_client[((size_t)inst * n + p) * A.exec_cap + s - 1u] = c + 1u;
+    if (kx()->dot_client && s <= kx()->exec_cap && lid == 0)
+      kx()->dot_client[((size_t)inst * n + p) * kx()->exec_cap + s - 1u] = c + 1u;
     act_send(basic ? M_STORE : M_COLLECT, dot, (1u << n) - 1u);
   }
 
@@ -714,12 +742,12 @@ struct Big {
     const uint32_t c = sv(SL_CLIENT);
     const uint32_t nk = (sv(SL_CNT) >> 16) & 3u;
     const uint32_t x0 = rl(pa, A_EXEC + p);
-    if (lid < nk && A.executed && x0 + lid < A.exec_cap)
-      A.executed[((size_t)inst * n + p) * A.exec_cap + x0 + lid] = dot;
+    if (lid < nk && kx()->executed && x0 + lid < kx()->exec_cap)
+      kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + x0 + lid] = dot;
     lset(pa, A_EXEC + p, x0 + nk);
     if ((rd(CL(c, 0)) & 0xFFu) == p) client_result(c, nk);  // pending.wait_for registered this rifl at p
     if (err) return;
-    if (gc_ms) gc_commit(p, dot);  // Forward(MCommitDot) (basic.rs:246-251), before the slot can go
+    if (gc_ms_()) gc_commit(p, dot);  // Forward(MCommitDot) (basic.rs:246-251), before the slot can go
     const uint32_t masks = sv(SL_MASKS);
     if (((masks >> 24) & 0xFFu) + 1u == n) sput(SL_DOT, 0u);  // executed everywhere: free the slot
     else sput(SL_MASKS, masks + (1u << 24));
@@ -861,7 +889,7 @@ struct Big {
     rput(R_PST, (ps & ~3u) | ST_COMMIT);
     const uint32_t masks = sv(SL_MASKS);
     sput(SL_MASKS, masks + (1u << 16));
-    if (gc_ms) gc_commit(p, dot);  // Forward(MCommitDot) to self
+    if (gc_ms_()) gc_commit(p, dot);  // Forward(MCommitDot) to self
   }
 
   // atlas.rs:477-524 / epaxos.rs:430-477
@@ -966,7 +994,7 @@ struct Big {
   // AggregatePending (runner.rs:406-424), executor metrics, execution log
   __device__ __forceinline__ void on_execute(uint32_t sl, uint32_t d, uint32_t start) {
     const uint32_t p = xp;
-    if (xk < A.exec_cap && A.executed && lid == 0) A.executed[((size_t)inst * n + p) * A.exec_cap + xk] = d;
+    if (xk < kx()->exec_cap && kx()->executed && lid == 0) kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + xk] = d;
     ++xk;
     hist_delay(now - start);  // ExecutionDelay (graph/mod.rs:514-518)
     if (rd(RC(sl, p, R_WAIT))) unlink(sl);
@@ -1083,12 +1111,12 @@ struct Big {
       const uint32_t cpr = act ? CL(c, 0) : 0u;
       const uint32_t m = min(64u, cnt - r0);
       if (act) {
-        if (A.executed && xk + lid < A.exec_cap) A.executed[((size_t)inst * n + p) * A.exec_cap + xk + lid] = d;
+        if (kx()->executed && xk + lid < kx()->exec_cap) kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + xk + lid] = d;
         W(g.o_wl, nwl + lid) = sl;
-        if (A.delay_hist) {  // ExecutionDelay (graph/mod.rs:514-518)
-          const uint32_t bn = min(now - st, A.delay_bins - 1u);
+        if (kx()->delay_hist) {  // ExecutionDelay (graph/mod.rs:514-518)
+          const uint32_t bn = min(now - st, kx()->delay_bins - 1u);
           if (bn < HD_BINS) atomicAdd(&lds[HC_BINS + bn], 1u);
-          else atomicAdd(&A.delay_hist[bn], 1ull);
+          else atomicAdd(&kx()->delay_hist[bn], 1ull);
         }
         if (((mk >> 24) & 0xFFu) + 1u == n) S(sl, SL_DOT) = 0u;  // executed everywhere: free the slot
         else S(sl, SL_MASKS) = mk + (1u << 24);
@@ -1383,12 +1411,12 @@ struct Big {
       }
       if (act) {
         RC(sl, p, R_PST) = ps | PS_EXEC;  // executed_clock.add (tarjan.rs:293)
-        if (A.executed && xk + lid < A.exec_cap) A.executed[((size_t)inst * n + p) * A.exec_cap + xk + lid] = d;
+        if (kx()->executed && xk + lid < kx()->exec_cap) kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + xk + lid] = d;
         W(g.o_wl, nwl + lid) = sl;
-        if (A.delay_hist) {  // ExecutionDelay (graph/mod.rs:514-518)
-          const uint32_t bn = min(now - st, A.delay_bins - 1u);
+        if (kx()->delay_hist) {  // ExecutionDelay (graph/mod.rs:514-518)
+          const uint32_t bn = min(now - st, kx()->delay_bins - 1u);
           if (bn < HD_BINS) atomicAdd(&lds[HC_BINS + bn], 1u);
-          else atomicAdd(&A.delay_hist[bn], 1ull);
+          else atomicAdd(&kx()->delay_hist[bn], 1ull);
         }
         if (((mk >> 24) & 0xFFu) + 1u == n) S(sl, SL_DOT) = 0u;  // executed everywhere: free the slot
         else S(sl, SL_MASKS) = mk + (1u << 24);
@@ -1426,7 +1454,7 @@ struct Big {
     fsp = 1;
     uint32_t cv = rsl, ci = 0, cid = 1, clow = 1, ctp = 0, cdot = 0, cnd = 0, drow = 0, jm = 63u;
     frame_row(rsl, cdot, cnd, drow);
-    const bool pf = A.row_prefetch != 0;
+    const bool pf = kx()->row_prefetch != 0;
     bool pv = pf;  // prow holds the current frame's first deps' rows
     uint32_t prow = 0;
     uint32_t pm = dep_status(drow, cnd, cdot, jm, pf, prow);
@@ -1811,7 +1839,7 @@ struct Big {
   // Client::cmd_send: the next command of client c -> SubmitToProc
   __device__ __forceinline__ bool client_send(uint32_t c) {
     const uint32_t issued = rd(CL(c, 1));
-    if (issued >= cmds) return false;
+    if (issued >= cmds_()) return false;
     put(CL(c, 1), issued + 1u);
     put(CL(c, 2), now);  // Pending::start
     const uint32_t d = msg_delay(rd(CL(c, 4)));
@@ -1836,15 +1864,15 @@ struct Big {
         const uint32_t lat = now - rd(CL(c, 2));  // latency.as_millis()
         lat_sum += lat;
 #ifndef FX_SIMX_EVLOG
-        if (lid == 0 && A.latency_log && issued - 1u < A.lat_cap)
-          A.latency_log[((size_t)inst * g.C + c) * A.lat_cap + issued - 1u] = lat;
+        if (lid == 0 && kx()->latency_log && issued - 1u < kx()->lat_cap)
+          kx()->latency_log[((size_t)inst * g.C + c) * kx()->lat_cap + issued - 1u] = lat;
 #endif
         hist_lat(rd(CL(c, 0)) >> 8, lat);
         if (!client_send(c)) {
           ++clients_done;
           if (clients_done == g.C) {
             if (has_extra) {
-              final_ms = now + extra;
+              final_ms = now + extra_();
               in_extra = true;
             } else {
               done = true;
@@ -1857,12 +1885,12 @@ struct Big {
       case E_TICK: {
         XPROF_T0();
         gc_tick(to);
-        push_event(now + gc_ms, (1u << 6) | (to << 3), E_TICK | (to << 8), 0);
+        push_event(now + gc_ms_(), (1u << 6) | (to << 3), E_TICK | (to << 8), 0);
         XPROF_ADD(PF_GC);
         return;
       }
       case E_NOTIF:  // GraphExecutor::executed is None (executor/mod.rs:74-79)
-        push_event(now + en_ms, 0u, E_NOTIF | (to << 8), 0);
+        push_event(now + en_ms_(), 0u, E_NOTIF | (to << 8), 0);
         return;
       case M_GC: {
         XPROF_T0();
@@ -1901,28 +1929,18 @@ __global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
   s.ltl = reinterpret_cast<uint16_t*>(smem + LDS_WORDS);
   s.lstk = s.ltl + s.g.NS;
   s.lid = threadIdx.x;
-  s.A = a;
   s.M = a.arena + (size_t)inst * s.g.words;
   s.lds = smem;
   s.inst = inst;
   const fx_sim_spec& sp = a.specs[inst];
-  s.seed = sp.seed;
-  s.rng_inst = sp.instance;
   s.protocol = sp.protocol;
   s.n = s.g.n;
   s.f = sp.f;
   s.C = s.g.C;
   s.K = s.g.K;
-  s.gc_ms = sp.gc_interval_ms;
-  s.en_ms = sp.executed_notification_ms;
-  s.cmds = sp.commands_per_client;
-  s.conflict_ = sp.conflict_rate;
-  s.pool = sp.pool_size;
-  s.ro_pct = sp.read_only_pct;
   s.reorder = sp.reorder_messages != 0;
   s.nfr = sp.nfr != 0;
   s.has_extra = sp.extra_sim_time_ms >= 0;
-  s.extra = s.has_extra ? (uint32_t)sp.extra_sim_time_ms : 0u;
   const uint32_t n = s.n;
   uint32_t fq, wq;
   if (s.protocol == FX_PROTOCOL_ATLAS) {
@@ -2003,15 +2021,15 @@ __global__ __launch_bounds__(64, FX_SIMX_WAVES) void k_simx(ArgsX a) {
   }
   __syncthreads();
   // periodic events (runner.rs:179-187), then clients (run(), C5 ascending)
-  if (s.gc_ms)
-    for (uint32_t p = 0; p < n; ++p) s.push_event(s.gc_ms, (1u << 6) | (p << 3), E_TICK | (p << 8), 0);
+  if (s.gc_ms_())
+    for (uint32_t p = 0; p < n; ++p) s.push_event(s.gc_ms_(), (1u << 6) | (p << 3), E_TICK | (p << 8), 0);
   const bool sim_en = a.sim_exec_notif || s.has_extra;
   for (uint32_t p = 0; p < n; ++p) {
-    if (sim_en) s.push_event(s.en_ms, 0u, E_NOTIF | (p << 8), 0);
+    if (sim_en) s.push_event(s.en_ms_(), 0u, E_NOTIF | (p << 8), 0);
     else ++s.seq;  // keep the insertion numbering of the reference
   }
   for (uint32_t c = 0; c < s.C && !s.err; ++c) {
-    if (s.cmds == 0) s.err = FX_ERR_INVALID_ARG;
+    if (s.cmds_() == 0) s.err = FX_ERR_INVALID_ARG;
     else s.client_send(c);
   }
   // ------------------------------------------------------------ loop
