@@ -1,0 +1,19 @@
+# k_simx occupancy A/B with the compiled configs[3] geometry: 3 vs 4 waves per SIMD
+# (build_w4g), dense-sim at 3,072 and 4,096 instances
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+M=gpurun_out/r5o2; mkdir -p $M
+FX_LIB=fantoch_amd/build_w4g/libfantoch_amd.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
+  tests/test_sim_large.py tests/test_sim_capture.py tests/test_poison_all.py -k "not pred and not executor and not escalation and not persistent" > $M/tests.log 2>&1 || { echo "tests rc=$?"; tail -40 $M/tests.log; exit 1; }
+tail -1 $M/tests.log
+run() {  # name seeds env...
+  local nm=$1 sd=$2; shift 2
+  env "$@" timeout -k 10 300 python3 bench.py --mode dense-sim --no-cpu-baseline --steps 2 --warmup 1 --seeds $sd > $M/$nm.log 2>&1 \
+    || { echo "$nm rc=$?"; tail -5 $M/$nm.log; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open('$M/$nm.log').read().strip().splitlines()[-1]); print('%-10s %8.2f M cmds/s  %8.1f ms' % ('$nm', d['value']/1e6, d['ms_per_step']))"
+}
+run w3 3072
+
+run w3_4096 4096
+run w4_3072 3072 FX_LIB=fantoch_amd/build_w4g/libfantoch_amd.so
+run w4_4096 4096 FX_LIB=fantoch_amd/build_w4g/libfantoch_amd.so
