@@ -68,6 +68,14 @@ struct Lay {
   }
 };
 
+// the SMALL tier of the compiled n = 5 build (k_pred<false, 5, 5, 2>): 64
+// vertices, 64 index slots per source, 512-bit windows, lists 4 per vertex
+__host__ __device__ inline Lay small_fixed_layout(uint32_t n, uint32_t D) {
+  Lay L{};
+  L.make(64, 64, 16, n, D, 4 * 64);
+  return L;
+}
+
 struct PArgs {
   KArgs k;
   const uint32_t* clo;
@@ -75,6 +83,10 @@ struct PArgs {
   const uint32_t* ndeps;
 };
 
+// WG: more than one wavefront (stream) per workgroup; each touches only its
+// own tables, so a wave-level barrier orders its LDS accesses (a workgroup
+// barrier would couple the streams, whose control flow differs)
+template <bool WG = false>
 struct Pr {
   PArgs a;
   Lay L;
@@ -85,6 +97,15 @@ struct Pr {
   // index finds no waiter, so its scan of the vertex table is skipped
   uint32_t nreg0 = 0, nreg1 = 0;
 
+  __device__ __forceinline__ void sync() {
+    if constexpr (WG) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+      __syncthreads();
+    }
+  }
   __device__ __forceinline__ void put(uint32_t b, uint32_t i, uint32_t v) {
     if (lid == 0) m[b + i] = v;
   }
@@ -97,7 +118,7 @@ struct Pr {
   }
   __device__ __forceinline__ void reg_clear(uint32_t v) {
     for (uint32_t i = lid; i < 2 * L.DW; i += 64) m[L.vreg + ((i / L.DW) * L.P + v) * L.DW + i % L.DW] = 0;
-    __syncthreads();
+    sync();
   }
 
   // AEClock over a frontier word + ring bitmap (committed: c*, executed: e*)
@@ -185,7 +206,7 @@ struct Pr {
       }
       cnt += __builtin_popcountll(b);
     }
-    __syncthreads();
+    sync();
     if (ph) nreg1 -= cnt;
     else nreg0 -= cnt;
     if (!cnt) return;  // an empty frame does nothing
@@ -199,7 +220,7 @@ struct Pr {
         m[L.lists + base + r] = x;
       }
     }
-    __syncthreads();
+    sync();
     ltop += cnt;
     put(L.frames, fsp * 4 + 0, ph);
     put(L.frames, fsp * 4 + 1, base);
@@ -369,7 +390,7 @@ struct Pr {
       for (uint32_t j = lid + 64; j < nd; j += 64) m[L.vdeps + v * L.D + j] = a.k.deps[(size_t)j * a.k.plane + at];
     }
     put(L.hidx, h, v + 1);
-    __syncthreads();
+    sync();
     push_removed(0, d);  // try_phase_one_pending(dot)
     run();
     if (err) return;
@@ -380,31 +401,36 @@ struct Pr {
   }
 };
 
-// FN / FD != 0: the SMALL tier's layout for n = FN sources and FD dep planes
-// compiled in (the configs[1] shape, n = 5): table offsets become immediates,
-// which frees the scalar registers the layout's fields held (the generic
-// build spills about 50 SGPRs to VGPR lanes)
-template <bool HBM, uint32_t FN = 0, uint32_t FD = 0>
-__global__ __launch_bounds__(64) void k_pred(PArgs a, Lay Lrt) {
+// FN / FD != 0 (the configs[1] shape, n = 5, dmax = 5): the SMALL tier with
+// its layout compiled in -- table offsets become immediates, which frees the
+// scalar registers the layout's fields held (the generic build spills about
+// 50 SGPRs to VGPR lanes) -- and sized for occupancy: 64 index slots per
+// source and 512-bit clock windows (7.9 KB of tables instead of 9.8), WPB = 2
+// streams per workgroup.  A CU holds at most 16 workgroups, and 9.8 KB tables
+// at one stream each stopped there; 20 streams fit now.  Streams that
+// outgrow the smaller tables rerun on the LDS tier as before.
+template <bool HBM, uint32_t FN = 0, uint32_t FD = 0, uint32_t WPB = 1>
+__global__ __launch_bounds__(64 * WPB) void k_pred(PArgs a, Lay Lrt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t li = xcd_slot(blockIdx.x);
-  if (li >= a.k.num_lanes) return;
+  const uint32_t wv = WPB > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
+  const uint32_t li = xcd_slot(blockIdx.x) * WPB + wv;
+  if (li >= a.k.num_lanes) return;  // whole wavefront
   Lay L = Lrt;
   if constexpr (FN != 0) {
-    L.make(64, 128, 32, FN, FD, 4 * 64);
+    L = small_fixed_layout(FN, FD);
     a.k.n = FN;
     a.k.dmax = FD;
   }
-  Pr w;
+  Pr<(WPB > 1)> w;
   w.a = a;
   w.L = L;
-  w.lid = threadIdx.x;
+  w.lid = threadIdx.x & 63u;
   w.s = a.k.stream_map ? a.k.stream_map[li] : li;
-  w.m = HBM ? a.k.state + (size_t)li * L.words : smem;
+  w.m = HBM ? a.k.state + (size_t)li * L.words : smem + wv * L.words;
   for (uint32_t i = w.lid; i < L.words; i += 64) w.m[i] = 0;
-  __syncthreads();
+  w.sync();
   for (uint32_t i = w.lid; i < L.P; i += 64) w.m[L.vfree + i] = L.P - 1u - i;
-  __syncthreads();
+  w.sync();
   w.nfree = L.P;
   const uint32_t len = a.k.lengths ? min(a.k.lengths[w.s], a.k.steps) : a.k.steps;
   uint32_t row = len ? w.row_load(0) : 0u, next = len > 4 ? w.row_load(4) : 0u;
@@ -504,13 +530,15 @@ extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* ou
     if (!configured) {
       (void)hipFuncSetAttribute((const void*)pred::k_pred<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)pred::k_pred<false, 5, 5>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
+      (void)hipFuncSetAttribute((const void*)pred::k_pred<false, 5, 5, 2>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       configured = true;
     }
-    if (tier == FX_PRED_TIER_SMALL && in->base.n == 5 && std::max(in->base.dmax, 1u) == 5)
-      hipLaunchKernelGGL((pred::k_pred<false, 5, 5>), dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
-    else
+    if (tier == FX_PRED_TIER_SMALL && in->base.n == 5 && std::max(in->base.dmax, 1u) == 5) {
+      const pred::Lay L5 = pred::small_fixed_layout(5, 5);
+      hipLaunchKernelGGL((pred::k_pred<false, 5, 5, 2>), dim3(xcd_grid((num_lanes + 1u) / 2u)), dim3(128),
+                         (size_t)L5.words * 4 * 2, hs, a, L5);
+    } else
       hipLaunchKernelGGL(pred::k_pred<false>, dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
   }
   if (hipGetLastError() != hipSuccess) return FX_ERR_HIP;
