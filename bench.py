@@ -99,9 +99,10 @@ def parse(argv=None):
 MODE_DEFAULTS = {
     "sim": dict(seeds=4096, conflicts="0,2,10,50,100", protocol="epaxos", f=2),
     # BASELINE configs[3] on the simulator: one resident wavefront per
-    # instance, k_simx runs 3 waves per SIMD (164 VGPRs): 12 per CU x 256 CUs
-    # = 3,072 (4,096 adds a second, one-third-occupied round: 99 -> 72 M)
-    "dense-sim": dict(seeds=3072, conflicts="100", protocol="both", f=2),
+    # instance; k_simx's configs[3] build runs 4 waves per SIMD: 16 per CU x
+    # 256 CUs = 4,096, one round (3 waves per SIMD and 3,072 instances:
+    # 117 M; 4 and 4,096: 138 M, tools/r5_occ2.sh)
+    "dense-sim": dict(seeds=4096, conflicts="100", protocol="both", f=2),
     # configs[3] on the batched executor: 3,072 instances = 15,360 streams,
     # one wavefront each, 5 per CU (LDS tables): 12 rounds, so the last
     # round's tail weighs less than at 768 instances (68.3 M; 1,536: 73.2 M;
