@@ -409,6 +409,9 @@ struct Pr {
 // streams per workgroup.  A CU holds at most 16 workgroups, and 9.8 KB tables
 // at one stream each stopped there; 20 streams fit now.  Streams that
 // outgrow the smaller tables rerun on the LDS tier as before.
+#ifndef FX_PRED_WPB
+#define FX_PRED_WPB 2  // streams per workgroup of the compiled n = 5 SMALL build
+#endif
 template <bool HBM, uint32_t FN = 0, uint32_t FD = 0, uint32_t WPB = 1>
 __global__ __launch_bounds__(64 * WPB) void k_pred(PArgs a, Lay Lrt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -530,14 +533,15 @@ extern "C" int fx_pred_execute(const fx_pred_batch* in, const fx_order_batch* ou
     if (!configured) {
       (void)hipFuncSetAttribute((const void*)pred::k_pred<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)pred::k_pred<false, 5, 5, 2>,
+      (void)hipFuncSetAttribute((const void*)pred::k_pred<false, 5, 5, FX_PRED_WPB>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       configured = true;
     }
     if (tier == FX_PRED_TIER_SMALL && in->base.n == 5 && std::max(in->base.dmax, 1u) == 5) {
       const pred::Lay L5 = pred::small_fixed_layout(5, 5);
-      hipLaunchKernelGGL((pred::k_pred<false, 5, 5, 2>), dim3(xcd_grid((num_lanes + 1u) / 2u)), dim3(128),
-                         (size_t)L5.words * 4 * 2, hs, a, L5);
+      constexpr uint32_t W = FX_PRED_WPB;
+      hipLaunchKernelGGL((pred::k_pred<false, 5, 5, W>), dim3(xcd_grid((num_lanes + W - 1u) / W)), dim3(64 * W),
+                         (size_t)L5.words * 4 * W, hs, a, L5);
     } else
       hipLaunchKernelGGL(pred::k_pred<false>, dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
   }
