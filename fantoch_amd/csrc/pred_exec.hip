@@ -37,14 +37,15 @@ struct Lay {
   uint32_t P, Q, WB, n, D, DW, FD, LL;
   uint32_t vdot, vrec, vclo, vchi, vmiss, vnd, vreg, vdeps, vfree, hidx, cfront, cbits, efront, ebits, frames,
       lists, tmp, words;
-  __host__ __device__ void make(uint32_t P_, uint32_t Q_, uint32_t WB_, uint32_t n_, uint32_t D_, uint32_t LL_) {
+  __host__ __device__ void make(uint32_t P_, uint32_t Q_, uint32_t WB_, uint32_t n_, uint32_t D_, uint32_t LL_,
+                                uint32_t FD_ = 0) {
     P = P_;
     Q = Q_;
     WB = WB_;
     n = n_;
     D = D_;
     DW = (D + 31) / 32;
-    FD = P;
+    FD = FD_ ? FD_ : P;
     LL = LL_;
     uint32_t o = 0;
     vdot = o; o += P;
@@ -68,11 +69,18 @@ struct Lay {
   }
 };
 
-// the SMALL tier of the compiled n = 5 build (k_pred<false, 5, 5, 2>): 64
-// vertices, 64 index slots per source, 512-bit windows, lists 4 per vertex
+// the SMALL tier of the compiled n = 5 build (k_pred<false, 5, 5, WPB>): 64
+// vertices, 64 index slots per source, 512-bit windows, FX_PRED_FRAMES
+// recursion frames and FX_PRED_LISTS waiter-list entries
+#ifndef FX_PRED_FRAMES
+#define FX_PRED_FRAMES 64
+#endif
+#ifndef FX_PRED_LISTS
+#define FX_PRED_LISTS 256
+#endif
 __host__ __device__ inline Lay small_fixed_layout(uint32_t n, uint32_t D) {
   Lay L{};
-  L.make(64, 64, 16, n, D, 4 * 64);
+  L.make(64, 64, 16, n, D, FX_PRED_LISTS, FX_PRED_FRAMES);
   return L;
 }
 
@@ -410,7 +418,7 @@ struct Pr {
 // at one stream each stopped there; 20 streams fit now.  Streams that
 // outgrow the smaller tables rerun on the LDS tier as before.
 #ifndef FX_PRED_WPB
-#define FX_PRED_WPB 2  // streams per workgroup of the compiled n = 5 SMALL build
+#define FX_PRED_WPB 4  // streams per workgroup of the compiled n = 5 SMALL build
 #endif
 template <bool HBM, uint32_t FN = 0, uint32_t FD = 0, uint32_t WPB = 1>
 __global__ __launch_bounds__(64 * WPB) void k_pred(PArgs a, Lay Lrt) {
