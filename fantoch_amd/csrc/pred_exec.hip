@@ -70,17 +70,24 @@ struct Lay {
 };
 
 // the SMALL tier of the compiled n = 5 build (k_pred<false, 5, 5, WPB>): 64
-// vertices, 64 index slots per source, 512-bit windows, FX_PRED_FRAMES
-// recursion frames and FX_PRED_LISTS waiter-list entries
+// vertices, FX_PRED_Q index slots per source, FX_PRED_WB-word clock windows,
+// FX_PRED_FRAMES recursion frames and FX_PRED_LISTS waiter-list entries
+// (6.7 KB: 24 streams per CU at 4 per workgroup)
 #ifndef FX_PRED_FRAMES
-#define FX_PRED_FRAMES 64
+#define FX_PRED_FRAMES 32
 #endif
 #ifndef FX_PRED_LISTS
-#define FX_PRED_LISTS 256
+#define FX_PRED_LISTS 96
+#endif
+#ifndef FX_PRED_Q
+#define FX_PRED_Q 64
+#endif
+#ifndef FX_PRED_WB
+#define FX_PRED_WB 16
 #endif
 __host__ __device__ inline Lay small_fixed_layout(uint32_t n, uint32_t D) {
   Lay L{};
-  L.make(64, 64, 16, n, D, FX_PRED_LISTS, FX_PRED_FRAMES);
+  L.make(64, FX_PRED_Q, FX_PRED_WB, n, D, FX_PRED_LISTS, FX_PRED_FRAMES);
   return L;
 }
 
