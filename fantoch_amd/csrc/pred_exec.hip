@@ -72,7 +72,7 @@ struct Lay {
 // the SMALL tier of the compiled n = 5 build (k_pred<false, 5, 5, WPB>): 64
 // vertices, FX_PRED_Q index slots per source, FX_PRED_WB-word clock windows,
 // FX_PRED_FRAMES recursion frames and FX_PRED_LISTS waiter-list entries
-// (6.7 KB: 24 streams per CU at 4 per workgroup)
+// (5.6 KB: 28 streams per CU at 4 per workgroup)
 #ifndef FX_PRED_FRAMES
 #define FX_PRED_FRAMES 32
 #endif
@@ -80,10 +80,10 @@ struct Lay {
 #define FX_PRED_LISTS 96
 #endif
 #ifndef FX_PRED_Q
-#define FX_PRED_Q 64
+#define FX_PRED_Q 32
 #endif
 #ifndef FX_PRED_WB
-#define FX_PRED_WB 16
+#define FX_PRED_WB 8
 #endif
 __host__ __device__ inline Lay small_fixed_layout(uint32_t n, uint32_t D) {
   Lay L{};
@@ -419,10 +419,10 @@ struct Pr {
 // FN / FD != 0 (the configs[1] shape, n = 5, dmax = 5): the SMALL tier with
 // its layout compiled in -- table offsets become immediates, which frees the
 // scalar registers the layout's fields held (the generic build spills about
-// 50 SGPRs to VGPR lanes) -- and sized for occupancy: 64 index slots per
-// source and 512-bit clock windows (7.9 KB of tables instead of 9.8), WPB = 2
-// streams per workgroup.  A CU holds at most 16 workgroups, and 9.8 KB tables
-// at one stream each stopped there; 20 streams fit now.  Streams that
+// 50 SGPRs to VGPR lanes) -- and sized for occupancy: smaller tables
+// (small_fixed_layout) and WPB streams per workgroup.  A CU holds at most 16
+// workgroups, so one stream per workgroup stopped at 16 streams per CU
+// whatever the tables; 4 per workgroup on 5.6 KB tables run 28.  Streams that
 // outgrow the smaller tables rerun on the LDS tier as before.
 #ifndef FX_PRED_WPB
 #define FX_PRED_WPB 4  // streams per workgroup of the compiled n = 5 SMALL build

@@ -1,5 +1,5 @@
 # round-5: k_pred 6.7 KB tables (in-tree) vs 32 index slots per source and
-# and 96 list entries (build_pw4t: 6.7 KB tables, 24 streams per CU); the GPU
+# 256-bit windows (build_pw4t: 5.6 KB, 28 streams per CU); the GPU
 # pred tests of both first
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
