@@ -95,7 +95,10 @@ struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-
 // looked up for all of its deps at once when the frame is entered (lane j:
 // dep j, one round trip), so an edge only reads the dep's vertex
 constexpr uint32_t RS_EXEC = 0x80000000u;
-template <bool PK, uint32_t FD = 0>
+// WG: several streams (wavefronts) per workgroup, each on its own tables: a
+// wave-level barrier orders a wave's LDS accesses (a workgroup barrier would
+// couple streams whose control flow differs)
+template <bool PK, uint32_t FD = 0, bool WG = false>
 struct W {
 #ifdef FX_WIDE_NO_RS
   static constexpr bool RS = false;
@@ -112,6 +115,15 @@ struct W {
   bool partial = false;  // FX_FLAG_PARTIAL
   uint32_t nml = 0;      // missing deps collected by a first search (partial)
 
+  __device__ __forceinline__ void sync() {
+    if constexpr (WG) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+      __syncthreads();
+    }
+  }
   __device__ __forceinline__ uint32_t& at(uint32_t base, uint32_t i) { return m[base + i]; }
   // a uniform store: every lane writes the same word (LDS: no exec-mask
   // save / restore around it; HBM: lane 0)
@@ -264,7 +276,7 @@ struct W {
         lset(L.tmp, r, v);
       }
     }
-    __syncthreads();
+    sync();
     if (nexec + cnt > a.steps) { err = FX_ERR_ORDER_OVERFLOW; return; }
     if (nwl + cnt > L.wlcap) { err = FX_ERR_CAPACITY; return; }
     // emission, one lane per member (members are distinct vertices): the
@@ -285,7 +297,7 @@ struct W {
         at(L.wl, nwl + r) = d;
       }
     }
-    __syncthreads();
+    sync();
     nexec += cnt;
     nfree += cnt;
     nwl += cnt;
@@ -508,7 +520,7 @@ struct W {
         }
       }
     }
-    __syncthreads();
+    sync();
     // ids of finished (popped) vertices are gone with their slots; a finished
     // vertex still present was on the stack, handled above
     tsp = 0;
@@ -553,7 +565,7 @@ struct W {
     if (c >= PW) { err = FX_ERR_CAPACITY; return; }
     put(L.vwl, v * PW + c, m);
     put(L.vwn, v, c + 1);
-    __syncthreads();
+    sync();
   }
 
   // check_pending (mod.rs:556-587) + try_pending (589-642)
@@ -586,7 +598,7 @@ struct W {
         }
         cnt += __builtin_popcountll(b);
       }
-      __syncthreads();
+      sync();
       if (!cnt) continue;
       // rank sort the waiters by dot into tl
       for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
@@ -598,7 +610,7 @@ struct W {
           lset(L.tl, r, x);
         }
       }
-      __syncthreads();
+      sync();
       // try_pending: visited-skip set = vertices marked with this epoch
       ++epoch;
       uint32_t cur = epoch;
@@ -632,7 +644,7 @@ struct W {
     if constexpr (PK) {
       if (epoch < PK_EPOCH_MAX) return;
       for (uint32_t i = lid; i < L.P; i += 64) m[L.vmark + i] = 0u;
-      __syncthreads();
+      sync();
       epoch = 1;
     }
   }
@@ -645,10 +657,10 @@ struct W {
     const uint32_t kind = FX_HDR_KIND(a.hdr[ix(r)]);
     if (kind == FX_KIND_EXECUTED && partial) {  // RequestReply::Executed (mod.rs:394-402)
       clock_add(d);
-      __syncthreads();
+      sync();
       nwl = 0;
       put(L.wl, nwl++, d);
-      __syncthreads();
+      sync();
       check_pending();
       return;
     }
@@ -679,7 +691,7 @@ struct W {
     put(L.vce, v, NONE);
     if (partial) put(L.vwn, v, 0);
     lput(L.hidx, h, hword(v, d));
-    __syncthreads();
+    sync();
     if (kind == FX_KIND_INDEX_ONLY) return;  // VertexIndex::index without a search (test hook)
     nwl = 0;
     // Search-result cache (as sim_big.hip x_add_): the first search from v
@@ -708,7 +720,7 @@ struct W {
         if (cm && cm != d && cs >= 1 && cs <= L.n && find(cm) == NONE && !contains(cm)) {
           index_pending(v, cm);
           put(L.vce, v, nexec);
-          __syncthreads();
+          sync();
           return;  // no search ran: nothing released
         }
       }
@@ -730,38 +742,44 @@ struct W {
       err = FX_ERR_CAPACITY;  // "just added dot must be pending" (mod.rs:257-259)
       return;
     }
-    __syncthreads();
+    sync();
     check_pending();
   }
 };
 
+// streams per workgroup of the compiled n = 5 LDS build (1: one stream per
+// workgroup; k > 1: k neighbouring streams share a CU and their plane lines)
+#ifndef FX_WIDE_WPB
+#define FX_WIDE_WPB 1
+#endif
 // FN / FD != 0: the layout of n = FN sources and FD dep planes compiled in
 // (the configs[3] shape, n = 5): table offsets become immediates and the
 // layout's fields leave the scalar registers, which the DFS is short of
-template <bool HBM, uint32_t FN = 0, uint32_t FD = 0>
-__global__ __launch_bounds__(64) void k_graph_wide(KArgs a, Lay Lrt) {
+template <bool HBM, uint32_t FN = 0, uint32_t FD = 0, uint32_t WPB = 1>
+__global__ __launch_bounds__(64 * WPB) void k_graph_wide(KArgs a, Lay Lrt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t lane_idx = xcd_slot(blockIdx.x);
-  if (lane_idx >= a.num_lanes) return;
+  const uint32_t wv = WPB > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
+  const uint32_t lane_idx = xcd_slot(blockIdx.x) * WPB + wv;
+  if (lane_idx >= a.num_lanes) return;  // whole wavefront
   Lay L = Lrt;
   if constexpr (FN != 0) L.make(512, 256, 32, FN, FD, false, true);
-  W<!HBM, FD> w;
+  W<!HBM, FD, (WPB > 1)> w;
   w.a = a;
   w.L = L;
-  w.lid = threadIdx.x;
+  w.lid = threadIdx.x & 63u;
   w.slot = lane_idx;
   w.s = a.stream_map ? a.stream_map[lane_idx] : lane_idx;
   w.partial = HBM && (a.flags & FX_FLAG_PARTIAL);
-  w.m = HBM ? a.state + (size_t)lane_idx * L.words : smem;
+  w.m = HBM ? a.state + (size_t)lane_idx * L.words : smem + wv * L.words;
   const uint32_t len = a.lengths ? min(a.lengths[w.s], a.steps) : a.steps;
   if (a.flags & FX_FLAG_INIT) {
     // init tables (the dep rows are written before they are read)
     for (uint32_t i = w.lid; i < L.words; i += 64)
       if (i < L.vdeps || i >= L.vdeps + L.P * L.D) w.m[i] = 0;
-    __syncthreads();
+    w.sync();
     for (uint32_t i = w.lid; i < L.P; i += 64) w.lset(L.vfree, i, L.P - 1u - i);
     if (a.init_frontier && w.lid < L.n) w.m[L.front + w.lid] = a.init_frontier[(size_t)w.s * 8 + w.lid];
-    __syncthreads();
+    w.sync();
     w.nfree = L.P;
     if (w.partial && w.lid == 0) a.req[(size_t)lane_idx * (1 + 2 * (size_t)a.req_cap)] = 0;
   } else {  // resume (HBM tables only): the tables are in place, the scalars saved
@@ -865,11 +883,17 @@ int launch_wide(const KArgs& a, bool hbm, hipStream_t hs) {
     if (!configured) {
       (void)hipFuncSetAttribute((const void*)wide::k_graph_wide<false, 5, 5>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)wide::k_graph_wide<false, 5, 5, FX_WIDE_WPB>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       (void)hipFuncSetAttribute((const void*)wide::k_graph_wide<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
       configured = true;
     }
-    if (a.n == 5 && std::max(a.dmax, 1u) == 5)
+    constexpr uint32_t WPB = FX_WIDE_WPB;
+    if (a.n == 5 && std::max(a.dmax, 1u) == 5 && WPB > 1 && (size_t)L.words * 4 * WPB <= 160 * 1024)
+      hipLaunchKernelGGL((wide::k_graph_wide<false, 5, 5, WPB>), dim3(xcd_grid((a.num_lanes + WPB - 1) / WPB)),
+                         dim3(64 * WPB), (size_t)L.words * 4 * WPB, hs, a, L);
+    else if (a.n == 5 && std::max(a.dmax, 1u) == 5)
       hipLaunchKernelGGL((wide::k_graph_wide<false, 5, 5>), dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
     else
       hipLaunchKernelGGL(wide::k_graph_wide<false>, dim3(grid), dim3(64), (size_t)L.words * 4, hs, a, L);
