@@ -1916,15 +1916,23 @@ struct Big {
 #ifndef FX_SIMX_WAVES_GS
 #define FX_SIMX_WAVES_GS 4
 #endif
+// instances per workgroup of that build (a CU holds at most 16 workgroups)
+#ifndef FX_SIMX_WPB
+#define FX_SIMX_WPB 1
+#endif
 // GS != 0: the geometry geo_compiled(GS) compiled in (the host launches it
 // when the batch's geometry equals it word for word): its offsets become
 // immediates instead of scalar registers, of which the kernel is short
-template <uint32_t NG, bool LX, uint32_t GS = 0>
-__global__ __launch_bounds__(64, (GS != 0 && !LX) ? FX_SIMX_WAVES_GS : FX_SIMX_WAVES) void k_simx(ArgsX a) {
-  // LDS_WORDS of histogram caches, then (LX) the Tarjan words and stack: u16[NS] each
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t inst = blockIdx.x;
-  if (inst >= a.instances) return;
+template <uint32_t NG, bool LX, uint32_t GS = 0, uint32_t WPB = 1>
+__global__ __launch_bounds__(64 * WPB, (GS != 0 && !LX) ? FX_SIMX_WAVES_GS : FX_SIMX_WAVES) void k_simx(ArgsX a) {
+  // LDS_WORDS of histogram caches, then (LX) the Tarjan words and stack: u16[NS] each;
+  // WPB > 1 (no LX): WPB instances per workgroup, LDS_WORDS each
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem_all[];
+  static_assert(WPB == 1 || !LX, "one LX instance per workgroup");
+  const uint32_t wv = WPB > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
+  uint32_t* smem = smem_all + wv * LDS_WORDS;
+  const uint32_t inst = blockIdx.x * WPB + wv;
+  if (inst >= a.instances) return;  // whole wavefront
   Big<NG, LX> s;
   if constexpr (GS != 0) {
     constexpr GeoX gc = geo_compiled(GS);
@@ -1935,7 +1943,7 @@ __global__ __launch_bounds__(64, (GS != 0 && !LX) ? FX_SIMX_WAVES_GS : FX_SIMX_W
   }
   s.ltl = reinterpret_cast<uint16_t*>(smem + LDS_WORDS);
   s.lstk = s.ltl + s.g.NS;
-  s.lid = threadIdx.x;
+  s.lid = threadIdx.x & 63u;
   s.M = a.arena + (size_t)inst * s.g.words;
   s.lds = smem;
   s.inst = inst;
@@ -2026,7 +2034,13 @@ __global__ __launch_bounds__(64, (GS != 0 && !LX) ? FX_SIMX_WAVES_GS : FX_SIMX_W
       c0 += sp.clients_per_region;
     }
   }
-  __syncthreads();
+  if constexpr (WPB > 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
   // periodic events (runner.rs:179-187), then clients (run(), C5 ascending)
   if (s.gc_ms_())
     for (uint32_t p = 0; p < n; ++p) s.push_event(s.gc_ms_(), (1u << 6) | (p << 3), E_TICK | (p << 8), 0);
@@ -2089,7 +2103,13 @@ __global__ __launch_bounds__(64, (GS != 0 && !LX) ? FX_SIMX_WAVES_GS : FX_SIMX_W
     if (s.events >= max_events) s.err = FX_ERR_SIM_EVENTS;
   }
   // ----------------------------------------------------------- outputs
-  __syncthreads();
+  if constexpr (WPB > 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
   const uint32_t o_exec = gather(s.pa, (s.A_EXEC + s.lid) & 63u), o_fast = gather(s.pa, (s.A_FAST + s.lid) & 63u),
                  o_slow = gather(s.pa, (s.A_SLOW + s.lid) & 63u), o_stab = gather(s.pa, (s.A_STAB + s.lid) & 63u),
                  o_fr = gather(s.pa, (s.A_FR + s.lid) & 63u), o_sr = gather(s.pa, (s.A_SR + s.lid) & 63u);
@@ -2246,6 +2266,9 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
   static_assert(gc1.R > 4096 && gc1.R <= 8192, "configs[3] ring: NG = 2");
   if (gs1) {
     if (lx) hipLaunchKernelGGL((k_simx<2, true, 1>), grid, block, lds, hs, a);
+    else if (FX_SIMX_WPB > 1)
+      hipLaunchKernelGGL((k_simx<2, false, 1, FX_SIMX_WPB>), dim3((b->instances + FX_SIMX_WPB - 1) / FX_SIMX_WPB),
+                         dim3(64 * FX_SIMX_WPB), lds * FX_SIMX_WPB, hs, a);
     else hipLaunchKernelGGL((k_simx<2, false, 1>), grid, block, lds, hs, a);
   } else if (lx) {
     if (a.g.R <= 4096) hipLaunchKernelGGL((k_simx<1, true>), grid, block, lds, hs, a);
