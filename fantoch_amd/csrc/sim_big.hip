@@ -1907,18 +1907,20 @@ struct Big {
 
 // waves per SIMD the register budget is built for (3: 168 VGPRs, no spills).
 // The build with configs[3]'s geometry compiled in (GS, HBM Tarjan records)
-// holds fewer values in registers and is built for 4 (128 VGPRs, 52 bytes of
-// spills per lane): 16 instances per CU instead of 12, 117 -> 138 M cmds/s
-// at 4,096 instances (tools/r5_occ2.sh)
+// holds fewer values in registers: at 4 (128 VGPRs, 52 bytes of spills per
+// lane) 16 instances per CU instead of 12, 117 -> 138 M cmds/s at 4,096
+// instances (tools/r5_occ2.sh); at 5 (102 VGPRs, 136 bytes of spills) with
+// two instances per workgroup (a CU holds at most 16 workgroups) 20 per CU,
+// 139.4 -> 144.3 M at 5,120 instances (tools/r5_x5.sh)
 #ifndef FX_SIMX_WAVES
 #define FX_SIMX_WAVES 3
 #endif
 #ifndef FX_SIMX_WAVES_GS
-#define FX_SIMX_WAVES_GS 4
+#define FX_SIMX_WAVES_GS 5
 #endif
 // instances per workgroup of that build (a CU holds at most 16 workgroups)
 #ifndef FX_SIMX_WPB
-#define FX_SIMX_WPB 1
+#define FX_SIMX_WPB 2
 #endif
 // GS != 0: the geometry geo_compiled(GS) compiled in (the host launches it
 // when the batch's geometry equals it word for word): its offsets become
