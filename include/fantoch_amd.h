@@ -263,7 +263,9 @@ typedef struct fx_pred_batch {
                                  conflicting command: up to FX_PRED_MAX_DEPS), or
                                  NULL = FX_HDR_ND (dmax <= 31) */
 } fx_pred_batch;
-/* Table tiers: SMALL = LDS, 64 pending (many wavefronts per CU); LDS = LDS,
+/* Table tiers: SMALL = LDS, 64 pending (many wavefronts per CU; at n = 5 and
+ * dmax = 5 also 32 dot-index slots per source, 256-seq clock windows and a
+ * 32-deep recursion, so such streams reach FX_ERR_CAPACITY sooner); LDS = LDS,
  * the most of 512 / 256 / 128 pending that fit (FX_ERR_UNSUPPORTED if none
  * does); HBM = tables in `state` (fx_pred_state_bytes), 8192 pending. */
 #define FX_PRED_TIER_SMALL 0u
