@@ -1690,19 +1690,23 @@ struct Sim : GP {
 // lets 16 instances share a CU (the default configs[1] geometry: 10.0 KB at
 // n = 5 — 4 waves issue more of the scalar unit's slots than 3 even with a few
 // spilled registers, +14 %), 3 otherwise, 2 for the 256-slot dot tables
-template <uint32_t HM, uint32_t DS, uint32_t WPS, uint32_t NX, class GP = GeoRT>
-__global__ __launch_bounds__(64, WPS) void k_sim(SimArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  const uint32_t inst = blockIdx.x;
-  if (inst >= a.instances) return;
+// WPB: instances per workgroup (a CU holds at most 16 workgroups; each
+// instance's wavefront works on its own LDS block, no workgroup barrier)
+template <uint32_t HM, uint32_t DS, uint32_t WPS, uint32_t NX, class GP = GeoRT, uint32_t WPB = 1>
+__global__ __launch_bounds__(64 * WPB, WPS) void k_sim(SimArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem_all[];
+  const uint32_t wv = WPB > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
+  const uint32_t inst = blockIdx.x * WPB + wv;
+  if (inst >= a.instances) return;  // whole wavefront
   Sim<HM, DS, NX, GP> s;
 #pragma unroll
   for (uint32_t k = 0; k < DS; ++k) s.sdv[k] = 0;
-  s.lid = threadIdx.x;
+  s.lid = threadIdx.x & 63u;
   s.trace = ((uint64_t)vdiv(0) << 32) | vdiv(0);
   s.deps_total = s.trace;
   s.lat_sum = s.trace;
   if constexpr (!GP::fixed) s.g = a.g;
+  uint32_t* smem = smem_all + wv * s.g.words;  // this instance's block (g.words per instance)
   s.lds = smem;
   const fx_sim_spec& sp = a.specs[inst];
   s.protocol = GP::fixed ? GP::proto : sp.protocol;
@@ -2025,7 +2029,7 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
     (void)hipFuncSetAttribute((const void*)sim::k_sim<2, 4, 2, NMAX>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 4, XNX, GeoC1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
-    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 5, XNX, GeoC1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 5, XNX, GeoC1, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
     (void)hipFuncSetAttribute((const void*)sim::k_sim<1, 1, 5, 1, GeoC2a>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);
@@ -2055,7 +2059,9 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   const bool five = false;
 #endif
   if (fixed_ok && one_f && five && geo_is<GeoC1>(a.g, s0)) {
-    hipLaunchKernelGGL((sim::k_sim<1, 1, 5, XNX, GeoC1>), grid, block, lds, hs, a);
+    // two instances per workgroup: 20 per CU (a CU holds at most 16 workgroups)
+    hipLaunchKernelGGL((sim::k_sim<1, 1, 5, XNX, GeoC1, 2>), dim3((b->instances + 1) / 2), dim3(128), lds * 2, hs,
+                       a);
   } else if (fixed_ok && five && geo_is<GeoC2a>(a.g, s0)) {
     hipLaunchKernelGGL((sim::k_sim<1, 1, 5, 1, GeoC2a>), grid, block, lds, hs, a);
   } else if (fixed_ok && one_f && four && geo_is<GeoC1>(a.g, s0)) {
