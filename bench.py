@@ -102,7 +102,7 @@ MODE_DEFAULTS = {
     # instance; k_simx's configs[3] build runs 5 waves per SIMD, two
     # instances per workgroup: 20 per CU x 256 CUs = 5,120, one round (3 waves
     # per SIMD and 3,072 instances: 117 M; 4 and 4,096: 139 M; 5 and 5,120:
-    # 144 M, tools/r5_occ2.sh, tools/r5_x5.sh)
+    # 144 M, profiles/archive/calls/r5_occ2.sh, profiles/archive/calls/r5_x5.sh)
     "dense-sim": dict(seeds=5120, conflicts="100", protocol="both", f=2),
     # configs[3] on the batched executor: 3,072 instances = 15,360 streams,
     # one wavefront each, 5 per CU (LDS tables): 12 rounds, so the last

@@ -55,6 +55,13 @@ def attach(roof, pm, alg_bytes_per_launch):
             roof["traffic_" + k] = pm[k]
     if pm.get("issue"):
         roof["issue"] = dict(pm["issue"], source="profiles/pmc_%s.json (%s)" % (pm.get("mode"), pm.get("source")))
+    # north_star's rocprof figures beside achieved GB/s: LDS bank conflicts
+    # (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE) and wave occupancy
+    # (SQ_WAVE_CYCLES per CU cycle), from the same counter record
+    if pm.get("lds_bank_conflict_frac") is not None:
+        roof["lds_bank_conflict_frac"] = pm["lds_bank_conflict_frac"]
+    if (pm.get("issue") or {}).get("mean_waves_per_cu") is not None:
+        roof["mean_waves_per_cu"] = pm["issue"]["mean_waves_per_cu"]
     if pm.get("kernel_pattern"):
         roof["pmc_kernel"] = pm["kernel_pattern"]
     return roof

@@ -36,6 +36,7 @@ FX_PROTOCOL_BASIC = 2
 FX_SIM_FLAG_EXEC_NOTIFICATIONS = 1
 FX_SIM_FLAG_LARGE = 2
 FX_SIM_FLAG_GENERIC = 4
+FX_SIM_FLAG_ARENA_FILL = 8
 FX_SIM_STAT_FAST, FX_SIM_STAT_SLOW, FX_SIM_STAT_STABLE = 0, 8, 16
 FX_SIM_STAT_EVENTS, FX_SIM_STAT_END_MS, FX_SIM_STAT_TRACE, FX_SIM_STAT_SEQ = 24, 25, 26, 27
 FX_SIM_STAT_DEPS = 28
@@ -274,6 +275,7 @@ SIGNATURES = [
     ("fx_graph_executor_parallel", ctypes.c_int, []),
     ("fx_graph_executor_transfer_stats", ctypes.c_int, [ctypes.c_void_p, u64p, u64p]),
     ("fx_graph_executor_persist_stats", ctypes.c_int, [ctypes.c_void_p, u64p, ctypes.c_uint32]),
+    ("fx_graph_executor_debug_hooks", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]),
     ("fx_sim_plan", ctypes.c_int,
      [ctypes.POINTER(SimSpec), ctypes.c_uint32, ctypes.c_uint32, u32p]),
     ("fx_sim_plan_large", ctypes.c_int,

@@ -209,6 +209,7 @@ struct fx_graph_executor {
     // kernel's compute / fence ticks, polls and poll round trips (100 MHz)
     uint64_t stats[FX_PERSIST_STATS] = {};  // + host prep / convert (ns), compute shader cycles, flush total / post-wait reads / pre-publish (ns)
     bool want_stats = false;  // FX_HANDLE_STATS=1: the kernel's fence / poll / cycle words too
+    uint32_t debug_skip_status = 0, debug_hold_ticks = 0;  // test hooks (fx_graph_executor_debug_hooks)
   } ps;
   bool persist_ok = true;
 };
@@ -374,8 +375,14 @@ struct Wait {
 };
 
 // The end of a failed wait: ask the kernel to stop and give its stream one
-// more deadline to drain.  A stream that drains is reusable; one that does not
-// is abandoned (never synchronised again, never pooled).
+// more deadline to drain.  A stream that drains is reusable: an expired wait
+// (a slow but healthy kernel, e.g. queued behind other work) then returns
+// FX_ERR_CAPACITY, and flush() moves the log to the batch tiers as it does
+// for a capacity escalation (the executor state the kernel saved is not
+// needed: the batch tiers rerun the log from its start).  A stream error, or a
+// kernel that did not stop, is sticky; such a stream is abandoned (never
+// synchronised again, never pooled, and the handle's buffers are leaked when
+// it is freed: the kernel may still write them).
 int persist_abort(fx_graph_executor* ex, int st, const char* where, uint32_t hi) {
   auto& P = ex->ps;
   std::fprintf(stderr, "fantoch_amd persistent handle: %s while waiting for the %s (rows %u, consumed %u)\n",
@@ -397,6 +404,7 @@ int persist_abort(fx_graph_executor* ex, int st, const char* where, uint32_t hi)
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
   ex->persist_ok = false;
+  if (st == FX_ERR_TIMEOUT && !P.dead) return FX_ERR_CAPACITY;
   return ex->sticky = st;
 }
 
@@ -412,7 +420,10 @@ int persist_stop(fx_graph_executor* ex) {
     const hipError_t q = hipStreamQuery(ex->ps.stream);
     if (q == hipSuccess) break;
     if (q != hipErrorNotReady) return persist_abort(ex, FX_ERR_HIP, "stop", ex->ps.pub);
-    if (std::chrono::steady_clock::now() > w.end) return persist_abort(ex, FX_ERR_TIMEOUT, "stop", ex->ps.pub);
+    if (std::chrono::steady_clock::now() > w.end) {
+      const int r = persist_abort(ex, FX_ERR_TIMEOUT, "stop", ex->ps.pub);
+      return r == FX_ERR_CAPACITY ? FX_OK : r;  // drained on the second deadline: stopped
+    }
     if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
   ex->ps.launched = false;
@@ -432,10 +443,8 @@ int persist_launch_now(fx_graph_executor* ex, bool init) {
   a.at_commit = ex->cfg.execute_at_commit ? 1u : 0u;
   a.init = init ? 1u : 0u;
   a.done0 = pctl(ex)[fx::PERSIST_DONE];
-  {
-    const char* e = std::getenv("FX_HANDLE_DEBUG_SKIP_STATUS");
-    a.debug_skip_status = e ? (uint32_t)std::atol(e) : 0u;
-  }
+  a.debug_skip_status = ex->ps.debug_skip_status;
+  a.debug_hold_ticks = ex->ps.debug_hold_ticks;
   pctl(ex)[fx::PERSIST_RUN] = 1u;  // the kernel clears it when it exits
   std::atomic_thread_fence(std::memory_order_seq_cst);
   if (fx::persist_launch(a, ex->ps.stream) != FX_OK) return FX_ERR_HIP;
@@ -918,6 +927,15 @@ fx_graph_executor* fx_graph_executor_new(uint8_t process_id, uint64_t shard_id, 
 void fx_graph_executor_free(fx_graph_executor* ex) {
   if (!ex) return;
   const bool stopped = persist_stop(ex) == FX_OK;
+  if (ex->ps.dead) {
+    // the persistent kernel never answered the stop request: it may still
+    // read and write the handle's mapped words, rings and state block, and a
+    // free or stream destroy would wait for it (or free memory under it).
+    // The whole handle is leaked on purpose: no HIP call touches it again.
+    std::fprintf(stderr, "fantoch_amd persistent handle: freed while its kernel is unresponsive; "
+                         "its buffers and streams are leaked\n");
+    return;
+  }
   if (ex->ps.stream) {
     bool pooled = false;
     if (stopped && ex->ps.ctl.p) {  // the kernel has exited: the resources go back to the pool
@@ -933,9 +951,7 @@ void fx_graph_executor_free(fx_graph_executor* ex) {
         pooled = true;
       }
     }
-    // an abandoned stream (its kernel never answered the stop request) is
-    // leaked: destroying it would wait for the kernel
-    if (!pooled && !ex->ps.dead) (void)hipStreamDestroy(ex->ps.stream);
+    if (!pooled) (void)hipStreamDestroy(ex->ps.stream);
   }
   hipStream_t s = ex->stream;
   delete ex;  // DevBufs free first
@@ -1245,6 +1261,13 @@ int fx_graph_executor_parallel(void) { return 1; }
 int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out, uint32_t n) {
   if (!ex || (!out && n)) return FX_ERR_INVALID_ARG;
   for (uint32_t i = 0; i < n && i < FX_PERSIST_STATS; ++i) out[i] = ex->ps.stats[i];
+  return FX_OK;
+}
+
+int fx_graph_executor_debug_hooks(fx_graph_executor* ex, uint32_t skip_status_flush, uint32_t hold_ms) {
+  if (!ex || hold_ms > 10000u) return FX_ERR_INVALID_ARG;
+  ex->ps.debug_skip_status = skip_status_flush;
+  ex->ps.debug_hold_ticks = hold_ms * 100000u;  // s_memrealtime: 100 MHz
   return FX_OK;
 }
 

@@ -104,9 +104,13 @@ struct PersistArgs {
   uint32_t* state;      // device: the wave tier's saved state of one stream
   uint32_t row_slots, out_slots;  // powers of two
   uint32_t n, at_commit, init, done0;
-  // test hook (FX_HANDLE_DEBUG_SKIP_STATUS=k): the k-th flush of this launch
-  // publishes no status, so the host's bounded wait must expire (0 = never)
+  // test hooks (fx_graph_executor_debug_hooks; 0 = off): the k-th flush of
+  // this launch publishes no status, so the host's bounded wait must expire;
+  // the kernel ignores the stop request and the idle exit until it has been
+  // idle this many 100 MHz ticks (bounded: it still exits by itself), so the
+  // host's stop request goes unanswered
   uint32_t debug_skip_status;
+  uint32_t debug_hold_ticks;
 };
 constexpr uint32_t PERSIST_ROW_WORDS = 16;  // dot, hdr, 14 deps
 constexpr uint32_t PERSIST_CTL_WORDS = 64;

@@ -183,7 +183,6 @@ struct ArgsX {
   const uint8_t* rank;
   uint32_t RP;
   uint32_t exec_cap, lat_cap, max_events, sim_exec_notif;
-  uint32_t row_prefetch;  // LX search: prefetch the first deps' rows (vmax <= 15; FX_SIMX_PF=0 turns it off)
   uint32_t* executed;
   uint32_t* executed_len;
   uint32_t* latency_log;
@@ -267,15 +266,7 @@ enum : uint32_t { PF_POP = 0, PF_EVENT = 1, PF_XADD = 2, PF_FIND = 3, PF_CHECK =
                   PC_EVENTS = 22, PC_SEND = 23, PC_CACHE = 11 };
 
 // NG: registers of group minima per lane (message pool <= 4096 NG entries)
-// LX: the Tarjan state of a search in LDS (a u16 id word per dot slot,
-// search-epoch tagged, and the Tarjan stack as u16 slots) instead of the
-// per-(slot, process) HBM records: no HBM store per DFS recursion and no HBM
-// round trip to resume a frame (tarjan.rs:96-316 needs a dep's state only as
-// "unvisited / on the stack (id) / assigned to an SCC", and within one search
-// a visited vertex that is not executed is on the stack).  For slot tables of
-// fewer than 4,096 dots and <= 32 deps per vertex (configs[3]: 2,560 slots,
-// 10 KB of LDS per instance).
-template <uint32_t NG, bool LX = false>
+template <uint32_t NG>
 struct Big {
   // ---------------------------------------------------------------- context
   uint32_t lid;
@@ -283,9 +274,6 @@ struct Big {
   GeoX g;
   uint32_t* M;    // this instance's arena
   uint32_t* lds;  // histogram caches
-  uint16_t* ltl;   // LX: Tarjan word per slot: id (12) | assigned to an SCC << 12 | search epoch (3) << 13
-  uint16_t* lstk;  // LX: Tarjan stack (slots)
-  uint32_t tep = 7;  // LX: the search epoch (1..7; the table is cleared when it wraps to 1)
   uint32_t inst;
   uint32_t protocol, n, f, synod_f;
   // the instance's other workload parameters are read from its spec where
@@ -313,9 +301,27 @@ struct Big {
   }
   // FX_ERR_SIM_LATE with its source line in the stats row (as capacity failures)
   __device__ __forceinline__ void fail_late(uint32_t line) {
+#ifdef FX_SIMX_DIAG
+    if (!err) {
+      dput(0, line | (0xD1A6ull << 32));
+      dput(1, now | ((uint64_t)(uint32_t)events << 32));
+      dput(2, seq | ((uint64_t)nfree << 32));
+      dput(3, xp | (rtop << 8) | (nfrm << 16) | ((uint64_t)cur_info << 32));
+      dput(4, cur_arg | ((uint64_t)cur_hi << 32));
+    }
+#endif
     if (!err) err_site = line;
     err = FX_ERR_SIM_LATE;
   }
+#ifdef FX_SIMX_DIAG
+  // diagnostics build (make fvariant V=diag F=sim_big D=-DFX_SIMX_DIAG,
+  // tools/simx_diag.py): the first failure's state goes to stats slots 0..23
+  // of the instance (the protocol counters are not written in this build)
+  uint32_t cur_info = 0, cur_arg = 0, cur_hi = 0;
+  __device__ __forceinline__ void dput(uint32_t i, uint64_t v) {
+    if (lid == 0 && kx()->stats) kx()->stats[(size_t)inst * FX_SIM_STATS + i] = v;
+  }
+#endif
   uint32_t now = 0;  // ms
   uint32_t seq = 0;  // insertion counter (C3)
   uint64_t rdraws = 0;
@@ -531,6 +537,9 @@ struct Big {
     const uint32_t vi = W(g.o_inf, e0), va = W(g.o_arg, e0);
     const uint64_t hit = bal(kh == th && kl == tl);
     if (!hit) {  // the group's minimum is not among its leaves: a broken event tree
+#ifdef FX_SIMX_DIAG
+      if (!err) diag_tree(th, tl, grp, ln, bk, kh, kl);
+#endif
       fail_late(__LINE__);
       hi_out = NONE;
       return NONE;
@@ -556,6 +565,69 @@ struct Big {
     return grp * 64u + j;
   }
   __device__ __forceinline__ void free_event(uint32_t e) { put(W(g.o_free, nfree++), e); }
+#ifdef FX_SIMX_DIAG
+  // the broken group, its leaves, and every group whose lane minimum differs
+  // from the minimum of its leaves
+  __device__ void diag_tree(uint32_t th, uint32_t tl, uint32_t grp, uint32_t ln, uint32_t bk, uint32_t kh,
+                            uint32_t kl) {
+    dput(8, th | ((uint64_t)tl << 32));
+    dput(9, grp | ((uint64_t)ln << 16) | ((uint64_t)rl(bk, ln) << 32));
+    const uint32_t nh = dpp_min(kh), nl = dpp_min(kh == nh ? kl : NONE);
+    dput(10, nh | ((uint64_t)nl << 32));
+    dput(11, pop64(bal(kh == NONE)) | ((uint64_t)pop64(bal(kh == th)) << 8) | ((uint64_t)pop64(bal(kl == tl)) << 16));
+    uint32_t bad = 0, first = NONE, fh = 0, fl = 0, ah = 0, al = 0;
+    const uint32_t ngr = g.R >> 6;
+    for (uint32_t g2 = 0; g2 < ngr; ++g2) {
+      const uint32_t h2 = W(g.o_kh, g2 * 64u + lid), l2 = W(g.o_kl, g2 * 64u + lid);
+      const uint32_t mh = dpp_min(h2), ml = dpp_min(h2 == mh ? l2 : NONE);
+      uint32_t sh = NONE, slo = NONE;
+#pragma unroll
+      for (uint32_t k = 0; k < NG; ++k)
+        if ((g2 >> 6) == k) {
+          sh = rl(gh[k], g2 & 63u);
+          slo = rl(gl[k], g2 & 63u);
+        }
+      if (sh != mh || slo != ml) {
+        if (!bad) {
+          first = g2;
+          fh = sh;
+          fl = slo;
+          ah = mh;
+          al = ml;
+        }
+        ++bad;
+      }
+    }
+    dput(12, bad | ((uint64_t)first << 32));
+    dput(13, fh | ((uint64_t)fl << 32));
+    dput(14, ah | ((uint64_t)al << 32));
+    // lanes of the group-minimum registers beyond the pool's groups must hold NONE
+    uint32_t junk = 0, jv = 0, jl = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < NG; ++k) {
+      const bool off = k * 64u + lid >= ngr;
+      const uint64_t m = bal(off && (gh[k] != NONE || gl[k] != NONE));
+      if (m && !junk) {
+        jl = k * 64u + ctz64(m);
+        jv = rl(gh[k], ctz64(m));
+      }
+      junk += pop64(m);
+    }
+    dput(15, junk | ((uint64_t)jl << 16) | ((uint64_t)jv << 32));
+  }
+  // a message for a dot whose slot no longer holds it
+  __device__ void diag_slot(uint32_t d, uint32_t p) {
+    dput(8, d | ((uint64_t)p << 32));
+    const uint32_t sl = src_ok(d) ? hslot(d) : NONE;
+    dput(9, sl | ((uint64_t)rl(pa, A_SEQ + ((FX_DOT_SRC(d) - 1u) & 7u)) << 32));
+    if (sl != NONE) {
+      dput(10, S(sl, SL_DOT) | ((uint64_t)S(sl, SL_MASKS) << 32));
+      dput(11, S(sl, SL_CNT) | ((uint64_t)S(sl, SL_CLIENT) << 32));
+      dput(12, RC(sl, p, R_PST) | ((uint64_t)RC(sl, p, R_WAIT) << 32));
+      dput(13, rl(hrow, SL_DOT) | ((uint64_t)hsl << 32));
+    }
+  }
+#endif
 
   // Runner::schedule_message (runner.rs:507-530): distance, times the C6
   // multiplier in [0, 10) when reordering (one draw per message, in schedule order)
@@ -703,6 +775,9 @@ struct Big {
   __device__ __forceinline__ void h_mstore(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
+#ifdef FX_SIMX_DIAG
+      if (!err) diag_slot(dot, p);
+#endif
       fail_late(__LINE__);
       return;
     }
@@ -715,6 +790,9 @@ struct Big {
   __device__ __forceinline__ void h_mstoreack(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
+#ifdef FX_SIMX_DIAG
+      if (!err) diag_slot(dot, p);
+#endif
       fail_late(__LINE__);
       return;
     }
@@ -730,6 +808,9 @@ struct Big {
   __device__ __forceinline__ void h_bcommit(uint32_t p, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
+#ifdef FX_SIMX_DIAG
+      if (!err) diag_slot(dot, p);
+#endif
       fail_late(__LINE__);
       return;
     }
@@ -757,6 +838,9 @@ struct Big {
   __device__ __forceinline__ void h_mcollect(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
+#ifdef FX_SIMX_DIAG
+      if (!err) diag_slot(dot, p);
+#endif
       fail_late(__LINE__);
       return;
     }
@@ -799,6 +883,9 @@ struct Big {
   __device__ __forceinline__ void h_mcollectack(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
+#ifdef FX_SIMX_DIAG
+      if (!err) diag_slot(dot, p);
+#endif
       fail_late(__LINE__);
       return;
     }
@@ -876,6 +963,9 @@ struct Big {
   __device__ __forceinline__ void h_mcommit(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
+#ifdef FX_SIMX_DIAG
+      if (!err) diag_slot(dot, p);
+#endif
       fail_late(__LINE__);
       return;
     }
@@ -896,6 +986,9 @@ struct Big {
   __device__ __forceinline__ void h_mconsensus(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
+#ifdef FX_SIMX_DIAG
+      if (!err) diag_slot(dot, p);
+#endif
       fail_late(__LINE__);
       return;
     }
@@ -912,6 +1005,9 @@ struct Big {
   __device__ __forceinline__ void h_mconsensusack(uint32_t p, uint32_t from, uint32_t dot) {
     const uint32_t sl = hslot_of(dot, p);
     if (sl == NONE) {
+#ifdef FX_SIMX_DIAG
+      if (!err) diag_slot(dot, p);
+#endif
       fail_late(__LINE__);
       return;
     }
@@ -1163,9 +1259,7 @@ struct Big {
   __device__ __forceinline__ uint32_t find_scc(uint32_t rsl, uint32_t* missing, uint32_t mark_epoch, bool* saved) {
     XPROF_T0();
     XPROF_CNT(PC_FIND, 1);
-    uint32_t r;
-    if constexpr (LX) r = find_scc_lx_(rsl, missing, mark_epoch, saved);
-    else r = find_scc_(rsl, missing, mark_epoch, saved);
+    const uint32_t r = find_scc_(rsl, missing, mark_epoch, saved);
     XPROF_ADD(PF_FIND);
     return r;
   }
@@ -1258,6 +1352,26 @@ struct Big {
           broken = broken || bal((psx & (PS_INGRAPH | PS_EXEC)) != PS_INGRAPH);
         }
         if (broken) {
+#ifdef FX_SIMX_DIAG
+          if (!err) {
+            dput(8, rsl | ((uint64_t)tsp << 32));
+            dput(9, ctp | ((uint64_t)cv << 32));
+            for (uint32_t i0 = ctp; i0 < tsp; i0 += 64) {
+              const uint32_t i = i0 + lid;
+              const uint32_t x = i < tsp ? W(g.o_tstk, i) : 0u;
+              const uint32_t psx = i < tsp ? RC(x, p, R_PST) : PS_INGRAPH;
+              const uint64_t m = bal((psx & (PS_INGRAPH | PS_EXEC)) != PS_INGRAPH);
+              if (m) {
+                const uint32_t j = ctz64(m), xj = rl(x, j);
+                dput(10, xj | ((uint64_t)rl(psx, j) << 32));
+                dput(11, S(xj, SL_DOT) | ((uint64_t)S(xj, SL_MASKS) << 32));
+                dput(12, RC(xj, p, R_TL) | ((uint64_t)RC(xj, p, R_MARK) << 32));
+                dput(13, (i0 + j) | ((uint64_t)pop64(m) << 32));
+                break;
+              }
+            }
+          }
+#endif
           fail_late(__LINE__);
           break;
         }
@@ -1297,268 +1411,6 @@ struct Big {
         if (markit) RC(x, p, R_MARK) = (RC(x, p, R_MARK) & 1u) | (mark_epoch << 1);
       }
     }
-    tsp = 0;
-    return result;
-  }
-
-  // ====================================================== LX search
-  static constexpr uint32_t LT_ID = 0xFFFu, LT_SCC = 0x1000u;
-  __device__ __forceinline__ uint32_t lt_get(uint32_t sl) { return uni(ltl[sl]); }
-  __device__ __forceinline__ void lt_set(uint32_t sl, uint32_t v) { ltl[sl] = (uint16_t)v; }  // every lane, same word
-  // the id of a vertex visited by this search (0: not visited)
-  __device__ __forceinline__ uint32_t lt_id(uint32_t e) const { return (e >> 13) == tep ? e & LT_ID : 0u; }
-
-  // the static state of a frame's deps (lanes [0, cnd)): a dep that is the
-  // vertex itself, of a freed slot or executed at xp is skipped (tarjan.rs:
-  // 128-145); one not in xp's graph is missing (148-157); the others are
-  // pending.  None of these change during the search (no vertex is added, and
-  // an SCC member executes only through the search, which the LDS word
-  // records), so a resumed frame needs no reload.  Returns the pending mask;
-  // *jm = the first missing dep (the search stops there), 63 if none.
-  // With pf (vmax <= 15), the same round trip prefetches the dep rows of the
-  // frame's first four deps (lanes 16 g + w: value word w of dep g, lane
-  // 16 g + 15 its count word; the words share the cache lines of the tags
-  // read anyway), so descending into one of them needs no row load.
-  __device__ __forceinline__ uint32_t dep_status(uint32_t drow, uint32_t cnd, uint32_t cdot, uint32_t& jm, bool pf,
-                                                 uint32_t& prow) {
-    uint32_t tag = 0, ps = 0;
-    const bool live = lid < cnd && drow != cdot && src_ok(drow);
-    XPROF_T0();
-    const uint32_t grp = lid >> 4, w = lid & 15u;
-    const uint32_t dg = gather(drow, grp);
-    prow = 0;
-    if (pf && grp < cnd && dg != cdot && src_ok(dg)) prow = S(hslot(dg), w == 15u ? SL_CNT : g.sl_value + w);
-    if (live) {
-      const uint32_t sl = hslot(drow);
-      tag = S(sl, SL_DOT);
-      ps = RC(sl, xp, R_PST);
-    }
-    const bool act = live && tag == drow && !(ps & PS_EXEC);
-    const uint64_t miss = bal(act && !(ps & PS_INGRAPH));
-    jm = miss ? ctz64(miss) : 63u;
-    const uint32_t pmask = (uint32_t)bal(act && (ps & PS_INGRAPH));
-    XPROF_ADD(PF_DEPST);
-    return pmask;
-  }
-
-  // save_scc for the LX search: the members lstk[base, base + cnt) (their LDS
-  // words already say "assigned"); ranks by dot computed lane-parallel and,
-  // for up to 64 members, permuted across lanes with no memory round trip;
-  // the executed-clock bit of each member is set here (tarjan.rs:293).
-  __device__ __forceinline__ void save_scc_lx(uint32_t base, uint32_t cnt) {
-    hist_chain(cnt);
-    ++xe;  // the graph lost vertices: every cached search result of xp is stale
-    if (nwl + cnt > 2u * g.NS) {
-      fail_cap(__LINE__);
-      return;
-    }
-    const uint32_t p = xp;
-    // member slots and dots in lanes (chunks of 64), ranked by dot
-    const bool direct = cnt <= 64u;
-    uint32_t sorted = 0;
-    {
-    XPROF_T0();
-    for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
-      const uint32_t i = i0 + lid;
-      const uint32_t msl = i < cnt ? (uint32_t)lstk[base + i] : 0u;
-      const uint32_t md = i < cnt ? S(msl, SL_DOT) : NONE;
-      uint32_t rank = 0;
-      for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
-        const uint32_t k = k0 + lid;
-        const uint32_t kd = k0 == i0 ? md : (k < cnt ? S((uint32_t)lstk[base + k], SL_DOT) : NONE);
-        const uint32_t m = min(64u, cnt - k0);
-        for (uint32_t j = 0; j < m; ++j) rank += rl(kd, j) < md ? 1u : 0u;
-      }
-      if (direct) {
-        // lane rank <- member i (ds_permute: a forward permutation)
-        const int addr = (int)((i < cnt ? rank : 63u) << 2);
-        sorted = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)msl);
-        // the permuted dots must ascend over lanes [0, cnt) (every lane written once)
-        const uint32_t sd = (uint32_t)__builtin_amdgcn_ds_permute(addr, (int)md);
-        const uint32_t pd = gather(sd, (lid - 1u) & 63u);
-        if (bal(lid < cnt && ((lid > 0 && sd <= pd) || sd == 0u || sd == NONE))) {
-          fail_late(__LINE__);
-          return;
-        }
-      } else if (i < cnt) {
-        W(g.o_tl, rank) = msl;
-      }
-    }
-    XPROF_ADD(PF_SORT);
-    }
-    XPROF_T0();
-    for (uint32_t r0 = 0; r0 < cnt && !err; r0 += 64) {
-      const uint32_t r = r0 + lid;
-      const bool act = r < cnt;
-      uint32_t sl = 0, d = 0, st = 0, wt = 0, c = 0, cw = 0, mk = 0, ps = 0;
-      if (act) {
-        sl = direct ? sorted : W(g.o_tl, r);
-        d = S(sl, SL_DOT);
-        st = RC(sl, p, R_START);
-        wt = RC(sl, p, R_WAIT);
-        ps = RC(sl, p, R_PST);
-        c = S(sl, SL_CLIENT);
-        cw = S(sl, SL_CNT);
-        mk = S(sl, SL_MASKS);
-      }
-      const uint32_t cpr = act ? CL(c, 0) : 0u;
-      const uint32_t m = min(64u, cnt - r0);
-      // an SCC member must be in xp's graph and not executed yet (the
-      // reference's expects, tarjan.rs:245-255): anything else is a broken table
-      if (bal(act && ((ps & (PS_INGRAPH | PS_EXEC)) != PS_INGRAPH || d == 0u))) {
-        fail_late(__LINE__);
-        return;
-      }
-      if (act) {
-        RC(sl, p, R_PST) = ps | PS_EXEC;  // executed_clock.add (tarjan.rs:293)
-        if (kx()->executed && xk + lid < kx()->exec_cap) kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + xk + lid] = d;
-        W(g.o_wl, nwl + lid) = sl;
-        if (kx()->delay_hist) {  // ExecutionDelay (graph/mod.rs:514-518)
-          const uint32_t bn = min(now - st, kx()->delay_bins - 1u);
-          if (bn < HD_BINS) atomicAdd(&lds[HC_BINS + bn], 1u);
-          else atomicAdd(&kx()->delay_hist[bn], 1ull);
-        }
-        if (((mk >> 24) & 0xFFu) + 1u == n) S(sl, SL_DOT) = 0u;  // executed everywhere: free the slot
-        else S(sl, SL_MASKS) = mk + (1u << 24);
-      }
-      xk += m;
-      nwl += m;
-      const uint64_t need = bal(act && (wt != 0 || (cpr & 0xFFu) == p));
-      for (uint64_t mm = need; mm && !err; mm &= mm - 1) {
-        const uint32_t j = ctz64(mm);
-        if (rl(wt, j)) unlink(rl(sl, j));
-        if ((rl(cpr, j) & 0xFFu) == p) client_result(rl(c, j), (rl(cw, j) >> 16) & 3u);
-      }
-    }
-    XPROF_ADD(PF_EMIT);
-  }
-
-  // find_scc + strong_connect + finalize (as find_scc_) over the LDS state.
-  // Frames 0..63 in lanes: slot | next dep << 24; stack position | low << 12 |
-  // first missing dep << 24; the pending-deps mask.  Deeper frames in
-  // W(o_fv / o_fi / o_fp).
-  __device__ __forceinline__ uint32_t find_scc_lx_(uint32_t rsl, uint32_t* missing, uint32_t mark_epoch, bool* saved) {
-    const uint32_t p = xp;
-    *saved = false;
-    tep = tep == 7u ? 1u : tep + 1u;
-    if (tep == 1u) {  // the epoch wrapped: no word of an older search may match
-      uint32_t* w = reinterpret_cast<uint32_t*>(ltl);
-      for (uint32_t i = lid; i < g.NS / 2u; i += 64) w[i] = 0u;
-    }
-    const uint32_t te = tep << 13;
-    idc = 1;
-    tsp = 0;
-    uint32_t frs = 0, frt = 0, frp = 0;
-    lt_set(rsl, 1u | te);
-    lstk[tsp++] = (uint16_t)rsl;
-    fsp = 1;
-    uint32_t cv = rsl, ci = 0, cid = 1, clow = 1, ctp = 0, cdot = 0, cnd = 0, drow = 0, jm = 63u;
-    frame_row(rsl, cdot, cnd, drow);
-    const bool pf = kx()->row_prefetch != 0;
-    bool pv = pf;  // prow holds the current frame's first deps' rows
-    uint32_t prow = 0;
-    uint32_t pm = dep_status(drow, cnd, cdot, jm, pf, prow);
-    uint32_t result = FOUND;
-    for (uint32_t guard = 0; fsp && !err; ++guard) {
-      if (guard > 64u * g.NS + 64u) {
-        fail_cap(__LINE__);
-        break;
-      }
-      // the next pending dep before the first missing one
-      const uint32_t lim = min(cnd, jm);
-      const uint32_t rest = ci < 32u ? (pm >> ci) << ci : 0u;
-      const uint32_t nx = rest ? (uint32_t)__builtin_ctz(rest) : 32u;
-      XPROF_CNT(PC_EDGES, 1);
-      if (nx < lim) {
-        ci = nx + 1u;
-        const uint32_t d = rl(drow, nx), sl = hslot(d);
-        const uint32_t lw = lt_get(sl), id = lt_id(lw);
-        if (id == 0) {  // recurse (tarjan.rs:172-214)
-          XPROF_CNT(PC_RECURSE, 1);
-          const uint32_t f = fsp - 1u;
-          const uint32_t fw = cv | (ci << 24), tw = ctp | (clow << 12) | (jm << 24);
-          if (f < 64u) {
-            lset(frs, f, fw);
-            lset(frt, f, tw);
-            lset(frp, f, pm);
-          } else {
-            put(W(g.o_fv, f), fw);
-            put(W(g.o_fi, f), tw);
-            put(W(g.o_fp, f), pm);
-          }
-          ++idc;
-          if (idc > LT_ID || tsp >= g.NS || fsp >= g.NS) {
-            fail_cap(__LINE__);
-            break;
-          }
-          lt_set(sl, idc | te);
-          ctp = tsp;
-          lstk[tsp++] = (uint16_t)sl;
-          ++fsp;
-          cv = sl;
-          ci = 0;
-          cid = idc;
-          clow = idc;
-          if (pv && nx < 4u) {  // the row came with the parent's dep states
-            const uint32_t cw = rl(prow, 16u * nx + 15u);
-            const uint32_t rw = gather(prow, (16u * nx + lid) & 63u);
-            cdot = d;
-            cnd = (cw >> 8) & 0xFFu;
-            drow = lid < cnd ? rw : 0u;
-          } else {
-            frame_row(sl, cdot, cnd, drow);
-          }
-          pm = dep_status(drow, cnd, cdot, jm, pf, prow);
-          pv = pf;
-        } else if (!(lw & LT_SCC)) {  // on the stack (tarjan.rs:215-225)
-          clow = min(clow, id);
-        }
-        continue;
-      }
-      if (jm < cnd && ci <= jm) {  // missing (tarjan.rs:148-157, shard_count == 1)
-        *missing = rl(drow, jm);
-        result = MISSING;
-        break;
-      }
-      // cv finished
-      const uint32_t lowv = clow;
-      if (cid == lowv) {  // SCC root: the members lstk[ctp, tsp) (tarjan.rs:233-312)
-        for (uint32_t i = ctp + lid; i < tsp; i += 64) {
-          const uint32_t x = lstk[i];
-          ltl[x] = (uint16_t)(ltl[x] | LT_SCC);
-        }
-        save_scc_lx(ctp, tsp - ctp);
-        tsp = ctp;
-        *saved = true;
-        if (err) break;
-      }
-      --fsp;
-      if (fsp) {  // resume the parent frame (tarjan.rs:211: low = min(low, dep low))
-        const uint32_t f = fsp - 1u;
-        uint32_t fw, tw;
-        if (f < 64u) {
-          fw = rl(frs, f);
-          tw = rl(frt, f);
-          pm = rl(frp, f);
-        } else {
-          fw = rd(W(g.o_fv, f));
-          tw = rd(W(g.o_fi, f));
-          pm = rd(W(g.o_fp, f));
-        }
-        cv = fw & 0xFFFFFFu;
-        ci = fw >> 24;
-        ctp = tw & 0xFFFu;
-        jm = tw >> 24;
-        clow = min((tw >> 12) & LT_ID, lowv);
-        cid = lt_id(lt_get(cv));
-        frame_row(cv, cdot, cnd, drow);
-        pv = false;  // (the resumed frame's deps' rows are loaded when descended into)
-      }
-    }
-    // finalize: a failed search marks the vertices left on the stack visited
-    // (try_pending's skip rule); their LDS words lapse with the epoch
-    if (mark_epoch && result == MISSING)
-      for (uint32_t i = lid; i < tsp; i += 64) RC((uint32_t)lstk[i], p, R_MARK) = mark_epoch << 1;
     tsp = 0;
     return result;
   }
@@ -1909,9 +1761,9 @@ struct Big {
 // The build with configs[3]'s geometry compiled in (GS, HBM Tarjan records)
 // holds fewer values in registers: at 4 (128 VGPRs, 52 bytes of spills per
 // lane) 16 instances per CU instead of 12, 117 -> 138 M cmds/s at 4,096
-// instances (tools/r5_occ2.sh); at 5 (102 VGPRs, 136 bytes of spills) with
+// instances (profiles/archive/calls/r5_occ2.sh); at 5 (102 VGPRs, 136 bytes of spills) with
 // two instances per workgroup (a CU holds at most 16 workgroups) 20 per CU,
-// 139.4 -> 144.3 M at 5,120 instances (tools/r5_x5.sh)
+// 139.4 -> 144.3 M at 5,120 instances (profiles/archive/calls/r5_x5.sh)
 #ifndef FX_SIMX_WAVES
 #define FX_SIMX_WAVES 3
 #endif
@@ -1925,17 +1777,15 @@ struct Big {
 // GS != 0: the geometry geo_compiled(GS) compiled in (the host launches it
 // when the batch's geometry equals it word for word): its offsets become
 // immediates instead of scalar registers, of which the kernel is short
-template <uint32_t NG, bool LX, uint32_t GS = 0, uint32_t WPB = 1>
-__global__ __launch_bounds__(64 * WPB, (GS != 0 && !LX) ? FX_SIMX_WAVES_GS : FX_SIMX_WAVES) void k_simx(ArgsX a) {
-  // LDS_WORDS of histogram caches, then (LX) the Tarjan words and stack: u16[NS] each;
-  // WPB > 1 (no LX): WPB instances per workgroup, LDS_WORDS each
+template <uint32_t NG, uint32_t GS = 0, uint32_t WPB = 1>
+__global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVES) void k_simx(ArgsX a) {
+  // LDS_WORDS of histogram caches per instance (WPB instances per workgroup)
   extern __shared__ __attribute__((aligned(16))) uint32_t smem_all[];
-  static_assert(WPB == 1 || !LX, "one LX instance per workgroup");
   const uint32_t wv = WPB > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
   uint32_t* smem = smem_all + wv * LDS_WORDS;
   const uint32_t inst = blockIdx.x * WPB + wv;
   if (inst >= a.instances) return;  // whole wavefront
-  Big<NG, LX> s;
+  Big<NG> s;
   if constexpr (GS != 0) {
     constexpr GeoX gc = geo_compiled(GS);
     static_assert(gc.words != 0, "compiled geometry");
@@ -1943,8 +1793,6 @@ __global__ __launch_bounds__(64 * WPB, (GS != 0 && !LX) ? FX_SIMX_WAVES_GS : FX_
   } else {
     s.g = a.g;
   }
-  s.ltl = reinterpret_cast<uint16_t*>(smem + LDS_WORDS);
-  s.lstk = s.ltl + s.g.NS;
   s.lid = threadIdx.x & 63u;
   s.M = a.arena + (size_t)inst * s.g.words;
   s.lds = smem;
@@ -2084,6 +1932,11 @@ __global__ __launch_bounds__(64 * WPB, (GS != 0 && !LX) ? FX_SIMX_WAVES_GS : FX_
     s.now = t;
     const uint32_t kind = info & 15u, from = (info >> 4) & 15u, to = (info >> 8) & 15u;
     const uint32_t gcv = kind == M_GC && s.lid < n ? M[g.o_gp + e * n + s.lid] : 0u;
+#ifdef FX_SIMX_DIAG
+    s.cur_info = info;
+    s.cur_arg = arg;
+    s.cur_hi = hi;
+#endif
     s.free_event(e);
     s.run_event(kind, from, to, arg, gcv);
 #ifdef FX_SIMX_EVLOG
@@ -2118,7 +1971,11 @@ __global__ __launch_bounds__(64 * WPB, (GS != 0 && !LX) ? FX_SIMX_WAVES_GS : FX_
   if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = o_exec;
   if (a.stats) {
     unsigned long long* st = a.stats + (size_t)inst * FX_SIM_STATS;
+#ifdef FX_SIMX_DIAG
+    if (false) {
+#else
     if (s.lid < NMAX) {
+#endif
       const bool v = s.lid < n;
       st[FX_SIM_STAT_FAST + s.lid] = v ? o_fast : 0u;
       st[FX_SIM_STAT_SLOW + s.lid] = v ? o_slow : 0u;
@@ -2188,40 +2045,18 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
   if (!simx_geometry(b->host_specs[0], b->ring_entries, b->dot_slots, a.g)) return FX_ERR_UNSUPPORTED;
   const size_t bytes = (size_t)a.g.words * 4 * b->instances;
   void* arena = nullptr;
-  // FX_SIMX_ARENA (diagnostics): "fill" fills the arena with 0xA5 bytes
-  // before the launch, "uc" allocates it uncached
-  // "fill-<table>" fills with 0xA5 and then zeroes one table group of every
-  // instance: rec, slot, ev (info / arg / GC payloads), scr (search and
-  // worklist scratch), cl (clients)
-  static const std::string arena_env = [] {
+  // The arena starts zeroed; FX_SIM_FLAG_ARENA_FILL (tests) fills it with
+  // 0xA5 bytes instead: the kernel initialises every word it reads, so both
+  // give the same results (tests/test_poison_all.py).  FX_SIMX_ARENA=pool
+  // (diagnostics) keeps whatever the pool's memory held.
+  static const bool pool_env = [] {
     const char* e = std::getenv("FX_SIMX_ARENA");
-    return std::string(e ? e : "");
+    return e && std::string(e) == "pool";
   }();
-  // default: the arena starts zeroed (a launch must not depend on what an
-  // earlier launch left in the pool's memory: DESIGN.md §3.6); "pool" keeps
-  // the pool's contents (diagnostics)
-  static const int arena_mode = arena_env == "pool" ? 0 : arena_env.rfind("fill", 0) == 0 ? 2
-                              : arena_env == "uc" ? 3 : 1;
-  if (arena_mode == 3) {
-    if (hipExtMallocWithFlags(&arena, bytes, hipDeviceMallocUncached) != hipSuccess) return FX_ERR_HIP;
-  } else if (hipMallocAsync(&arena, bytes, hs) != hipSuccess) {
-    return FX_ERR_HIP;
-  }
-  if (arena_mode == 1 || arena_mode == 2)
-    if (hipMemsetAsync(arena, arena_mode == 1 ? 0 : 0xA5, bytes, hs) != hipSuccess) return FX_ERR_HIP;
-  if (arena_mode == 2 && arena_env.size() > 5) {
-    const std::string grp = arena_env.substr(5);
-    auto zero = [&](uint32_t off, uint32_t end) {
-      (void)hipMemset2DAsync((char*)arena + (size_t)off * 4, (size_t)a.g.words * 4, 0, (size_t)(end - off) * 4,
-                             b->instances, hs);
-    };
-    const GeoX& g = a.g;
-    if (grp == "rec") zero(g.o_rec, g.o_kd);
-    if (grp == "slot") zero(g.o_slot, g.o_rec);
-    if (grp == "ev") { zero(g.o_inf, g.o_arg); zero(g.o_arg, g.o_gp); zero(g.o_gp, g.o_free); }
-    if (grp == "scr") zero(g.o_tstk, g.words);
-    if (grp == "cl") zero(g.o_cl, g.o_kh);
-  }
+  if (hipMallocAsync(&arena, bytes, hs) != hipSuccess) return FX_ERR_HIP;
+  if (!pool_env || (b->flags & FX_SIM_FLAG_ARENA_FILL))
+    if (hipMemsetAsync(arena, (b->flags & FX_SIM_FLAG_ARENA_FILL) ? 0xA5 : 0, bytes, hs) != hipSuccess)
+      return FX_ERR_HIP;
   a.specs = b->specs;
   a.instances = b->instances;
   a.arena = (uint32_t*)arena;
@@ -2245,49 +2080,25 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
   a.stats = (unsigned long long*)o->stats;
   a.err = o->err;
   const dim3 grid(b->instances), block(64);
-  // the LDS Tarjan state (LX) when its ids fit 12 bits and a frame's deps a
-  // 32-bit mask: opt-in (FX_SIMX_LX=1) until an intermittent failure under
-  // register poisoning is explained; the HBM records otherwise
-  static const bool lx_env = [] {
-    const char* e = std::getenv("FX_SIMX_LX");
-    return e && e[0] == '1';
-  }();
-  const bool lx = lx_env && a.g.NS < 4096u && a.g.vmax <= 32u;
-  static const bool pf_env = [] {
-    const char* e = std::getenv("FX_SIMX_PF");
-    return !(e && e[0] == '0');
-  }();
-  a.row_prefetch = pf_env && a.g.vmax <= 15u ? 1u : 0u;
-  const size_t lds = (size_t)(LDS_WORDS + (lx ? a.g.NS : 0u)) * 4u;
-  static const bool gs_env = [] {  // FX_SIMX_GS=0: the generic build only (A/B)
-    const char* e = std::getenv("FX_SIMX_GS");
-    return !(e && e[0] == '0');
-  }();
+  const size_t lds = (size_t)LDS_WORDS * 4u;
+  // configs[3]'s geometry compiled in when the batch's equals it word for word
+  // (FX_SIM_FLAG_GENERIC: the run-time build, for A/B and its parity tests)
   constexpr GeoX gc1 = geo_compiled(1);
-  const bool gs1 = gs_env && std::memcmp(&a.g, &gc1, sizeof(GeoX)) == 0;
+  const bool gs1 = !(b->flags & FX_SIM_FLAG_GENERIC) && std::memcmp(&a.g, &gc1, sizeof(GeoX)) == 0;
   static_assert(gc1.R > 4096 && gc1.R <= 8192, "configs[3] ring: NG = 2");
+  static_assert(FX_SIMX_WPB >= 1, "instances per workgroup");
   if (gs1) {
-    if (lx) hipLaunchKernelGGL((k_simx<2, true, 1>), grid, block, lds, hs, a);
-    else if (FX_SIMX_WPB > 1)
-      hipLaunchKernelGGL((k_simx<2, false, 1, FX_SIMX_WPB>), dim3((b->instances + FX_SIMX_WPB - 1) / FX_SIMX_WPB),
-                         dim3(64 * FX_SIMX_WPB), lds * FX_SIMX_WPB, hs, a);
-    else hipLaunchKernelGGL((k_simx<2, false, 1>), grid, block, lds, hs, a);
-  } else if (lx) {
-    if (a.g.R <= 4096) hipLaunchKernelGGL((k_simx<1, true>), grid, block, lds, hs, a);
-    else if (a.g.R <= 8192) hipLaunchKernelGGL((k_simx<2, true>), grid, block, lds, hs, a);
-    else hipLaunchKernelGGL((k_simx<4, true>), grid, block, lds, hs, a);
+    hipLaunchKernelGGL((k_simx<2, 1, FX_SIMX_WPB>), dim3((b->instances + FX_SIMX_WPB - 1) / FX_SIMX_WPB),
+                       dim3(64 * FX_SIMX_WPB), lds * FX_SIMX_WPB, hs, a);
+  } else if (a.g.R <= 4096) {
+    hipLaunchKernelGGL((k_simx<1>), grid, block, lds, hs, a);
+  } else if (a.g.R <= 8192) {
+    hipLaunchKernelGGL((k_simx<2>), grid, block, lds, hs, a);
   } else {
-    if (a.g.R <= 4096) hipLaunchKernelGGL((k_simx<1, false>), grid, block, lds, hs, a);
-    else if (a.g.R <= 8192) hipLaunchKernelGGL((k_simx<2, false>), grid, block, lds, hs, a);
-    else hipLaunchKernelGGL((k_simx<4, false>), grid, block, lds, hs, a);
+    hipLaunchKernelGGL((k_simx<4>), grid, block, lds, hs, a);
   }
   const hipError_t le = hipGetLastError();
-  if (arena_mode == 3) {
-    (void)hipStreamSynchronize(hs);
-    (void)hipFree(arena);
-  } else {
-    (void)hipFreeAsync(arena, hs);
-  }
+  (void)hipFreeAsync(arena, hs);
   return le == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 

@@ -2053,7 +2053,7 @@ int fx_sim_run(const fx_sim_batch* b, const fx_sim_output* o, void* hip_stream) 
   // single-wave workgroups, so it still runs 4 per SIMD, with more spills
   // (configs[1] 416 vs 418 M cmds/s at 4; two instances per 128-lane
   // workgroup, 20 waves per CU, 399 M — r03f A/B; again in round 5, 408.4 vs
-  // 429.3 M, tools/r5_s5.sh: the scalar unit, not waiting, bounds k_sim)
+  // 429.3 M, profiles/archive/calls/r5_s5.sh: the scalar unit, not waiting, bounds k_sim)
 #ifdef FX_SIM_WPS5
   const bool five = lds <= 160u * 1024u / 20u;
 #else

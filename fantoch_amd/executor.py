@@ -213,6 +213,12 @@ class GraphExecutor:
         check(lib.fx_graph_executor_persist_stats(self._h, out, n))
         return [int(x) for x in out]
 
+    def debug_hooks(self, skip_status_flush=0, hold_ms=0):
+        """fx_graph_executor_debug_hooks (tests only): from the persistent
+        kernel's next launch, skip the status of its k-th flush and/or ignore
+        stop requests until it has been idle hold_ms."""
+        check(_lib.load().fx_graph_executor_debug_hooks(self._h, skip_status_flush, hold_ms))
+
 
 class ExecutorClone:
     """Executor index > 0 of a partial-replication process: GraphExecutionInfo::

@@ -216,11 +216,13 @@ class Result:
 
 def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bins=256,
         delay_bins=8192, ring_entries=0, dot_slots=0, max_events=0, flags=0, stream=None,
-        large=False, generic=False, tiered=True, before_launch=None):
+        large=False, generic=False, tiered=True, before_launch=None, arena_fill=False):
     """Simulates every instance of `specs` on the GPU; returns a Result.
     large=True forces the large-instance kernel (FX_SIM_FLAG_LARGE);
-    generic=True the run-time-geometry build of the all-on-chip kernel even
-    for a compiled-in geometry (FX_SIM_FLAG_GENERIC); tiered=False: one
+    generic=True the run-time-geometry build of either kernel even for a
+    compiled-in geometry (FX_SIM_FLAG_GENERIC); arena_fill=True (tests) the
+    large-instance kernel's arena starts filled with 0xA5 bytes instead of
+    zeroed (FX_SIM_FLAG_ARENA_FILL); tiered=False: one
     fx_sim_run, instances that outgrow the tables keep FX_ERR_SIM_CAPACITY.
     before_launch(stream): called once the inputs and outputs are on the
     device, right before the launch (diagnostics: tools/sim_poison.py)."""
@@ -240,6 +242,8 @@ def run(specs, planet=None, exec_cap=None, lat_cap=None, lat_bins=8192, chain_bi
         flags |= _lib.FX_SIM_FLAG_LARGE
     if generic:
         flags |= _lib.FX_SIM_FLAG_GENERIC
+    if arena_fill:
+        flags |= _lib.FX_SIM_FLAG_ARENA_FILL
     host = (_lib.SimSpec * N)(*specs)
     dspec = DeviceBuffer(ctypes.sizeof(host))
     check(lib.fx_dev_h2d(dspec.ptr, ctypes.addressof(host), ctypes.sizeof(host), stream), "h2d")

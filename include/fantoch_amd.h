@@ -462,6 +462,13 @@ int fx_graph_executor_transfer_stats(const fx_graph_executor* ex, uint64_t* h2d,
  * kernel's words are read only with FX_HANDLE_STATS=1 in the environment. */
 #define FX_PERSIST_STATS 15
 int fx_graph_executor_persist_stats(const fx_graph_executor* ex, uint64_t* out, uint32_t n);
+/* Test hooks of the persistent mode (tests only; 0 = off), taking effect at
+ * the kernel's next launch: skip_status_flush = k makes the k-th flush of a
+ * launch publish no status, so the host's bounded wait expires; hold_ms keeps
+ * the kernel resident, ignoring the stop request and its idle exit, until it
+ * has been idle that long (at most 10 s: it still exits by itself), so the
+ * host's stop request goes unanswered and the handle is abandoned. */
+int fx_graph_executor_debug_hooks(fx_graph_executor* ex, uint32_t skip_status_flush, uint32_t hold_ms);
 
 /* ------------------------------------------------------- quorum sizes */
 #define FX_PROTOCOL_ATLAS 0u
@@ -520,9 +527,12 @@ typedef struct fx_sim_spec {
                                              (GraphExecutor::executed is None; they matter
                                              only for where a run with extra time stops) */
 #define FX_SIM_FLAG_LARGE 2u              /* run the large-instance kernel */
-#define FX_SIM_FLAG_GENERIC 4u            /* the all-on-chip kernel built for run-time geometry even
+#define FX_SIM_FLAG_GENERIC 4u            /* either kernel's build for run-time geometry even
                                              when the batch has one of the geometries compiled in
-                                             (BASELINE configs[0]-[2]; same results, for A/B tests) */
+                                             (BASELINE configs[0]-[3]; same results, for A/B tests) */
+#define FX_SIM_FLAG_ARENA_FILL 8u         /* tests: the large-instance kernel's arena starts filled
+                                             with 0xA5 bytes instead of zeroed (the kernel must not
+                                             read a word it did not write) */
 typedef struct fx_sim_batch {
   const fx_sim_spec* specs;        /* [instances] device copy                          */
   const fx_sim_spec* host_specs;   /* [instances] host copy (validation, geometry)     */

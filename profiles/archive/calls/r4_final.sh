@@ -1,6 +1,6 @@
 # Round-4 closing checks on the GPU box: every GPU test, smoke, the handle and
 # executor bench lines.  Each step under its own limit; stops at the first failure.
-# usage: bash tools/r4_final.sh   (outputs under gpurun_out/fin/)
+# usage: bash profiles/archive/calls/r4_final.sh   (outputs under gpurun_out/fin/)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 M=gpurun_out/fin; rm -rf $M; mkdir -p $M

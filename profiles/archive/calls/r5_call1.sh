@@ -1,7 +1,7 @@
-# round-5 call: the GPU tests (tools/r5_tests.sh), then the k_simx occupancy A/B
+# round-5 call: the GPU tests (profiles/archive/calls/r5_tests.sh), then the k_simx occupancy A/B
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-bash tools/r5_tests.sh || exit 1
+bash profiles/archive/calls/r5_tests.sh || exit 1
 M=gpurun_out/xab; mkdir -p $M
 for v in xw3 xw4; do
   for s in 3072 4096; do

@@ -5,4 +5,4 @@ M=gpurun_out/r5p; mkdir -p $M
 timeout -k 10 400 python -u -m pytest tests/test_pred_gpu.py tests/test_poison_all.py -k "pred" -x -q --timeout 200 \
   --timeout-method thread > $M/tests7.log 2>&1 || { echo "pred tests rc=$?"; tail -30 $M/tests7.log; exit 1; }
 tail -1 $M/tests7.log
-PREFIX=gpurun_out/r5prof/r05h_ bash tools/r5_measure.sh pred || exit 1
+PREFIX=gpurun_out/r5prof/r05h_ bash profiles/archive/calls/r5_measure.sh pred || exit 1

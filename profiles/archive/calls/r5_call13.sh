@@ -8,4 +8,4 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
   tests/test_sim_large.py tests/test_sim_capture.py tests/test_poison_all.py tests/test_pred_gpu.py > $M/tests.log 2>&1 \
   || { echo "tests rc=$?"; tail -40 $M/tests.log; exit 1; }
 tail -1 $M/tests.log
-PREFIX=gpurun_out/r5prof/r05h_ bash tools/r5_measure.sh dense-sim pred || exit 1
+PREFIX=gpurun_out/r5prof/r05h_ bash profiles/archive/calls/r5_measure.sh dense-sim pred || exit 1

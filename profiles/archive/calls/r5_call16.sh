@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
   tests/test_sim_large.py tests/test_sim_capture.py tests/test_poison_all.py -k "not pred and not executor and not escalation and not persistent" \
   > $M/tests.log 2>&1 || { echo "tests rc=$?"; tail -40 $M/tests.log; exit 1; }
 tail -1 $M/tests.log
-PREFIX=gpurun_out/r5prof/r05k_ bash tools/r5_measure.sh dense-sim || exit 1
+PREFIX=gpurun_out/r5prof/r05k_ bash profiles/archive/calls/r5_measure.sh dense-sim || exit 1
 FX_LIB=fantoch_amd/build_x6/libfantoch_amd.so timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
   tests/test_sim_large.py -k config3 > $M/tests6.log 2>&1 || { echo "tests6 rc=$?"; tail -40 $M/tests6.log; exit 1; }
 tail -1 $M/tests6.log

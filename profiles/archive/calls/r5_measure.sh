@@ -4,7 +4,7 @@
 # that attaches them (<prefix><mode>_bench.json).  Everything lands under
 # gpurun_out/r5prof/ (gpurun brings that directory back; copy the files into
 # profiles/ afterwards).  Stops at the first failing step.
-# usage: PREFIX=gpurun_out/r5prof/r05a_ bash tools/r5_measure.sh [mode ...]
+# usage: PREFIX=gpurun_out/r5prof/r05a_ bash profiles/archive/calls/r5_measure.sh [mode ...]
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 M=gpurun_out/r5m; mkdir -p $M

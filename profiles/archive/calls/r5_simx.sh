@@ -1,6 +1,6 @@
 # k_simx changes: its parity tests first, then a dense-sim A/B against a
 # baseline build (fantoch_amd/build_<base>/) and the in-tree library with and
-# without the LDS Tarjan state.  usage: bash tools/r5_simx.sh [base]
+# without the LDS Tarjan state.  usage: bash profiles/archive/calls/r5_simx.sh [base]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 M=gpurun_out/r5x; mkdir -p $M

@@ -1,6 +1,6 @@
 # Round 5: new GPU tests first (-x stops at the first failure), then the whole
 # GPU suite, smoke and the headline bench line (histogram parity on its sample).
-# usage: bash tools/r5_tests.sh [pytest selection for the first step]
+# usage: bash profiles/archive/calls/r5_tests.sh [pytest selection for the first step]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 M=gpurun_out/r5; mkdir -p $M

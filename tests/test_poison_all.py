@@ -65,11 +65,21 @@ _SIM_CASES = {
 }
 
 
+# k_simx launch variants: the default launch, its arena filled with 0xA5 bytes
+# instead of zeroed (FX_SIM_FLAG_ARENA_FILL: the kernel must initialise every
+# arena word it reads), and the run-time-geometry build for
+# the shapes that otherwise run the configs[3] build (FX_SIM_FLAG_GENERIC)
+_SIMX_VARIANTS = {"default": {}, "arena_fill": dict(arena_fill=True), "generic": dict(generic=True)}
+
+
+@pytest.mark.parametrize("variant", sorted(_SIMX_VARIANTS))
 @pytest.mark.parametrize("fill", FILLS, ids=FILL_IDS)
 @pytest.mark.parametrize("case", sorted(_SIM_CASES))
-def test_poisoned_k_simx(case, fill):
+def test_poisoned_k_simx(case, fill, variant):
+    if variant == "generic" and not case.startswith("config3"):
+        pytest.skip("the sim_test shapes run the generic build already")
     specs, orc = _oracle_sim(case)
-    res = S.run(specs, planet(), large=True, before_launch=poisoner(*fill))
+    res = S.run(specs, planet(), large=True, before_launch=poisoner(*fill), **_SIMX_VARIANTS[variant])
     bad = ["instance %d err %d site %d events %d" % (i, int(e), int(res.stats[i, _lib.FX_SIM_STAT_ERR_SITE]),
                                                     res.events(i)) for i, e in enumerate(res.err) if e]
     assert not bad, "instances failed under fill %s: %s" % (fill, "; ".join(bad))
