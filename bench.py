@@ -67,6 +67,12 @@ def parse(argv=None):
     ap.add_argument("--f", type=int, default=None)
     ap.add_argument("--window", type=int, default=8)
     ap.add_argument("--cycle-pct", type=int, default=30)
+    ap.add_argument("--huge-shape", choices=["s5", "conflict2", "conflict100"], default="s5",
+                    help="--mode huge: SURVEY §8(d)'s S5 stream (per-key chains over --key-pool keys plus "
+                         "cycles), or the conflict-key streams at 2 %% / 100 %% conflicts")
+    ap.add_argument("--key-pool", type=int, default=1000, help="--mode huge s5: keys in the pool")
+    ap.add_argument("--horizon", type=int, default=None,
+                    help="--mode huge: rounds searched back for a command's deps (s5 default 640: mean deps ~ 3)")
     ap.add_argument("--seed", type=int, default=20250213)
     ap.add_argument("--conflict-block", type=int, default=-1,
                     help="instances per conflict rate block (-1 = --seeds: conflict-major "

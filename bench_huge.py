@@ -39,8 +39,19 @@ def main_huge(args):
     if lib.fx_device_count() <= 0:
         raise SystemExit("no GPU visible to libfantoch_amd")
     cmds = args.cmds if args.cmds is not None else 200_000  # n x cmds = 10^6 Adds per executor
-    p = fs.synth_params(seed=args.seed, instances=1, n=5, cmds=cmds, window=args.window,
-                        cycle_pct=args.cycle_pct, conflicts=(2,))
+    shape = getattr(args, "huge_shape", "conflict2")
+    if shape == "s5":  # per-key chains over a key pool plus cycles
+        horizon = args.horizon if args.horizon is not None else 640
+        p = fs.synth_params(seed=args.seed, instances=1, n=5, cmds=cmds, window=args.window,
+                            cycle_pct=args.cycle_pct, horizon=horizon, key_pool=args.key_pool)
+        shape_desc = "per-key chains over %d keys, %d %%%% concurrent pairs cycling, horizon %d" % (
+            args.key_pool, args.cycle_pct, horizon)
+    else:
+        rate = 2 if shape == "conflict2" else 100
+        horizon = args.horizon if args.horizon is not None else 64
+        p = fs.synth_params(seed=args.seed, instances=1, n=5, cmds=cmds, window=args.window,
+                            cycle_pct=args.cycle_pct, horizon=horizon, conflicts=(rate,))
+        shape_desc = "%d %%%% conflicts, %d %%%% cycles" % (rate, args.cycle_pct)
     S, steps, dmax = fs.synth_shape(p)
     pw = _lib.plane_words(S, steps)
     stream = torch.cuda.current_stream(dev)
@@ -131,9 +142,9 @@ def main_huge(args):
         "value": round(value, 1), "unit": "cmds/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-        "data": "synthetic Atlas commit streams (fx_synth: 2 %% conflicts, 30 %% cycles, window %d)" % args.window,
-        "config": {"workload": "single huge instance: 5 executors x %d Adds with cycles (BASELINE configs[4])"
-                               % steps,
+        "data": ("synthetic Atlas commit streams (fx_synth: " + shape_desc + ", window %d)") % args.window,
+        "config": {"workload": "single huge instance: 5 executors x %d Adds with cycles (BASELINE configs[4]), "
+                               "shape %s" % (steps, shape), "mean_deps": round(nd_total / n_adds, 3),
                    "parallelism": "quiescent-cut decomposition on one GPU; replicas only across GPUs"},
         "segments": int(stats.segments), "max_segment": int(stats.max_segment),
         "whole_streams": int(stats.whole_streams),

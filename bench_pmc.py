@@ -19,8 +19,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 _NOT_WORK = {"gpus", "steps", "warmup", "cpu_baseline_seconds", "no_cpu_baseline", "traffic_json", "pmc_key"}
 
 
+# arguments that shape only --mode huge's stream
+_HUGE_ONLY = {"huge_shape", "key_pool", "horizon"}
+
+
 def workload_key(args):
-    return json.dumps({k: v for k, v in sorted(vars(args).items()) if k not in _NOT_WORK}, sort_keys=True)
+    skip = _NOT_WORK | (set() if getattr(args, "mode", None) == "huge" else _HUGE_ONLY)
+    return json.dumps({k: v for k, v in sorted(vars(args).items()) if k not in skip}, sort_keys=True)
 
 
 def path(mode):

@@ -121,7 +121,8 @@ class SynthParams(ctypes.Structure):
                 ("cmds_per_process", ctypes.c_uint32), ("window", ctypes.c_uint32),
                 ("cycle_pct", ctypes.c_uint32), ("horizon", ctypes.c_uint32),
                 ("num_conflicts", ctypes.c_uint32), ("conflict_pct", ctypes.c_uint32 * 8),
-                ("conflict_block", ctypes.c_uint32), ("clients", ctypes.c_uint32)]
+                ("conflict_block", ctypes.c_uint32), ("clients", ctypes.c_uint32),
+                ("key_pool", ctypes.c_uint32)]
 
 
 class Config(ctypes.Structure):

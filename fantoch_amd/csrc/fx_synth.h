@@ -51,7 +51,7 @@ FX_HD uint64_t synth_rand(uint64_t seed, uint64_t inst, uint64_t a, uint64_t b) 
 struct SynthInstance {
   uint64_t seed;
   uint32_t inst;  // global instance index
-  uint32_t n, cmds, window, cycle_pct, horizon, conflict, clients;
+  uint32_t n, cmds, window, cycle_pct, horizon, conflict, clients, key_pool;
 };
 
 FX_HD SynthInstance synth_instance(const fx_synth_params& p, uint32_t local) {
@@ -64,6 +64,7 @@ FX_HD SynthInstance synth_instance(const fx_synth_params& p, uint32_t local) {
   si.cycle_pct = p.cycle_pct;
   si.horizon = p.horizon;
   si.clients = p.clients;
+  si.key_pool = p.key_pool;
   const uint32_t nc = p.num_conflicts ? p.num_conflicts : 1;
   const uint32_t ci = p.conflict_block ? (si.inst / p.conflict_block) % nc : si.inst % nc;
   si.conflict = p.conflict_pct[ci];
@@ -118,8 +119,49 @@ FX_HD uint32_t synth_deps_clients(const SynthInstance& si, uint32_t g, uint32_t*
   return nd;
 }
 
+// S5 (BASELINE configs[4]): per-key chains over a pool of
+// key_pool keys.  Command g's key is a C6 draw from the pool; per source, it
+// depends on that source's latest command on the same key within `horizon`
+// rounds (SequentialKeyDeps latest-per-key, sequential.rs:74-118, unioned over
+// the quorum) — except that with probability cycle_pct the pair (s, s2) of
+// round j depends on each other (a concurrent pair whose MCollects crossed:
+// a 2-cycle; chains through such pairs close longer cycles).
+FX_HD uint32_t synth_pool_key(const SynthInstance& si, uint32_t g) {
+  return (uint32_t)(synth_rand(si.seed, si.inst, g, PURPOSE_KEY) % si.key_pool);
+}
+FX_HD bool synth_pair_cycle(const SynthInstance& si, uint32_t j, uint32_t a, uint32_t b) {
+  const uint32_t lo = a < b ? a : b, hi = a < b ? b : a;
+  return si.cycle_pct > 0 &&
+         (uint32_t)(synth_rand(si.seed, si.inst, ((uint64_t)j << 8) | (lo << 4) | hi, PURPOSE_CYCLE + 8) % 100u) <
+             si.cycle_pct;
+}
+FX_HD uint32_t synth_deps_pool(const SynthInstance& si, uint32_t g, uint32_t* out) {
+  const uint32_t n = si.n;
+  const uint32_t s = g % n + 1;
+  const uint32_t j = g / n + 1;
+  const uint32_t key = synth_pool_key(si, g);
+  const uint32_t lo = j > si.horizon ? j - si.horizon : 1u;
+  uint32_t nd = 0;
+  for (uint32_t s2 = 1; s2 <= n; ++s2) {
+    uint32_t dep = 0;
+    if (s2 != s && synth_pair_cycle(si, j, s, s2)) {
+      dep = j;
+    } else {
+      // rounds strictly before g in generation order
+      for (uint32_t jj = s2 < s ? j : j - 1; jj >= lo && jj >= 1; --jj)
+        if (synth_pool_key(si, (jj - 1) * n + (s2 - 1)) == key) {
+          dep = jj;
+          break;
+        }
+    }
+    if (dep) out[nd++] = FX_PACK_DOT(s2, dep);
+  }
+  return nd;
+}
+
 // Deps of command g, ascending by packed dot (one per source at most).
 FX_HD uint32_t synth_deps(const SynthInstance& si, uint32_t g, uint32_t* out) {
+  if (si.key_pool > 1) return synth_deps_pool(si, g, out);
   if (si.clients > 1) return synth_deps_clients(si, g, out);
   const uint32_t n = si.n;
   const uint32_t s = g % n + 1;

@@ -37,6 +37,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -1275,6 +1276,7 @@ static int check_synth(const fx_synth_params* p) {
     return FX_ERR_INVALID_ARG;
   if ((uint64_t)p->instances * p->n >= (1ull << 32)) return FX_ERR_INVALID_ARG;
   if (p->clients > 1 && p->cmds_per_process % p->clients) return FX_ERR_INVALID_ARG;
+  if (p->key_pool == 1 || (p->key_pool > 1 && p->clients > 1)) return FX_ERR_INVALID_ARG;
   return FX_OK;
 }
 
@@ -1315,8 +1317,16 @@ int fx_synth_generate_host(const fx_synth_params* p, uint32_t* dot, uint32_t* hd
   memset(dot, 0, plane * 4);
   memset(hdr, 0, plane * 4);
   memset(deps, 0, plane * 4 * p->n);
-  for (uint32_t inst = 0; inst < p->instances; ++inst)
-    for (uint32_t g = 0; g < steps; ++g) synth_emit(*p, inst, g, S, steps, dot, hdr, deps);
+  // every command writes its own words of the planes: commands split over threads
+  const size_t total = (size_t)p->instances * steps;
+  const uint32_t nt = total < 4096 ? 1u : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (uint32_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (size_t i = t; i < total; i += nt)
+        synth_emit(*p, (uint32_t)(i / steps), (uint32_t)(i % steps), S, steps, dot, hdr, deps);
+    });
+  for (auto& x : th) x.join();
   return FX_OK;
 }
 

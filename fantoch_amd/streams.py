@@ -73,7 +73,7 @@ def pack_streams(streams, n):
 
 
 def synth_params(seed=1, instances=1, n=5, cmds=100, window=8, cycle_pct=30, horizon=64,
-                 conflicts=(0, 2, 10, 50, 100), instance_base=0, conflict_block=0, clients=1):
+                 conflicts=(0, 2, 10, 50, 100), instance_base=0, conflict_block=0, clients=1, key_pool=0):
     p = _lib.SynthParams()
     p.seed = seed
     p.instances = instances
@@ -88,6 +88,7 @@ def synth_params(seed=1, instances=1, n=5, cmds=100, window=8, cycle_pct=30, hor
         p.conflict_pct[i] = c
     p.conflict_block = conflict_block
     p.clients = clients
+    p.key_pool = key_pool
     return p
 
 

@@ -309,6 +309,15 @@ typedef struct fx_synth_params {
                                 with probability cycle_pct a random concurrent command
                                 of any other source: large SCCs, BASELINE configs[3];
                                 cmds_per_process must be a multiple of C)            */
+  uint32_t key_pool;         /* 0: the conflict-key model above.  K >= 2 (one client
+                                per process): SURVEY §8(d)'s S5 stream, per-key chains
+                                over a pool of K keys: every command's key is a C6
+                                draw from the pool, its deps are, per source, the
+                                latest command on that key within `horizon` rounds
+                                (its own source: earlier seqs only), and with
+                                probability cycle_pct two commands of the same round
+                                depend on each other (2-cycles; longer cycles through
+                                the chains).  conflict_pct is not used.              */
 } fx_synth_params;
 
 /* Planes of the synthetic batch: S = instances * n, steps = n * cmds, dmax = n. */

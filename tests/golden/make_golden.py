@@ -46,6 +46,8 @@ SYNTH = {
                          conflicts=(100,)),
     "no_pending": dict(seed=105, n=5, instances=10, cmds=40, window=0, cycle_pct=0),
     "ragged_n2": dict(seed=106, n=2, instances=33, cmds=37, window=5, cycle_pct=40),
+    # SURVEY §8(d) S5's shape (configs[4]): per-key chains over a key pool plus cycles
+    "s5_pool": dict(seed=107, n=5, instances=4, cmds=400, window=8, cycle_pct=30, horizon=96, key_pool=50),
 }
 
 
@@ -90,14 +92,18 @@ def hists(planes, order, release, nexec, nbc=NBINS_CHAIN, nbd=NBINS_DELAY):
 def synth_params_array(case):
     conf = list(case.get("conflicts", (0, 2, 10, 50, 100)))
     keys = ["seed", "n", "instances", "cmds", "window", "cycle_pct"]
-    return np.array([case[k] for k in keys] + [len(conf)] + conf, np.int64)
+    extra = [case["horizon"], case["key_pool"]] if "key_pool" in case else []  # (older vectors: none)
+    return np.array([case[k] for k in keys] + [len(conf)] + conf + extra, np.int64)
 
 
 def params_from_array(a):
     seed, n, instances, cmds, window, cycle_pct, nc = (int(x) for x in a[:7])
     conf = tuple(int(x) for x in a[7:7 + nc])
-    return dict(seed=seed, n=n, instances=instances, cmds=cmds, window=window,
-                cycle_pct=cycle_pct, conflicts=conf)
+    out = dict(seed=seed, n=n, instances=instances, cmds=cmds, window=window,
+               cycle_pct=cycle_pct, conflicts=conf)
+    if len(a) >= 9 + nc:
+        out.update(horizon=int(a[7 + nc]), key_pool=int(a[8 + nc]))
+    return out
 
 
 def synth_expected(case):
@@ -152,8 +158,10 @@ def kats():
     return out
 
 
-def main():
+def main(only=None):
     for name, case in SYNTH.items():
+        if only and name not in only:
+            continue
         planes, exp = synth_expected(case)
         np.savez_compressed(os.path.join(HERE, "synth_%s.npz" % name), digest=planes_digest(planes),
                             **exp)
@@ -162,5 +170,5 @@ def main():
         json.dump(kats(), fh, indent=1, sort_keys=True)
 
 
-if __name__ == "__main__":
-    main()
+if __name__ == "__main__":  # python make_golden.py [case ...]: only those vectors (and kats.json)
+    main(sys.argv[1:] or None)

@@ -95,6 +95,47 @@ def test_config4_single_huge_instance_cut():
           "%d segments, longest %d" % (t_gpu, t_cpu, res.cut_stats.segments, res.cut_stats.max_segment))
 
 
+def test_config4_s5_single_huge_instance_cut():
+    """BASELINE configs[4] on the stream SURVEY §8(d) specifies (S5): one
+    instance, five executors of 10^6 Adds each, per-key chains over 1,000 keys
+    plus cycles, mean deps ~3 (bench.py --mode huge's default shape);
+    bit-exact with the oracle, histograms included."""
+    p = fs.synth_params(seed=2026, instances=1, n=5, cmds=200_000, window=8, cycle_pct=30, horizon=640,
+                        key_pool=1000)
+    planes = fs.synth_host(p)
+    nd = ((planes.hdr >> 24) & 31).astype(np.int64).sum() / (planes.S * planes.steps)
+    assert 2.8 < nd < 3.2, nd
+    res = fd.run_batch(planes, cut=True, nbins_chain=64, nbins_delay=2048)
+    assert res.status == _lib.FX_OK
+    o_order, o_rel, o_nexec = assert_parity(planes, res)
+    assert np.all(res.nexec == planes.steps)
+    chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 64, 2048)
+    assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
+    st = res.cut_stats
+    print("S5: %d segments, longest %d, whole streams %d" % (st.segments, st.max_segment, st.whole_streams))
+    assert st.failed_streams == 0
+
+
+@pytest.mark.parametrize("rate", [50, 100])
+def test_high_conflict_single_instance_cut(rate):
+    """One instance at high conflict rates (every command on the shared key at
+    100 %, 30 % concurrent cycles): cuts become rare, and segments longer than
+    the driver's limit (or a stream without a final cut) run whole; either way
+    bit-exact with the oracle."""
+    p = fs.synth_params(seed=2027, instances=1, n=5, cmds=20_000, window=8, cycle_pct=30, conflicts=(rate,))
+    planes = fs.synth_host(p)
+    res = fd.run_batch(planes, cut=True, nbins_chain=256, nbins_delay=2048)
+    assert res.status == _lib.FX_OK
+    o_order, o_rel, o_nexec = assert_parity(planes, res)
+    assert np.all(res.nexec == planes.steps)
+    chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 256, 2048)
+    assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
+    st = res.cut_stats
+    print("%d %%: %d segments, longest %d, whole streams %d" % (rate, st.segments, st.max_segment,
+                                                               st.whole_streams))
+    assert st.failed_streams == 0
+
+
 def test_cut_every_stream_empty():
     """All lengths 0: no segment at all; every stream still gets nexec = 0 and
     FX_OK (the outputs start as a sentinel, device.run_batch)."""
