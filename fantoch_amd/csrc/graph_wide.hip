@@ -46,6 +46,12 @@ constexpr uint32_t PK_EPOCH_SHIFT = 11, PK_EPOCH_MAX = (1u << 21) - 4096u;
 
 struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-bit clock windows
   uint32_t P, Q, WB, n, D, wlcap;
+  // per-source strides of the index (entries) and the clock windows (words).
+  // Packed (LDS): one word more than a source's part, so the same slot /
+  // window word of different sources falls in different LDS banks (the deps of
+  // one vertex, looked up lane-parallel, come from different sources with
+  // nearby seqs: without the pad they hit one bank, a 5-way conflict)
+  uint32_t QS, WBS;
   bool pk;
   uint32_t vdot, vrec, vnd, vdeps, vwait, vid, vlow, vmark, vce, vfree, tstk, fv, fi, wl, tl, tmp, hidx, front, bits, sc, words;
   // partial replication only (0 words otherwise): per-vertex parent lists
@@ -59,6 +65,8 @@ struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-
     n = n_;
     D = D_;
     pk = packed;
+    QS = packed ? Q + 2u : Q;
+    WBS = packed ? WB + 1u : WB;
     uint32_t o = 0;
     const uint32_t h = packed ? P / 2 : P;  // a u16 list of P entries
     vdot = o; o += P;
@@ -79,9 +87,9 @@ struct Lay {  // table layout (u32 words) for capacity P, index Q per source, W-
     wl = o; o += wlcap;
     tl = o; o += h;
     tmp = o; o += h;
-    hidx = o; o += packed ? n * Q / 2 : n * Q;
+    hidx = o; o += packed ? n * QS / 2 : n * QS;
     front = o; o += 8;
-    bits = o; o += n * WB;
+    bits = o; o += n * WBS;
     sc = o; o += 4;  // saved scalars of a resumable (HBM) stream: nfree, nexec, epoch
     vwn = o; o += partial ? P : 0;
     vwl = o; o += partial ? P * PW : 0;
@@ -215,11 +223,11 @@ struct W {
     if (sq <= f) return;
     if (sq - f - 1 >= L.WB * 32u) { err = FX_ERR_CAPACITY; return; }
     const uint32_t mask = L.WB * 32u - 1u;
-    const uint32_t b = sq & mask, wi = (src - 1) * L.WB + (b >> 5);
+    const uint32_t b = sq & mask, wi = (src - 1) * L.WBS + (b >> 5);
     put(L.bits, wi, rd(L.bits, wi) | (1u << (b & 31u)));
     // advance the frontier over contiguous seqs, clearing their bits
     for (;;) {
-      const uint32_t nb = (f + 1) & mask, nw = (src - 1) * L.WB + (nb >> 5);
+      const uint32_t nb = (f + 1) & mask, nw = (src - 1) * L.WBS + (nb >> 5);
       const uint32_t word = rd(L.bits, nw);
       if (!((word >> (nb & 31u)) & 1u)) break;
       put(L.bits, nw, word & ~(1u << (nb & 31u)));
@@ -237,7 +245,7 @@ struct W {
     if (sq <= f) return true;
     if (sq - f - 1 >= L.WB * 32u) return false;
     const uint32_t b = sq & (L.WB * 32u - 1u);
-    return (rd(L.bits, (src - 1) * L.WB + (b >> 5)) >> (b & 31u)) & 1u;
+    return (rd(L.bits, (src - 1) * L.WBS + (b >> 5)) >> (b & 31u)) & 1u;
   }
 
   // ------------------------------------------------------- vertex index
@@ -245,7 +253,7 @@ struct W {
   // without a read of the vertex table.  Packed: a u16 (vertex + 1), and the
   // vertex's dot is compared (read in the same round trip as its Tarjan word).
   __device__ __forceinline__ uint32_t hslot(uint32_t d) const {
-    return (FX_DOT_SRC(d) - 1) * L.Q + (FX_DOT_SEQ(d) & (L.Q - 1u));
+    return (FX_DOT_SRC(d) - 1) * L.QS + (FX_DOT_SEQ(d) & (L.Q - 1u));
   }
   __device__ __forceinline__ uint32_t htag(uint32_t d) const {
     return (FX_DOT_SEQ(d) >> __builtin_ctz(L.Q)) << 16;
@@ -314,8 +322,8 @@ struct W {
     const uint32_t si = ok ? src - 1u : 0u;
     const uint32_t bb = sq & (L.WB * 32u - 1u);
     const uint32_t f = ok ? at(L.front, si) : 0u;
-    const uint32_t bw = ok ? at(L.bits, si * L.WB + (bb >> 5)) : 0u;
-    const uint32_t hw = ok ? lget(L.hidx, si * L.Q + (sq & (L.Q - 1u))) : 0u;
+    const uint32_t bw = ok ? at(L.bits, si * L.WBS + (bb >> 5)) : 0u;
+    const uint32_t hw = ok ? lget(L.hidx, si * L.QS + (sq & (L.Q - 1u))) : 0u;
     const bool ex = ok && (sq <= f || (sq - f - 1u < L.WB * 32u && ((bw >> (bb & 31u)) & 1u)));
     return ex ? RS_EXEC : hw;
   }
@@ -421,8 +429,8 @@ struct W {
         const bool inr = src >= 1 && src <= L.n;
         const uint32_t si = inr ? src - 1 : 0u;
         const uint32_t bb = sq & (L.WB * 32u - 1u);
-        const uint32_t hw = lrd(L.hidx, si * L.Q + (sq & (L.Q - 1u)));
-        const uint32_t bw = rd(L.bits, si * L.WB + (bb >> 5));
+        const uint32_t hw = lrd(L.hidx, si * L.QS + (sq & (L.Q - 1u)));
+        const uint32_t bw = rd(L.bits, si * L.WBS + (bb >> 5));
         const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)frv, (int)si);
         const bool executed = inr && (sq <= f || (sq - f - 1u < L.WB * 32u && ((bw >> (bb & 31u)) & 1u)));
         if (d == cdot || executed) continue;  // self or executed (tarjan.rs:128-145)
@@ -709,7 +717,7 @@ struct W {
       const bool okj = lid < nd && sj >= 1 && sj <= L.n;
       const uint32_t bj = qj & (L.WB * 32u - 1u);
       const uint32_t fj = okj ? at(L.front, sj - 1) : 0u;
-      const uint32_t wj = okj ? at(L.bits, (sj - 1) * L.WB + (bj >> 5)) : 0u;
+      const uint32_t wj = okj ? at(L.bits, (sj - 1) * L.WBS + (bj >> 5)) : 0u;
       const bool exj = okj && (qj <= fj || (qj - fj - 1u < L.WB * 32u && ((wj >> (bj & 31u)) & 1u)));
       const uint64_t cand = __ballot(lid < nd && drj != d && !exj);
       const uint32_t u = cand ? (uint32_t)__builtin_amdgcn_readlane((int)drj, (int)__builtin_ctzll(cand)) : 0u;

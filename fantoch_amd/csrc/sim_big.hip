@@ -1891,6 +1891,25 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
   } else {
     __syncthreads();
   }
+#ifdef FX_SIMX_DIAG
+  // canaries in arena words the simulation never writes (client words 6 / 7,
+  // the ready list's last entry), checked after every event: a write the
+  // kernel did not make (or a stray one of its own) shows up at its event
+  const uint32_t can_v = 0xC0FFEE00u | (inst & 0xFFu);
+  const uint32_t can_a = g.o_cl + 6u, can_b = g.o_cl + (s.C - 1u) * 8u + 7u, can_c = g.o_rdy + s.C + 63u;
+  if (s.lid == 0) {
+    M[can_a] = can_v;
+    M[can_b] = can_v;
+    M[can_c] = can_v;
+  }
+  if constexpr (WPB > 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+#endif
   // periodic events (runner.rs:179-187), then clients (run(), C5 ascending)
   if (s.gc_ms_())
     for (uint32_t p = 0; p < n; ++p) s.push_event(s.gc_ms_(), (1u << 6) | (p << 3), E_TICK | (p << 8), 0);
@@ -1938,6 +1957,17 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
     s.cur_hi = hi;
 #endif
     s.free_event(e);
+#ifdef FX_SIMX_DIAG
+    {
+      const uint32_t ca = uni(M[can_a]), cb = uni(M[can_b]), cc = uni(M[can_c]);
+      if ((ca != can_v || cb != can_v || cc != can_v) && !s.err) {
+        s.dput(16, ca | ((uint64_t)cb << 32));
+        s.dput(17, cc | ((uint64_t)s.events << 32));
+        s.fail_late(__LINE__);
+        break;
+      }
+    }
+#endif
     s.run_event(kind, from, to, arg, gcv);
 #ifdef FX_SIMX_EVLOG
     // debug build (tools/simx_repro.py): every event's key, info, argument and
@@ -2038,6 +2068,12 @@ size_t simx_arena_bytes(const fx_sim_spec& sp, uint32_t ring, uint32_t dots) {
   return simx_geometry(sp, ring, dots, g) ? (size_t)g.words * 4 : 0;
 }
 
+// fills `words` words with v (the arena clear of FX_SIMX_ARENA=zkern)
+__global__ void k_fill_words(uint32_t* p, size_t words, uint32_t v) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
 // Launches the large-instance simulator (fx_sim_run validated the batch).
 int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
   using namespace simx;
@@ -2047,16 +2083,29 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
   void* arena = nullptr;
   // The arena starts zeroed; FX_SIM_FLAG_ARENA_FILL (tests) fills it with
   // 0xA5 bytes instead: the kernel initialises every word it reads, so both
-  // give the same results (tests/test_poison_all.py).  FX_SIMX_ARENA=pool
-  // (diagnostics) keeps whatever the pool's memory held.
-  static const bool pool_env = [] {
+  // give the same results (tests/test_poison_all.py).  FX_SIMX_ARENA
+  // (diagnostics): `pool` keeps whatever the pool's memory
+  // held; `zsync` waits for the clear before the launch; `zkern` clears with
+  // a kernel of ours instead of hipMemsetAsync; `plain` takes the arena from
+  // hipMalloc instead of the stream-ordered pool.
+  static const int arena_mode = [] {
     const char* e = std::getenv("FX_SIMX_ARENA");
-    return e && std::string(e) == "pool";
+    const std::string v = e ? e : "";
+    return v == "pool" ? 1 : v == "zsync" ? 2 : v == "zkern" ? 3 : v == "plain" ? 4 : 0;
   }();
-  if (hipMallocAsync(&arena, bytes, hs) != hipSuccess) return FX_ERR_HIP;
-  if (!pool_env || (b->flags & FX_SIM_FLAG_ARENA_FILL))
-    if (hipMemsetAsync(arena, (b->flags & FX_SIM_FLAG_ARENA_FILL) ? 0xA5 : 0, bytes, hs) != hipSuccess)
-      return FX_ERR_HIP;
+  const int fillv = (b->flags & FX_SIM_FLAG_ARENA_FILL) ? 0xA5 : 0;
+  if (arena_mode == 4) {
+    if (hipMalloc(&arena, bytes) != hipSuccess) return FX_ERR_HIP;
+  } else if (hipMallocAsync(&arena, bytes, hs) != hipSuccess) {
+    return FX_ERR_HIP;
+  }
+  if (arena_mode == 3) {
+    hipLaunchKernelGGL(k_fill_words, dim3(1024), dim3(256), 0, hs, (uint32_t*)arena, bytes / 4,
+                       (uint32_t)fillv * 0x01010101u);
+  } else if (arena_mode != 1 || fillv) {
+    if (hipMemsetAsync(arena, fillv, bytes, hs) != hipSuccess) return FX_ERR_HIP;
+  }
+  if (arena_mode == 2 && hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
   a.specs = b->specs;
   a.instances = b->instances;
   a.arena = (uint32_t*)arena;
@@ -2098,7 +2147,12 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
     hipLaunchKernelGGL((k_simx<4>), grid, block, lds, hs, a);
   }
   const hipError_t le = hipGetLastError();
-  (void)hipFreeAsync(arena, hs);
+  if (arena_mode == 4) {
+    (void)hipStreamSynchronize(hs);
+    (void)hipFree(arena);
+  } else {
+    (void)hipFreeAsync(arena, hs);
+  }
   return le == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 

@@ -15,6 +15,8 @@ the kernel snapshotted at its first failure (stats slots 0..15):
                             12 R_PST | R_WAIT << 32   13 copy's tag | copy slot << 32
   SCC member not pending:   8 root | tsp << 32   9 ctp | cv << 32   10 member | status << 32
                             11 its tag | masks << 32   12 R_TL | R_MARK << 32   13 index | count << 32
+  a canary changed:         16 canaries a | b << 32   17 canary c | events << 32 (words the
+                            simulation never writes, set at the start; checked after every event)
 No oracle: a failure is the signal."""
 import os
 import sys
@@ -43,7 +45,7 @@ for rep in range(reps):
                 if not e:
                     continue
                 fails += 1
-                st = [int(x) for x in res.stats[i, :16]]
+                st = [int(x) for x in res.stats[i, :18]]
                 print("rep %d %s fill %s: instance %d err %d site %d events %d" % (
                     rep, case, fill, i, int(e), int(res.stats[i, _lib.FX_SIM_STAT_ERR_SITE]), res.events(i)))
                 print("   " + " ".join("%d:%016x" % (k, v) for k, v in enumerate(st) if v), flush=True)
