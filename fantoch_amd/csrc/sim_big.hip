@@ -43,6 +43,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -2068,10 +2069,36 @@ size_t simx_arena_bytes(const fx_sim_spec& sp, uint32_t ring, uint32_t dots) {
   return simx_geometry(sp, ring, dots, g) ? (size_t)g.words * 4 : 0;
 }
 
-// fills `words` words with v (the arena clear of FX_SIMX_ARENA=zkern)
-__global__ void k_fill_words(uint32_t* p, size_t words, uint32_t v) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x)
-    p[i] = v;
+// The arenas of the large-instance simulator: one hipMalloc'ed block per
+// stream, grown when a launch needs more (hipFree waits for the device, so a
+// block is never freed under a running launch) and reused by every later
+// launch on that stream, which stream order serialises.  Launches on
+// different streams get different blocks.  Never freed (process lifetime, as
+// the batch executor's scratch).
+void* simx_arena(hipStream_t hs, size_t bytes) {
+  struct Block {
+    hipStream_t s;
+    void* p;
+    size_t cap;
+  };
+  static std::mutex mu;
+  static std::vector<Block>* blocks = new std::vector<Block>();
+  std::lock_guard<std::mutex> g(mu);
+  for (Block& bl : *blocks) {
+    if (bl.s != hs) continue;
+    if (bl.cap >= bytes) return bl.p;
+    (void)hipFree(bl.p);
+    bl.p = nullptr;
+    bl.cap = 0;
+    const size_t grown = bytes + bytes / 8;
+    if (hipMalloc(&bl.p, grown) != hipSuccess) return nullptr;
+    bl.cap = grown;
+    return bl.p;
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  blocks->push_back(Block{hs, p, bytes});
+  return p;
 }
 
 // Launches the large-instance simulator (fx_sim_run validated the batch).
@@ -2080,32 +2107,26 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
   ArgsX a{};
   if (!simx_geometry(b->host_specs[0], b->ring_entries, b->dot_slots, a.g)) return FX_ERR_UNSUPPORTED;
   const size_t bytes = (size_t)a.g.words * 4 * b->instances;
-  void* arena = nullptr;
-  // The arena starts zeroed; FX_SIM_FLAG_ARENA_FILL (tests) fills it with
-  // 0xA5 bytes instead: the kernel initialises every word it reads, so both
-  // give the same results (tests/test_poison_all.py).  FX_SIMX_ARENA
-  // (diagnostics): `pool` keeps whatever the pool's memory
-  // held; `zsync` waits for the clear before the launch; `zkern` clears with
-  // a kernel of ours instead of hipMemsetAsync; `plain` takes the arena from
-  // hipMalloc instead of the stream-ordered pool.
-  static const int arena_mode = [] {
+  // The arena comes from a per-stream cache of hipMalloc'ed memory
+  // (simx_arena) and starts zeroed; FX_SIM_FLAG_ARENA_FILL (tests) fills it
+  // with 0xA5 bytes instead: the kernel initialises every word it reads, so
+  // both give the same results (tests/test_poison_all.py).
+  // FX_SIMX_ARENA=async (diagnostics) restores the round-5 allocation, a
+  // stream-ordered pool block per launch (hipMallocAsync / hipFreeAsync): with
+  // it about 2 % of small launches saw large parts of their arena zeroed by a
+  // write no kernel of ours made, part-way through the run.
+  static const bool async_env = [] {
     const char* e = std::getenv("FX_SIMX_ARENA");
-    const std::string v = e ? e : "";
-    return v == "pool" ? 1 : v == "zsync" ? 2 : v == "zkern" ? 3 : v == "plain" ? 4 : 0;
+    return e && std::string(e) == "async";
   }();
-  const int fillv = (b->flags & FX_SIM_FLAG_ARENA_FILL) ? 0xA5 : 0;
-  if (arena_mode == 4) {
-    if (hipMalloc(&arena, bytes) != hipSuccess) return FX_ERR_HIP;
-  } else if (hipMallocAsync(&arena, bytes, hs) != hipSuccess) {
+  void* arena = nullptr;
+  if (async_env) {
+    if (hipMallocAsync(&arena, bytes, hs) != hipSuccess) return FX_ERR_HIP;
+  } else if (!(arena = simx_arena(hs, bytes))) {
     return FX_ERR_HIP;
   }
-  if (arena_mode == 3) {
-    hipLaunchKernelGGL(k_fill_words, dim3(1024), dim3(256), 0, hs, (uint32_t*)arena, bytes / 4,
-                       (uint32_t)fillv * 0x01010101u);
-  } else if (arena_mode != 1 || fillv) {
-    if (hipMemsetAsync(arena, fillv, bytes, hs) != hipSuccess) return FX_ERR_HIP;
-  }
-  if (arena_mode == 2 && hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
+  if (hipMemsetAsync(arena, (b->flags & FX_SIM_FLAG_ARENA_FILL) ? 0xA5 : 0, bytes, hs) != hipSuccess)
+    return FX_ERR_HIP;
   a.specs = b->specs;
   a.instances = b->instances;
   a.arena = (uint32_t*)arena;
@@ -2147,12 +2168,7 @@ int simx_launch(const fx_sim_batch* b, const fx_sim_output* o, hipStream_t hs) {
     hipLaunchKernelGGL((k_simx<4>), grid, block, lds, hs, a);
   }
   const hipError_t le = hipGetLastError();
-  if (arena_mode == 4) {
-    (void)hipStreamSynchronize(hs);
-    (void)hipFree(arena);
-  } else {
-    (void)hipFreeAsync(arena, hs);
-  }
+  if (async_env) (void)hipFreeAsync(arena, hs);
   return le == hipSuccess ? FX_OK : FX_ERR_HIP;
 }
 

@@ -33,13 +33,15 @@ from test_sim_large import planet  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 cases = sys.argv[2].split(",") if len(sys.argv) > 2 else ["config3_epaxos", "sim_epaxos_5_2", "sim_atlas_5_2"]
 fills = list(T.FILLS) + [None]
+arena_fill = os.environ.get("SIMX_DIAG_FILL") == "1"  # the arena starts as 0xA5 bytes (FX_SIM_FLAG_ARENA_FILL)
 fails = 0
 launches = 0
 for rep in range(reps):
     for case in cases:
         specs = T._SIM_CASES[case]()
         for fill in fills:
-            res = S.run(specs, planet(), large=True, before_launch=T.poisoner(*fill) if fill else None)
+            res = S.run(specs, planet(), large=True, before_launch=T.poisoner(*fill) if fill else None,
+                        arena_fill=arena_fill)
             launches += 1
             for i, e in enumerate(res.err):
                 if not e:
