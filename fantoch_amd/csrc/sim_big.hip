@@ -61,7 +61,20 @@ constexpr uint32_t HC_BINS = 64;    // ChainSize bins counted per instance in LD
 constexpr uint32_t HD_BINS = 256;   // ExecutionDelay bins counted per instance in LDS
 constexpr uint32_t HL_LOG = 6, HL_SLOTS = 1u << HL_LOG;  // client-latency cache
 constexpr uint32_t TIME_LIMIT = 1u << 24;  // ms; the event key holds time << 8
-constexpr uint32_t LDS_WORDS = HC_BINS + HD_BINS + 2 * HL_SLOTS;
+// per-instance LDS: the histogram caches, then lane tables kept out of the
+// register file (the 5-wave configs[3] build spills what does not fit): at
+// 8 p + s, p's committed GC frontier of source s + 1, its previous stable
+// frontier, the link delay p -> s
+// frontier, the link delay p -> s; and two 64-bit sums (the executor Adds'
+// deps, the client latencies)
+constexpr uint32_t L_GCF = HC_BINS + HD_BINS + 2 * HL_SLOTS, L_GPS = L_GCF + 64, L_DPQ = L_GPS + 64;
+constexpr uint32_t L_DEPS = L_DPQ + 64, L_LATSUM = L_DEPS + 2;
+// the top of the free event stack (FC entries): a push takes an entry with an
+// LDS read instead of a dependent HBM one; spilled / refilled FC / 2 at a time
+constexpr uint32_t FC = 64, L_FC = L_LATSUM + 2;
+// each process's table of the frontiers the others reported (GC, n x n x n <= 512)
+constexpr uint32_t L_GCO = L_FC + FC;
+constexpr uint32_t LDS_WORDS = L_GCO + NMAX * NMAX * NMAX;
 
 // event kinds (protocol kinds numbered as the oracle's trace, sim_oracle.cpp MK)
 enum : uint32_t {
@@ -325,15 +338,25 @@ struct Big {
 #endif
   uint32_t now = 0;  // ms
   uint32_t seq = 0;  // insertion counter (C3)
-  uint64_t rdraws = 0;
-  uint64_t events = 0, trace = 0, deps_total = 0, lat_sum = 0;
+  uint32_t rdraws = 0, events = 0;  // (32 bits: bounded by max_events; 64-bit counters live in LDS)
+  uint64_t trace = 0;
+  __device__ __forceinline__ void lds_add64(uint32_t off, uint32_t v) {
+    const uint64_t x = (uint64_t)uni(lds[off]) | ((uint64_t)uni(lds[off + 1]) << 32);
+    const uint64_t y = x + v;
+    put(lds[off], (uint32_t)y);
+    put(lds[off + 1], (uint32_t)(y >> 32));
+  }
+  __device__ __forceinline__ uint64_t lds64(uint32_t off) const {
+    return (uint64_t)uni(lds[off]) | ((uint64_t)uni(lds[off + 1]) << 32);
+  }
   uint32_t clients_done = 0;
   bool done = false, in_extra = false;
   uint32_t final_ms = 0;
 
   // event pool: minimum (key hi, key lo) of group 64 k + lane in gh[k], gl[k]
   uint32_t gh[NG], gl[NG];
-  uint32_t nfree = 0;
+  uint32_t nfree = 0;  // entries in the HBM part of the free stack
+  uint32_t fcn = 0;    // entries in its LDS top (lds[L_FC + 0 .. fcn))
   // lane p: proposal seq, Fast / Slow (and their read-only shares), executed
   // count, Stable, quorums (fast | write << 8 | majority << 16), GC reporters
   // (packed into two VGPRs, 8 lanes a field: pa lane A_x + p, pb lane B_x + p)
@@ -344,7 +367,7 @@ struct Big {
 
   // lane 8 p + s: p's committed frontier of source s + 1 (GC track), its
   // previous stable frontier, and the link delay p -> s
-  uint32_t gcf = 0, gps = 0, dpq = 0;
+  __device__ __forceinline__ uint32_t dpq_(uint32_t i) { return uni(lds[L_DPQ + i]); }
   // handler frames, frame fi in lane fi: action (0 none, 1 ToSend) | kind << 2 |
   // targets << 8 | next target << 16; dot; base of its ready results
 
@@ -494,11 +517,17 @@ struct Big {
       err = FX_ERR_TIME_RANGE;
       return NONE;
     }
-    if (nfree == 0) {
-      fail_cap(__LINE__);
-      return NONE;
+    if (fcn == 0) {  // refill the LDS top from the HBM stack: its top FC / 2 entries, in order
+      if (nfree == 0) {
+        fail_cap(__LINE__);
+        return NONE;
+      }
+      const uint32_t k = min(nfree, FC / 2u);
+      if (lid < k) lds[L_FC + lid] = W(g.o_free, nfree - k + lid);
+      nfree -= k;
+      fcn = k;
     }
-    const uint32_t e = rd(W(g.o_free, --nfree));
+    const uint32_t e = uni(lds[L_FC + --fcn]);
     const uint32_t hi = (t << 8) | cls, lo = seq++;
     put(W(g.o_kh, e), hi);
     put(W(g.o_kl, e), lo);
@@ -565,7 +594,19 @@ struct Big {
     }
     return grp * 64u + j;
   }
-  __device__ __forceinline__ void free_event(uint32_t e) { put(W(g.o_free, nfree++), e); }
+  __device__ __forceinline__ void free_event(uint32_t e) {
+    if (fcn == FC) {  // spill the LDS top's lower half to the HBM stack, in order
+      const uint32_t v = lds[L_FC + lid];  // (lanes < FC)
+      const uint32_t hi = lds[L_FC + ((lid + FC / 2u) & (FC - 1u))];
+      if (lid < FC / 2u) {
+        W(g.o_free, nfree + lid) = v;
+        lds[L_FC + lid] = hi;
+      }
+      nfree += FC / 2u;
+      fcn = FC / 2u;
+    }
+    put(lds[L_FC + fcn++], e);
+  }
 #ifdef FX_SIMX_DIAG
   // the broken group, its leaves, and every group whose lane minimum differs
   // from the minimum of its leaves
@@ -946,7 +987,7 @@ struct Big {
   // was freed was executed, hence committed, everywhere
   __device__ __forceinline__ void gc_commit(uint32_t p, uint32_t dot) {
     const uint32_t si = FX_DOT_SRC(dot) - 1u, sq = FX_DOT_SEQ(dot);
-    uint32_t fr = rl(gcf, p * 8u + si);
+    uint32_t fr = uni(lds[L_GCF + p * 8u + si]);
     if (sq != fr + 1u) return;
     const uint32_t top = rl(pa, A_SEQ + si);
     for (uint32_t guard = 0; guard <= g.NS; ++guard) {
@@ -957,7 +998,7 @@ struct Big {
       if (rd(S(sl, SL_DOT)) == d2 && (rd(RC(sl, p, R_PST)) & 3u) != ST_COMMIT) break;
       fr = nx;
     }
-    lset(gcf, p * 8u + si, fr);
+    put(lds[L_GCF + p * 8u + si], fr);
   }
 
   // atlas.rs:404-475 / epaxos.rs:370-428
@@ -1031,10 +1072,10 @@ struct Big {
   // periodic GarbageCollection at p (atlas.rs:699-714): MGarbageCollection
   // with p's committed frontier to every other process (ascending)
   __device__ __forceinline__ void gc_tick(uint32_t p) {
-    const uint32_t fv = gather(gcf, (p * 8u + lid) & 63u);  // lane s: frontier of source s + 1
+    const uint32_t fv = lds[L_GCF + ((p * 8u + lid) & 63u)];  // lane s: frontier of source s + 1
     for (uint32_t q = 0; q < n && !err; ++q) {
       if (q == p) continue;
-      const uint32_t d = msg_delay(rl(dpq, p * 8u + q));
+      const uint32_t d = msg_delay(dpq_(p * 8u + q));
       const uint32_t e = push_event(now + d, (2u << 6) | (p << 3) | q, M_GC | (p << 4) | (q << 8), 0);
       if (e == NONE) return;
       if (lid < n) W(g.o_gp, e * n + lid) = fv;
@@ -1048,18 +1089,18 @@ struct Big {
     // q's table of reported frontiers (row r = the last report from r, lane
     // r n + s = source s + 1) in one lane-parallel load; the report from
     // `from` is merged in registers and written back
-    const uint32_t nn = n * n, base = g.o_gco + q * nn;
-    uint32_t blk = lid < nn ? W(base, lid) : 0u;
+    const uint32_t nn = n * n, base = L_GCO + q * nn;
+    uint32_t blk = lid < nn ? lds[base + lid] : 0u;
     const uint32_t row = lid / n, src = lid - row * n;
     const uint32_t vs = gather(v, src & 63u);
     if (lid < nn && row == from) {
       blk = max(blk, vs);
-      W(base, lid) = blk;
+      lds[base + lid] = blk;
     }
     const uint32_t rep = rl(pb, B_REP + q) | (1u << from);
     lset(pb, B_REP + q, rep);
     uint32_t cur = 0;
-    const uint32_t mine = gather(gcf, (q * 8u + lid) & 63u);
+    const uint32_t mine = lds[L_GCF + ((q * 8u + lid) & 63u)];
     if (pop32(rep) == n - 1u) {
       cur = lid < n ? mine : 0u;
       for (uint32_t r = 0; r < n; ++r) {
@@ -1068,11 +1109,11 @@ struct Big {
         if (lid < n) cur = min(cur, o);
       }
     }
-    const uint32_t prev = gather(gps, (q * 8u + lid) & 63u);
+    const uint32_t prev = lds[L_GPS + ((q * 8u + lid) & 63u)];
     const uint32_t cnt = (lid < n && cur > prev) ? cur - prev : 0u;
     const uint32_t np = max(cur, prev);
     const uint32_t t = gather(np, lid & 7u);
-    if ((lid >> 3) == q && (lid & 7u) < n) gps = t;
+    if ((lid >> 3) == q && (lid & 7u) < n) lds[L_GPS + lid] = t;
     uint32_t total = 0;
     for (uint32_t s = 0; s < n; ++s) total += rl(cnt, s);
     if (lid == A_STAB + q) pa += total;
@@ -1469,7 +1510,7 @@ struct Big {
       return;
     }
     const uint32_t vc = (sv(SL_CNT) >> 8) & 0xFFu;
-    deps_total += vc;
+    lds_add64(L_DEPS, vc);
     const uint32_t depj = svl(g.sl_value, vc);
     // every dep's slot tag and record at p in one round trip (lane j: dep j):
     // AEClock::contains (tarjan.rs:131-132: a freed slot was executed
@@ -1610,7 +1651,7 @@ struct Big {
   __device__ __forceinline__ void send_p(uint32_t from, uint32_t to, uint32_t kind, uint32_t dot) {
     XPROF_T0();
     XPROF_CNT(PC_SEND, 1);
-    const uint32_t d = msg_delay(rl(dpq, from * 8u + to));
+    const uint32_t d = msg_delay(dpq_(from * 8u + to));
     push_event(now + d, 0u, kind | (from << 4) | (to << 8), dot);
     XPROF_ADD(PF_SEND);
   }
@@ -1715,7 +1756,7 @@ struct Big {
         const uint32_t issued = rd(CL(c, 1));
         note(4, c + 1, 0, issued);
         const uint32_t lat = now - rd(CL(c, 2));  // latency.as_millis()
-        lat_sum += lat;
+        lds_add64(L_LATSUM, lat);
 #ifndef FX_SIMX_EVLOG
         if (lid == 0 && kx()->latency_log && issued - 1u < kx()->lat_cap)
           kx()->latency_log[((size_t)inst * g.C + c) * kx()->lat_cap + issued - 1u] = lat;
@@ -1830,7 +1871,6 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
   for (uint32_t i = s.lid; i < LDS_WORDS; i += 64) smem[i] = 0;
   for (uint32_t i = s.lid; i < g.NS; i += 64) M[g.o_slot + i * g.SW + SL_DOT] = 0;
   for (uint32_t i = s.lid; i < g.n * g.ncli_keys * 2u; i += 64) M[g.o_kd + i] = 0;
-  for (uint32_t i = s.lid; i < g.n * g.n * g.n; i += 64) M[g.o_gco + i] = 0;
   for (uint32_t i = s.lid; i < g.R; i += 64) {
     M[g.o_kh + i] = NONE;
     M[g.o_kl + i] = NONE;
@@ -1856,7 +1896,7 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
     const uint32_t wqm = (uint32_t)bal(s.lid < n && pos < wq);
     const uint32_t mqm = (uint32_t)bal(s.lid < n && pos < maj);
     s.lset(s.pa, s.A_Q + p, fqm | (wqm << 8) | (mqm << 16));
-    if (s.lid >= p * 8u && s.lid < p * 8u + n) s.dpq = a.ping[rp * RP + sp.process_regions[s.lid - p * 8u]] / 2u;
+    if (s.lid >= p * 8u && s.lid < p * 8u + n) smem[L_DPQ + s.lid] = a.ping[rp * RP + sp.process_regions[s.lid - p * 8u]] / 2u;
   }
   // clients: for region in client_regions, clients_per_region each (runner.rs:143-163)
   {
@@ -1924,7 +1964,7 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
     else s.client_send(c);
   }
   // ------------------------------------------------------------ loop
-  const uint64_t max_events = a.max_events ? a.max_events : 0xFFFFFFFFull;
+  const uint32_t max_events = a.max_events ? a.max_events : 0xFFFFFFFFu;
 #ifdef FX_SIMX_EVLOG
   uint32_t evn = 0;
 #endif
@@ -2019,8 +2059,8 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
       st[FX_SIM_STAT_END_MS] = s.now;
       st[FX_SIM_STAT_TRACE] = s.trace;
       st[FX_SIM_STAT_SEQ] = s.seq;
-      st[FX_SIM_STAT_DEPS] = s.deps_total;
-      st[FX_SIM_STAT_LAT_SUM] = s.lat_sum;
+      st[FX_SIM_STAT_DEPS] = s.lds64(L_DEPS);
+      st[FX_SIM_STAT_LAT_SUM] = s.lds64(L_LATSUM);
       st[FX_SIM_STAT_ERR_SITE] = s.err_site;
 #ifdef FX_SIM_PROFILE
       for (uint32_t i = 0; i < 24; ++i) st[i] = s.prof[i];
