@@ -283,7 +283,15 @@ enum : uint32_t { PF_POP = 0, PF_EVENT = 1, PF_XADD = 2, PF_FIND = 3, PF_CHECK =
 template <uint32_t NG>
 struct Big {
   // ---------------------------------------------------------------- context
-  uint32_t lid;
+  // the lane id, opaque at every use: expressions of it (lane offsets of the
+  // lane-parallel loads) are recomputed where they are used instead of being
+  // hoisted out of the event loop and held -- or spilled -- for the whole run
+  uint32_t lid_;
+  __device__ __forceinline__ uint32_t lidv() const {
+    uint32_t x = lid_;
+    asm volatile("" : "+v"(x));
+    return x;
+  }
 
   GeoX g;
   uint32_t* M;    // this instance's arena
@@ -333,7 +341,7 @@ struct Big {
   // of the instance (the protocol counters are not written in this build)
   uint32_t cur_info = 0, cur_arg = 0, cur_hi = 0;
   __device__ __forceinline__ void dput(uint32_t i, uint64_t v) {
-    if (lid == 0 && kx()->stats) kx()->stats[(size_t)inst * FX_SIM_STATS + i] = v;
+    if (lidv() == 0 && kx()->stats) kx()->stats[(size_t)inst * FX_SIM_STATS + i] = v;
   }
 #endif
   uint32_t now = 0;  // ms
@@ -390,10 +398,10 @@ struct Big {
   __device__ __forceinline__ uint32_t& W(uint32_t off, uint32_t i) { return M[off + i]; }
   __device__ __forceinline__ uint32_t rd(uint32_t& x) { return uni(x); }
   __device__ __forceinline__ void put(uint32_t& dst, uint32_t v) {
-    if (lid == 0) dst = v;
+    if (lidv() == 0) dst = v;
   }
   __device__ __forceinline__ void lset(uint32_t& reg, uint32_t lane, uint32_t v) {
-    if (lid == lane) reg = v;
+    if (lidv() == lane) reg = v;
   }
   // dot table slot of a dot (direct-mapped per source)
   __device__ __forceinline__ uint32_t hslot(uint32_t d) const {
@@ -425,7 +433,7 @@ struct Big {
     XPROF_T0();
     hsl = sl;
     hpp = p;
-    hrow = lid < HR_S ? (lid < g.SW ? S(sl, lid) : 0u) : RC(sl, p, lid - HR_S);
+    hrow = lidv() < HR_S ? (lidv() < g.SW ? S(sl, lidv()) : 0u) : RC(sl, p, lidv() - HR_S);
 #ifdef FX_SIM_PROFILE
     hrow = uni(hrow) == 0xFFFFFFFFu ? hrow + 1u : hrow;  // (waits for the load inside the bracket)
 #endif
@@ -450,11 +458,11 @@ struct Big {
     put(RC(hsl, hpp, w), v);
     lset(hrow, HR_S + w, v);
   }
-  // lane-parallel read of slot words w0 + lid for lanes with lid < cnt
+  // lane-parallel read of slot words w0 + lidv() for lanes with lidv() < cnt
   __device__ __forceinline__ uint32_t svl(uint32_t w0, uint32_t cnt) {
-    const uint32_t w = w0 + lid;
+    const uint32_t w = w0 + lidv();
     const uint32_t gv = gather(hrow, w & 63u);
-    if (lid >= cnt) return 0u;
+    if (lidv() >= cnt) return 0u;
     return w < HR_S ? gv : S(hsl, w);
   }
   // the copy is valid from a handler's hslot_of to the end of the x_add that
@@ -465,7 +473,7 @@ struct Big {
   __device__ __forceinline__ void hist_chain(uint32_t v) {
     if (!kx()->chain_hist) return;
     const uint32_t b = min(v, kx()->chain_bins - 1u);
-    if (lid == 0) {
+    if (lidv() == 0) {
       if (b < HC_BINS) atomicAdd(&lds[b], 1u);
       else atomicAdd(&kx()->chain_hist[b], 1ull);
     }
@@ -473,7 +481,7 @@ struct Big {
   __device__ __forceinline__ void hist_delay(uint32_t v) {
     if (!kx()->delay_hist) return;
     const uint32_t b = min(v, kx()->delay_bins - 1u);
-    if (lid == 0) {
+    if (lidv() == 0) {
       if (b < HD_BINS) atomicAdd(&lds[HC_BINS + b], 1u);
       else atomicAdd(&kx()->delay_hist[b], 1ull);
     }
@@ -484,7 +492,7 @@ struct Big {
     const uint32_t h = (key * 2654435761u) >> (32 - HL_LOG);
     uint32_t* lc = lds + HC_BINS + HD_BINS;
     const uint32_t k = uni(lc[h]);
-    if (lid == 0) {
+    if (lidv() == 0) {
       if (k == key + 1u) {
         atomicAdd(&lc[HL_SLOTS + h], 1u);
       } else if (k == 0) {
@@ -523,7 +531,7 @@ struct Big {
         return NONE;
       }
       const uint32_t k = min(nfree, FC / 2u);
-      if (lid < k) lds[L_FC + lid] = W(g.o_free, nfree - k + lid);
+      if (lidv() < k) lds[L_FC + lidv()] = W(g.o_free, nfree - k + lidv());
       nfree -= k;
       fcn = k;
     }
@@ -534,7 +542,7 @@ struct Big {
     put(W(g.o_inf, e), info);
     put(W(g.o_arg, e), arg);
     const uint32_t grp = e >> 6;
-    if (lid == (grp & 63u)) {
+    if (lidv() == (grp & 63u)) {
 #pragma unroll
       for (uint32_t k = 0; k < NG; ++k)
         if ((grp >> 6) == k && (hi < gh[k] || (hi == gh[k] && lo < gl[k]))) {
@@ -562,7 +570,7 @@ struct Big {
     const uint32_t tl = dpp_min(bh == th ? bl : NONE);
     const uint32_t ln = ctz64(bal(bh == th && bl == tl));
     const uint32_t grp = rl(bk, ln) * 64u + ln;
-    const uint32_t e0 = grp * 64u + lid;
+    const uint32_t e0 = grp * 64u + lidv();
     uint32_t kh = W(g.o_kh, e0), kl = W(g.o_kl, e0);
     const uint32_t vi = W(g.o_inf, e0), va = W(g.o_arg, e0);
     const uint64_t hit = bal(kh == th && kl == tl);
@@ -577,14 +585,14 @@ struct Big {
     const uint32_t j = ctz64(hit);
     info_out = rl(vi, j);
     arg_out = rl(va, j);
-    if (lid == j) {
+    if (lidv() == j) {
       kh = NONE;
       kl = NONE;
       W(g.o_kh, e0) = NONE;
     }
     const uint32_t nh = dpp_min(kh);
     const uint32_t nl = dpp_min(kh == nh ? kl : NONE);
-    if (lid == (grp & 63u)) {
+    if (lidv() == (grp & 63u)) {
 #pragma unroll
       for (uint32_t k = 0; k < NG; ++k)
         if ((grp >> 6) == k) {
@@ -596,11 +604,11 @@ struct Big {
   }
   __device__ __forceinline__ void free_event(uint32_t e) {
     if (fcn == FC) {  // spill the LDS top's lower half to the HBM stack, in order
-      const uint32_t v = lds[L_FC + lid];  // (lanes < FC)
-      const uint32_t hi = lds[L_FC + ((lid + FC / 2u) & (FC - 1u))];
-      if (lid < FC / 2u) {
-        W(g.o_free, nfree + lid) = v;
-        lds[L_FC + lid] = hi;
+      const uint32_t v = lds[L_FC + lidv()];  // (lanes < FC)
+      const uint32_t hi = lds[L_FC + ((lidv() + FC / 2u) & (FC - 1u))];
+      if (lidv() < FC / 2u) {
+        W(g.o_free, nfree + lidv()) = v;
+        lds[L_FC + lidv()] = hi;
       }
       nfree += FC / 2u;
       fcn = FC / 2u;
@@ -620,7 +628,7 @@ struct Big {
     uint32_t bad = 0, first = NONE, fh = 0, fl = 0, ah = 0, al = 0;
     const uint32_t ngr = g.R >> 6;
     for (uint32_t g2 = 0; g2 < ngr; ++g2) {
-      const uint32_t h2 = W(g.o_kh, g2 * 64u + lid), l2 = W(g.o_kl, g2 * 64u + lid);
+      const uint32_t h2 = W(g.o_kh, g2 * 64u + lidv()), l2 = W(g.o_kl, g2 * 64u + lidv());
       const uint32_t mh = dpp_min(h2), ml = dpp_min(h2 == mh ? l2 : NONE);
       uint32_t sh = NONE, slo = NONE;
 #pragma unroll
@@ -647,7 +655,7 @@ struct Big {
     uint32_t junk = 0, jv = 0, jl = 0;
 #pragma unroll
     for (uint32_t k = 0; k < NG; ++k) {
-      const bool off = k * 64u + lid >= ngr;
+      const bool off = k * 64u + lidv() >= ngr;
       const uint64_t m = bal(off && (gh[k] != NONE || gl[k] != NONE));
       if (m && !junk) {
         jl = k * 64u + ctz64(m);
@@ -742,9 +750,9 @@ struct Big {
       put(KD(p, key1, ro ? 1u : 0u), dot);
     }
     const bool reads = !ro && !nfr;
-    const uint32_t i = lid - npast;
+    const uint32_t i = lidv() - npast;
     uint32_t v = 0;
-    if (lid < npast) v = pastv;
+    if (lidv() < npast) v = pastv;
     else if (i == 0) v = w0;
     else if (i == 1) v = reads ? r0 : 0u;
     else if (i == 2) v = w1;
@@ -754,7 +762,7 @@ struct Big {
     const uint64_t vm = bal(valid);
     for (uint64_t m = vm; m; m &= m - 1) {
       const uint32_t j = ctz64(m);
-      if (j < lid && rl(v, j) == v) first = false;
+      if (j < lidv() && rl(v, j) == v) first = false;
     }
     const uint64_t fm = bal(first);
     uint32_t rank = 0;
@@ -763,7 +771,7 @@ struct Big {
     for (uint64_t m = fm; m; m &= m - 1) {
       const uint32_t j = ctz64(m);
       const uint32_t vj = rl(v, j), rj = rl(rank, j);
-      if (lid == rj) outv = vj;
+      if (lidv() == rj) outv = vj;
     }
     return pop64(fm);
   }
@@ -793,8 +801,8 @@ struct Big {
     const uint32_t qw = rl(pa, A_Q + p);
     const uint32_t qm = (nfr && ro && nk == 1) ? (qw >> 16) & 0xFFu : qw & 0xFFu;
     // the fresh slot in one lane-parallel pass, and its per-process records
-    const uint32_t dv = gather(depv, (lid - SL_COLLECT) & 63u);
-    for (uint32_t i = lid; i < g.SW; i += 64) {
+    const uint32_t dv = gather(depv, (lidv() - SL_COLLECT) & 63u);
+    for (uint32_t i = lidv(); i < g.SW; i += 64) {
       uint32_t v = 0;
       if (i == SL_DOT) v = dot;
       else if (i == SL_CLIENT) v = c;
@@ -805,8 +813,8 @@ struct Big {
       else if (i >= SL_COLLECT && i < SL_COLLECT + nd) v = dv;
       S(sl, i) = v;
     }
-    for (uint32_t i = lid; i < g.n * RW; i += 64) M[g.o_rec + sl * g.n * RW + i] = 0;
-    if (kx()->dot_client && s <= kx()->exec_cap && lid == 0)
+    for (uint32_t i = lidv(); i < g.n * RW; i += 64) M[g.o_rec + sl * g.n * RW + i] = 0;
+    if (kx()->dot_client && s <= kx()->exec_cap && lidv() == 0)
       kx()->dot_client[((size_t)inst * n + p) * kx()->exec_cap + s - 1u] = c + 1u;
     act_send(basic ? M_STORE : M_COLLECT, dot, (1u << n) - 1u);
   }
@@ -865,8 +873,8 @@ struct Big {
     const uint32_t c = sv(SL_CLIENT);
     const uint32_t nk = (sv(SL_CNT) >> 16) & 3u;
     const uint32_t x0 = rl(pa, A_EXEC + p);
-    if (lid < nk && kx()->executed && x0 + lid < kx()->exec_cap)
-      kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + x0 + lid] = dot;
+    if (lidv() < nk && kx()->executed && x0 + lidv() < kx()->exec_cap)
+      kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + x0 + lidv()] = dot;
     lset(pa, A_EXEC + p, x0 + nk);
     if ((rd(CL(c, 0)) & 0xFFu) == p) client_result(c, nk);  // pending.wait_for registered this rifl at p
     if (err) return;
@@ -916,7 +924,7 @@ struct Big {
       return;
     }
     rput(R_PST, (ps & ~3u) | ST_COLLECT);
-    if (lid < g.amax) S(sl, g.sl_ack + p * g.amax + lid) = lid < nd ? depv : 0u;
+    if (lidv() < g.amax) S(sl, g.sl_ack + p * g.amax + lidv()) = lidv() < nd ? depv : 0u;
     if (protocol == FX_PROTOCOL_EPAXOS && from_self) return;  // epaxos.rs:290-300
     act_send(M_COLLECT_ACK, dot, 1u << from);
   }
@@ -940,7 +948,7 @@ struct Big {
     if (pop32(part) != fq_eff) return;
     // QuorumDeps: union + per-dep report counts; lanes [q amax, (q + 1) amax)
     // hold process q's reported deps
-    const uint32_t q = lid / g.amax, j = lid % g.amax;
+    const uint32_t q = lidv() / g.amax, j = lidv() % g.amax;
     const uint32_t aw = g.sl_ack + q * g.amax + j;
     const uint32_t ag = gather(hrow, aw & 63u);
     uint32_t v = 0;
@@ -954,7 +962,7 @@ struct Big {
       const uint32_t v2 = rl(v, l2);
       if (valid && v2 == v) {
         ++cnt;
-        if (l2 < lid) first = false;
+        if (l2 < lidv()) first = false;
       }
     }
     const uint64_t um = bal(first);
@@ -977,7 +985,7 @@ struct Big {
     sput(SL_CNT, (c0 & ~0xFF00u) | (nu << 8) | (fast ? 0u : (1u << 19)));
     const bool ro = (c0 >> 18) & 1u;
     // BaseProcess::path (base.rs:229-243): Fast / Slow at p, and their read-only shares
-    if (lid == (fast ? A_FAST : A_SLOW) + p || (ro && lid == (fast ? A_FR : A_SR) + p)) ++pa;
+    if (lidv() == (fast ? A_FAST : A_SLOW) + p || (ro && lidv() == (fast ? A_FR : A_SR) + p)) ++pa;
     if (fast) act_send(M_COMMIT, dot, (1u << n) - 1u);
     else act_send(M_CONSENSUS, dot, (rl(pa, A_Q + p) >> 8) & 0xFFu);  // skip_prepare: ballot = coordinator
   }
@@ -1072,13 +1080,13 @@ struct Big {
   // periodic GarbageCollection at p (atlas.rs:699-714): MGarbageCollection
   // with p's committed frontier to every other process (ascending)
   __device__ __forceinline__ void gc_tick(uint32_t p) {
-    const uint32_t fv = lds[L_GCF + ((p * 8u + lid) & 63u)];  // lane s: frontier of source s + 1
+    const uint32_t fv = lds[L_GCF + ((p * 8u + lidv()) & 63u)];  // lane s: frontier of source s + 1
     for (uint32_t q = 0; q < n && !err; ++q) {
       if (q == p) continue;
       const uint32_t d = msg_delay(dpq_(p * 8u + q));
       const uint32_t e = push_event(now + d, (2u << 6) | (p << 3) | q, M_GC | (p << 4) | (q << 8), 0);
       if (e == NONE) return;
-      if (lid < n) W(g.o_gp, e * n + lid) = fv;
+      if (lidv() < n) W(g.o_gp, e * n + lidv()) = fv;
     }
   }
   // MGarbageCollection at q from `from` (gc/clock.rs:50-138): merge the
@@ -1090,33 +1098,33 @@ struct Big {
     // r n + s = source s + 1) in one lane-parallel load; the report from
     // `from` is merged in registers and written back
     const uint32_t nn = n * n, base = L_GCO + q * nn;
-    uint32_t blk = lid < nn ? lds[base + lid] : 0u;
-    const uint32_t row = lid / n, src = lid - row * n;
+    uint32_t blk = lidv() < nn ? lds[base + lidv()] : 0u;
+    const uint32_t row = lidv() / n, src = lidv() - row * n;
     const uint32_t vs = gather(v, src & 63u);
-    if (lid < nn && row == from) {
+    if (lidv() < nn && row == from) {
       blk = max(blk, vs);
-      lds[base + lid] = blk;
+      lds[base + lidv()] = blk;
     }
     const uint32_t rep = rl(pb, B_REP + q) | (1u << from);
     lset(pb, B_REP + q, rep);
     uint32_t cur = 0;
-    const uint32_t mine = lds[L_GCF + ((q * 8u + lid) & 63u)];
+    const uint32_t mine = lds[L_GCF + ((q * 8u + lidv()) & 63u)];
     if (pop32(rep) == n - 1u) {
-      cur = lid < n ? mine : 0u;
+      cur = lidv() < n ? mine : 0u;
       for (uint32_t r = 0; r < n; ++r) {
         if (r == q) continue;
-        const uint32_t o = gather(blk, (r * n + lid) & 63u);
-        if (lid < n) cur = min(cur, o);
+        const uint32_t o = gather(blk, (r * n + lidv()) & 63u);
+        if (lidv() < n) cur = min(cur, o);
       }
     }
-    const uint32_t prev = lds[L_GPS + ((q * 8u + lid) & 63u)];
-    const uint32_t cnt = (lid < n && cur > prev) ? cur - prev : 0u;
+    const uint32_t prev = lds[L_GPS + ((q * 8u + lidv()) & 63u)];
+    const uint32_t cnt = (lidv() < n && cur > prev) ? cur - prev : 0u;
     const uint32_t np = max(cur, prev);
-    const uint32_t t = gather(np, lid & 7u);
-    if ((lid >> 3) == q && (lid & 7u) < n) lds[L_GPS + lid] = t;
+    const uint32_t t = gather(np, lidv() & 7u);
+    if ((lidv() >> 3) == q && (lidv() & 7u) < n) lds[L_GPS + lidv()] = t;
     uint32_t total = 0;
     for (uint32_t s = 0; s < n; ++s) total += rl(cnt, s);
-    if (lid == A_STAB + q) pa += total;
+    if (lidv() == A_STAB + q) pa += total;
   }
 
   // ===================================================== GraphExecutor
@@ -1132,7 +1140,7 @@ struct Big {
   // AggregatePending (runner.rs:406-424), executor metrics, execution log
   __device__ __forceinline__ void on_execute(uint32_t sl, uint32_t d, uint32_t start) {
     const uint32_t p = xp;
-    if (xk < kx()->exec_cap && kx()->executed && lid == 0) kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + xk] = d;
+    if (xk < kx()->exec_cap && kx()->executed && lidv() == 0) kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + xk] = d;
     ++xk;
     hist_delay(now - start);  // ExecutionDelay (graph/mod.rs:514-518)
     if (rd(RC(sl, p, R_WAIT))) unlink(sl);
@@ -1198,12 +1206,12 @@ struct Big {
       return;
     }
     for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
-      const uint32_t i = i0 + lid;
+      const uint32_t i = i0 + lidv();
       const uint32_t msl = i < cnt ? W(src, i) : 0u;
       const uint32_t md = i < cnt ? S(msl, SL_DOT) : NONE;
       uint32_t rank = 0;
       for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
-        const uint32_t k = k0 + lid;
+        const uint32_t k = k0 + lidv();
         const uint32_t kd = k0 == i0 ? md : (k < cnt ? S(W(src, k), SL_DOT) : NONE);
         const uint32_t m = min(64u, cnt - k0);
         for (uint32_t j = 0; j < m; ++j) rank += rl(kd, j) < md ? 1u : 0u;
@@ -1234,7 +1242,7 @@ struct Big {
     }
     const uint32_t p = xp;
     for (uint32_t r0 = 0; r0 < cnt && !err; r0 += 64) {
-      const uint32_t r = r0 + lid;
+      const uint32_t r = r0 + lidv();
       const bool act = r < cnt;
       uint32_t sl = 0, d = 0, st = 0, wt = 0, c = 0, cw = 0, mk = 0;
       if (act) {
@@ -1249,8 +1257,8 @@ struct Big {
       const uint32_t cpr = act ? CL(c, 0) : 0u;
       const uint32_t m = min(64u, cnt - r0);
       if (act) {
-        if (kx()->executed && xk + lid < kx()->exec_cap) kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + xk + lid] = d;
-        W(g.o_wl, nwl + lid) = sl;
+        if (kx()->executed && xk + lidv() < kx()->exec_cap) kx()->executed[((size_t)inst * n + p) * kx()->exec_cap + xk + lidv()] = d;
+        W(g.o_wl, nwl + lidv()) = sl;
         if (kx()->delay_hist) {  // ExecutionDelay (graph/mod.rs:514-518)
           const uint32_t bn = min(now - st, kx()->delay_bins - 1u);
           if (bn < HD_BINS) atomicAdd(&lds[HC_BINS + bn], 1u);
@@ -1277,7 +1285,7 @@ struct Big {
   __device__ __forceinline__ void dep_states(uint32_t drow, uint32_t ci, uint32_t cnd, uint32_t& ptag,
                                              uint32_t& ppst, uint32_t& ptl, uint32_t& pmk) {
     ptag = ppst = ptl = pmk = 0;
-    if (lid >= ci && lid < cnd && src_ok(drow)) {
+    if (lidv() >= ci && lidv() < cnd && src_ok(drow)) {
       const uint32_t sl = hslot(drow);
       ptag = S(sl, SL_DOT);
       ppst = RC(sl, xp, R_PST);
@@ -1288,10 +1296,10 @@ struct Big {
   // a vertex's dot, dep count and dep row (lane j = dep j), loaded together
   __device__ __forceinline__ void frame_row(uint32_t sl, uint32_t& cdot, uint32_t& cnd, uint32_t& drow) {
     const uint32_t t = S(sl, SL_DOT), cw = S(sl, SL_CNT);
-    drow = lid < g.vmax ? S(sl, g.sl_value + lid) : 0u;
+    drow = lidv() < g.vmax ? S(sl, g.sl_value + lidv()) : 0u;
     cdot = uni(t);
     cnd = (uni(cw) >> 8) & 0xFFu;
-    if (lid >= cnd) drow = 0;
+    if (lidv() >= cnd) drow = 0;
   }
 
   // find_scc (mod.rs:409-486) + strong_connect (tarjan.rs:96-316) + finalize
@@ -1381,7 +1389,7 @@ struct Big {
       if (cid == lowv) {  // SCC root: pop the members tstk[ctp, tsp) (tarjan.rs:233-312)
         bool broken = false;
         for (uint32_t i0 = ctp; i0 < tsp; i0 += 64) {
-          const uint32_t i = i0 + lid;
+          const uint32_t i = i0 + lidv();
           uint32_t psx = PS_INGRAPH;
           if (i < tsp) {
             const uint32_t x = W(g.o_tstk, i);
@@ -1399,7 +1407,7 @@ struct Big {
             dput(8, rsl | ((uint64_t)tsp << 32));
             dput(9, ctp | ((uint64_t)cv << 32));
             for (uint32_t i0 = ctp; i0 < tsp; i0 += 64) {
-              const uint32_t i = i0 + lid;
+              const uint32_t i = i0 + lidv();
               const uint32_t x = i < tsp ? W(g.o_tstk, i) : 0u;
               const uint32_t psx = i < tsp ? RC(x, p, R_PST) : PS_INGRAPH;
               const uint64_t m = bal((psx & (PS_INGRAPH | PS_EXEC)) != PS_INGRAPH);
@@ -1446,7 +1454,7 @@ struct Big {
     // finalize: ids of the vertices left on the stack; failed searches mark them visited
     const bool markit = mark_epoch && result == MISSING;
     for (uint32_t i0 = 0; i0 < tsp; i0 += 64) {
-      const uint32_t i = i0 + lid;
+      const uint32_t i = i0 + lidv();
       if (i < tsp) {
         const uint32_t x = W(g.o_tstk, i);
         RC(x, p, R_TL) = 0u;
@@ -1516,7 +1524,7 @@ struct Big {
     // AEClock::contains (tarjan.rs:131-132: a freed slot was executed
     // everywhere) and the search-result cache words below
     uint32_t dtag = 0, dps = 0, dcm = 0, dce = 0;
-    const bool dl = lid < vc && depj != d && src_ok(depj);
+    const bool dl = lidv() < vc && depj != d && src_ok(depj);
     if (dl) {
       const uint32_t dsl = hslot(depj);
       dtag = S(dsl, SL_DOT);
@@ -1525,7 +1533,7 @@ struct Big {
       dce = RC(dsl, p, R_CEPOCH);
     }
     bool keep = false;
-    if (lid < vc && depj != d) keep = !src_ok(depj) || (dtag == depj && !(dps & PS_EXEC));
+    if (lidv() < vc && depj != d) keep = !src_ok(depj) || (dtag == depj && !(dps & PS_EXEC));
     bool first = bal(keep) != 0;
     if (!first) {  // every dep executed: a singleton SCC
       XPROF_CNT(PC_FAST, 1);
@@ -1587,13 +1595,13 @@ struct Big {
           if (wbase == NONE || wk >= wbase + 64u) {
             wbase = wk;
             wps = wmk = 0;
-            if (wbase + lid < wcnt) {
-              const uint32_t w = W(g.o_tw, wbase + lid);
+            if (wbase + lidv() < wcnt) {
+              const uint32_t w = W(g.o_tw, wbase + lidv());
               wps = RC(w, p, R_PST);
               wmk = RC(w, p, R_MARK);
             }
           }
-          const uint64_t ok = bal(lid >= wk - wbase && wbase + lid < wcnt && !(wps & PS_EXEC) &&
+          const uint64_t ok = bal(lidv() >= wk - wbase && wbase + lidv() < wcnt && !(wps & PS_EXEC) &&
                                   (wmk >> 1) != cur);
           if (!ok) {
             wk = wbase + 64u;
@@ -1758,7 +1766,7 @@ struct Big {
         const uint32_t lat = now - rd(CL(c, 2));  // latency.as_millis()
         lds_add64(L_LATSUM, lat);
 #ifndef FX_SIMX_EVLOG
-        if (lid == 0 && kx()->latency_log && issued - 1u < kx()->lat_cap)
+        if (lidv() == 0 && kx()->latency_log && issued - 1u < kx()->lat_cap)
           kx()->latency_log[((size_t)inst * g.C + c) * kx()->lat_cap + issued - 1u] = lat;
 #endif
         hist_lat(rd(CL(c, 0)) >> 8, lat);
@@ -1835,7 +1843,7 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
   } else {
     s.g = a.g;
   }
-  s.lid = threadIdx.x & 63u;
+  s.lid_ = threadIdx.x & 63u;
   s.M = a.arena + (size_t)inst * s.g.words;
   s.lds = smem;
   s.inst = inst;
@@ -1868,10 +1876,10 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
   const GeoX& g = a.g;
   uint32_t* M = s.M;
   // ---------------------------------------------------------------- init
-  for (uint32_t i = s.lid; i < LDS_WORDS; i += 64) smem[i] = 0;
-  for (uint32_t i = s.lid; i < g.NS; i += 64) M[g.o_slot + i * g.SW + SL_DOT] = 0;
-  for (uint32_t i = s.lid; i < g.n * g.ncli_keys * 2u; i += 64) M[g.o_kd + i] = 0;
-  for (uint32_t i = s.lid; i < g.R; i += 64) {
+  for (uint32_t i = s.lidv(); i < LDS_WORDS; i += 64) smem[i] = 0;
+  for (uint32_t i = s.lidv(); i < g.NS; i += 64) M[g.o_slot + i * g.SW + SL_DOT] = 0;
+  for (uint32_t i = s.lidv(); i < g.n * g.ncli_keys * 2u; i += 64) M[g.o_kd + i] = 0;
+  for (uint32_t i = s.lidv(); i < g.R; i += 64) {
     M[g.o_kh + i] = NONE;
     M[g.o_kl + i] = NONE;
     M[g.o_free + i] = g.R - 1u - i;  // free stack
@@ -1885,18 +1893,18 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
   for (uint32_t p = 0; p < n; ++p) {
     const uint32_t rp = sp.process_regions[p];
     uint32_t pos = 0;
-    if (s.lid < n) {
-      const uint32_t kq = a.rank[rp * RP + sp.process_regions[s.lid]];
+    if (s.lidv() < n) {
+      const uint32_t kq = a.rank[rp * RP + sp.process_regions[s.lidv()]];
       for (uint32_t q2 = 0; q2 < n; ++q2) {
         const uint32_t k2 = a.rank[rp * RP + sp.process_regions[q2]];
-        if (k2 < kq || (k2 == kq && q2 < s.lid)) ++pos;
+        if (k2 < kq || (k2 == kq && q2 < s.lidv())) ++pos;
       }
     }
-    const uint32_t fqm = (uint32_t)bal(s.lid < n && pos < fq);
-    const uint32_t wqm = (uint32_t)bal(s.lid < n && pos < wq);
-    const uint32_t mqm = (uint32_t)bal(s.lid < n && pos < maj);
+    const uint32_t fqm = (uint32_t)bal(s.lidv() < n && pos < fq);
+    const uint32_t wqm = (uint32_t)bal(s.lidv() < n && pos < wq);
+    const uint32_t mqm = (uint32_t)bal(s.lidv() < n && pos < maj);
     s.lset(s.pa, s.A_Q + p, fqm | (wqm << 8) | (mqm << 16));
-    if (s.lid >= p * 8u && s.lid < p * 8u + n) smem[L_DPQ + s.lid] = a.ping[rp * RP + sp.process_regions[s.lid - p * 8u]] / 2u;
+    if (s.lidv() >= p * 8u && s.lidv() < p * 8u + n) smem[L_DPQ + s.lidv()] = a.ping[rp * RP + sp.process_regions[s.lidv() - p * 8u]] / 2u;
   }
   // clients: for region in client_regions, clients_per_region each (runner.rs:143-163)
   {
@@ -1913,7 +1921,7 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
       }
       const uint32_t dcs = a.ping[rc * RP + sp.process_regions[best]] / 2u;
       const uint32_t dcr = a.ping[sp.process_regions[best] * RP + rc] / 2u;
-      for (uint32_t i = s.lid; i < sp.clients_per_region; i += 64) {
+      for (uint32_t i = s.lidv(); i < sp.clients_per_region; i += 64) {
         const uint32_t c = c0 + i;
         M[g.o_cl + c * 8u + 0] = best | (rc << 8);
         M[g.o_cl + c * 8u + 1] = 0;
@@ -1938,7 +1946,7 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
   // kernel did not make (or a stray one of its own) shows up at its event
   const uint32_t can_v = 0xC0FFEE00u | (inst & 0xFFu);
   const uint32_t can_a = g.o_cl + 6u, can_b = g.o_cl + (s.C - 1u) * 8u + 7u, can_c = g.o_rdy + s.C + 63u;
-  if (s.lid == 0) {
+  if (s.lidv() == 0) {
     M[can_a] = can_v;
     M[can_b] = can_v;
     M[can_c] = can_v;
@@ -1991,7 +1999,7 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
     }
     s.now = t;
     const uint32_t kind = info & 15u, from = (info >> 4) & 15u, to = (info >> 8) & 15u;
-    const uint32_t gcv = kind == M_GC && s.lid < n ? M[g.o_gp + e * n + s.lid] : 0u;
+    const uint32_t gcv = kind == M_GC && s.lidv() < n ? M[g.o_gp + e * n + s.lidv()] : 0u;
 #ifdef FX_SIMX_DIAG
     s.cur_info = info;
     s.cur_arg = arg;
@@ -2013,7 +2021,7 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
 #ifdef FX_SIMX_EVLOG
     // debug build (tools/simx_repro.py): every event's key, info, argument and
     // the trace hash after it, into the instance's latency-log region
-    if (s.lid == 0 && a.latency_log && 4ull * evn + 3ull < (uint64_t)g.C * a.lat_cap) {
+    if (s.lidv() == 0 && a.latency_log && 4ull * evn + 3ull < (uint64_t)g.C * a.lat_cap) {
       uint32_t* lg = a.latency_log + (size_t)inst * g.C * a.lat_cap + 4ull * evn;
       lg[0] = hi;
       lg[1] = info;
@@ -2036,25 +2044,25 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
   } else {
     __syncthreads();
   }
-  const uint32_t o_exec = gather(s.pa, (s.A_EXEC + s.lid) & 63u), o_fast = gather(s.pa, (s.A_FAST + s.lid) & 63u),
-                 o_slow = gather(s.pa, (s.A_SLOW + s.lid) & 63u), o_stab = gather(s.pa, (s.A_STAB + s.lid) & 63u),
-                 o_fr = gather(s.pa, (s.A_FR + s.lid) & 63u), o_sr = gather(s.pa, (s.A_SR + s.lid) & 63u);
-  if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = o_exec;
+  const uint32_t o_exec = gather(s.pa, (s.A_EXEC + s.lidv()) & 63u), o_fast = gather(s.pa, (s.A_FAST + s.lidv()) & 63u),
+                 o_slow = gather(s.pa, (s.A_SLOW + s.lidv()) & 63u), o_stab = gather(s.pa, (s.A_STAB + s.lidv()) & 63u),
+                 o_fr = gather(s.pa, (s.A_FR + s.lidv()) & 63u), o_sr = gather(s.pa, (s.A_SR + s.lidv()) & 63u);
+  if (s.lidv() < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lidv()] = o_exec;
   if (a.stats) {
     unsigned long long* st = a.stats + (size_t)inst * FX_SIM_STATS;
 #ifdef FX_SIMX_DIAG
     if (false) {
 #else
-    if (s.lid < NMAX) {
+    if (s.lidv() < NMAX) {
 #endif
-      const bool v = s.lid < n;
-      st[FX_SIM_STAT_FAST + s.lid] = v ? o_fast : 0u;
-      st[FX_SIM_STAT_SLOW + s.lid] = v ? o_slow : 0u;
-      st[FX_SIM_STAT_STABLE + s.lid] = v ? o_stab : 0u;
-      st[FX_SIM_STAT_FAST_READS + s.lid] = v ? o_fr : 0u;
-      st[FX_SIM_STAT_SLOW_READS + s.lid] = v ? o_sr : 0u;
+      const bool v = s.lidv() < n;
+      st[FX_SIM_STAT_FAST + s.lidv()] = v ? o_fast : 0u;
+      st[FX_SIM_STAT_SLOW + s.lidv()] = v ? o_slow : 0u;
+      st[FX_SIM_STAT_STABLE + s.lidv()] = v ? o_stab : 0u;
+      st[FX_SIM_STAT_FAST_READS + s.lidv()] = v ? o_fr : 0u;
+      st[FX_SIM_STAT_SLOW_READS + s.lidv()] = v ? o_sr : 0u;
     }
-    if (s.lid == 0) {
+    if (s.lidv() == 0) {
       st[FX_SIM_STAT_EVENTS] = s.events;
       st[FX_SIM_STAT_END_MS] = s.now;
       st[FX_SIM_STAT_TRACE] = s.trace;
@@ -2067,7 +2075,7 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
 #endif
     }
   }
-  for (uint32_t i = s.lid; i < HC_BINS + HD_BINS; i += 64) {
+  for (uint32_t i = s.lidv(); i < HC_BINS + HD_BINS; i += 64) {
     const uint32_t c = smem[i];
     if (!c) continue;
     if (i < HC_BINS) {
@@ -2076,12 +2084,12 @@ __global__ __launch_bounds__(64 * WPB, GS != 0 ? FX_SIMX_WAVES_GS : FX_SIMX_WAVE
       atomicAdd(&a.delay_hist[i - HC_BINS], (unsigned long long)c);
     }
   }
-  for (uint32_t i = s.lid; i < HL_SLOTS; i += 64) {
+  for (uint32_t i = s.lidv(); i < HL_SLOTS; i += 64) {
     const uint32_t k = smem[HC_BINS + HD_BINS + i];
     if (k && a.lat_hist)
       atomicAdd(&a.lat_hist[k - 1u], (unsigned long long)smem[HC_BINS + HD_BINS + HL_SLOTS + i]);
   }
-  if (s.lid == 0) a.err[inst] = s.err;
+  if (s.lidv() == 0) a.err[inst] = s.err;
 }
 
 }  // namespace simx
