@@ -302,7 +302,15 @@ template <uint32_t HM, uint32_t DS, uint32_t NX, class GP>
 struct Sim : GP {
   using GP::g;
   // ---------------------------------------------------------------- context
-  uint32_t lid;
+  // the lane id, opaque at every use: expressions of it are recomputed where
+  // they are used instead of being hoisted out of the event loop and held --
+  // or spilled -- for the whole run
+  uint32_t lid_;
+  __device__ __forceinline__ uint32_t lidv() const {
+    uint32_t x = lid_;
+    asm volatile("" : "+v"(x));
+    return x;
+  }
   uint32_t* lds;
   uint32_t protocol, n, f, synod_f, fq, wq;
   // Per-instance parameters and rarely changed values in lanes of one VGPR
@@ -337,7 +345,7 @@ struct Sim : GP {
     return (uint64_t)prm(k) | ((uint64_t)prm(k + 1) << 32);
   }
   __device__ __forceinline__ void prm_set(uint32_t k, uint32_t x) {
-    if (lid == k) pv = x;
+    if (lidv() == k) pv = x;
   }
   uint32_t C;
   uint32_t err = 0;
@@ -437,7 +445,7 @@ struct Sim : GP {
   __device__ __forceinline__ void slot_set(uint32_t sl, uint32_t d) {
 #pragma unroll
     for (uint32_t k = 0; k < DS; ++k)
-      if ((sl >> 6) == k && lid == (sl & 63u)) sdv[k] = d;
+      if ((sl >> 6) == k && lidv() == (sl & 63u)) sdv[k] = d;
   }
   __device__ __forceinline__ uint32_t slot_alloc() const {
 #pragma unroll
@@ -463,8 +471,8 @@ struct Sim : GP {
   // executed command a device-scope atomic on the same few bins.
   __device__ __forceinline__ void hist_chain(uint32_t v) {
     if (v < HC_BINS) {
-      hcv += lid == v ? 1u : 0u;
-    } else if (lid == 0) {
+      hcv += lidv() == v ? 1u : 0u;
+    } else if (lidv() == 0) {
       KSimArgs* k = kargs();
       if (k->chain_hist) atomicAdd(&k->chain_hist[min(v, k->chain_bins - 1u)], 1ull);
     }
@@ -477,7 +485,7 @@ struct Sim : GP {
     const uint32_t h = (key * 2654435761u) >> 26;
     const uint32_t k = rl(hlk, h);
     if (k == key + 1u || k == 0) {
-      if (lid == h) {
+      if (lidv() == h) {
         hlk = key + 1u;
         ++hlc;
       }
@@ -486,7 +494,7 @@ struct Sim : GP {
     }
   }
   __device__ __forceinline__ void flush_lat(uint32_t key, uint32_t cnt) {
-    if (lid == 0) {
+    if (lidv() == 0) {
       KSimArgs* k = kargs();
       const uint32_t lat = key & 0xFFFFFFu, bins = k->lat_bins;
       if (k->lat_hist) atomicAdd(&k->lat_hist[(key >> 24) * bins + min(lat, bins - 1u)], (unsigned long long)cnt);
@@ -497,8 +505,8 @@ struct Sim : GP {
     return;
 #endif
     if (v < HD_BINS) {
-      if (lid == 0) atomicAdd(&lds[g.off_hist + v], 1u);
-    } else if (lid == 0) {
+      if (lidv() == 0) atomicAdd(&lds[g.off_hist + v], 1u);
+    } else if (lidv() == 0) {
       KSimArgs* k = kargs();
       if (k->delay_hist) atomicAdd(&k->delay_hist[min(v, k->delay_bins - 1u)], 1ull);
     }
@@ -519,7 +527,7 @@ struct Sim : GP {
   __device__ __forceinline__ void put(uint32_t& dst, uint32_t v) { dst = v; }
   // set lane `lane` of a lane table
   __device__ __forceinline__ void lset(uint32_t& reg, uint32_t lane, uint32_t v) {
-    if (lid == lane) reg = v;
+    if (lidv() == lane) reg = v;
   }
 
   // ------------------------------------------------------------- links
@@ -532,7 +540,7 @@ struct Sim : GP {
 
   __device__ __forceinline__ void head_set(uint32_t link, uint32_t t, uint32_t s) {
     const uint32_t ln = link & 63u, h = link >> 6;
-    if (lid == ln) {
+    if (lidv() == ln) {
 #pragma unroll
       for (uint32_t k = 0; k < HM; ++k)
         if (h == k) {
@@ -598,15 +606,15 @@ struct Sim : GP {
       fail_cap(__LINE__);
       return;
     }
-    const bool tq = lid < 8u && ((mask >> lid) & 1u);
-    const uint32_t r = pop32(mask & (lid < 8u ? (1u << lid) - 1u : 0u));
-    const uint32_t t = now + gather(dpq, (p * 8u + lid) & 63u);  // lane q: now + d(p, q)
+    const bool tq = lidv() < 8u && ((mask >> lidv()) & 1u);
+    const uint32_t r = pop32(mask & (lidv() < 8u ? (1u << lidv()) - 1u : 0u));
+    const uint32_t t = now + gather(dpq, (p * 8u + lidv()) & 63u);  // lane q: now + d(p, q)
     if (bal(tq && t >= (1u << 28))) {
       err = FX_ERR_TIME_RANGE;
       return;
     }
     const uint32_t base = p * (g.n - 1u);
-    const uint32_t rh = gather(rhv, (base + (lid < p ? lid : lid - 1u)) & 63u);  // lane q: link (p, q)'s list
+    const uint32_t rh = gather(rhv, (base + (lidv() < p ? lidv() : lidv() - 1u)) & 63u);  // lane q: link (p, q)'s list
     const uint32_t head = rh & 0xFFFFu;
     uint32_t e = 0;
     if (tq) {
@@ -622,8 +630,8 @@ struct Sim : GP {
     // lane base + i = link (p, q(i)) takes lane q(i)'s values: the new list
     // word, and time (28 bits) | rank << 28 | link was empty << 31 in one word
     const uint32_t tw = t | (r << 28) | (head == LNIL ? 1u << 31 : 0u);
-    const uint32_t i = lid - base;
-    const bool ll = lid >= base && i < g.n - 1u;
+    const uint32_t i = lidv() - base;
+    const bool ll = lidv() >= base && i < g.n - 1u;
     const uint32_t q = (ll ? (i < p ? i : i + 1u) : 0u) & 63u;
     const uint32_t v_nrh = gather(nrh, q), v_tw = gather(tw, q);
     if (ll && ((mask >> q) & 1u)) {
@@ -702,13 +710,13 @@ struct Sim : GP {
     }
     // candidates: lanes [0, npast) the past deps, lane npast / npast + 1 the
     // latest writes of the keys; the result is their sorted distinct set
-    const uint32_t v = lid < npast ? pastv : (lid == npast ? d0 : (lid == npast + 1 ? d1 : 0u));
+    const uint32_t v = lidv() < npast ? pastv : (lidv() == npast ? d0 : (lidv() == npast + 1 ? d1 : 0u));
     const bool valid = v != 0;
     bool first = valid;
     const uint64_t vm = bal(valid);
     for (uint64_t m = vm; m; m &= m - 1) {
       const uint32_t j = ctz64(m);
-      if (j < lid && rl(v, j) == v) first = false;
+      if (j < lidv() && rl(v, j) == v) first = false;
     }
     const uint64_t fm = bal(first);
     uint32_t rank = 0;
@@ -717,7 +725,7 @@ struct Sim : GP {
     for (uint64_t m = fm; m; m &= m - 1) {
       const uint32_t j = ctz64(m);
       const uint32_t vj = rl(v, j), rj = rl(rank, j);
-      if (lid == rj) outv = vj;
+      if (lidv() == rj) outv = vj;
     }
     return pop64(fm);
   }
@@ -734,14 +742,14 @@ struct Sim : GP {
     // the rifl of the dot (Result.rifls / monitors): dot (p, s) was
     // submitted by client c + 1, whose k-th dot is its command k
     const uint32_t inst = prm(P_INST);
-    if (lid == 0) {
+    if (lidv() == 0) {
       KSimArgs* k = kargs();
       if (k->dot_client && s <= k->exec_cap) k->dot_client[((size_t)inst * n + p) * k->exec_cap + s - 1u] = c + 1u;
     }
     uint32_t nk = 0;
     const uint32_t keys = gen_keys(c + 1, idx, nk);
     // fresh slot
-    if (lid < g.slotw) S(sl, lid) = 0;
+    if (lidv() < g.slotw) S(sl, lidv()) = 0;
     slot_set(sl, dot);
     put(S(sl, SL_CLIENT), c);
     put(S(sl, SL_IDX), idx);
@@ -753,7 +761,7 @@ struct Sim : GP {
     }
     uint32_t depv = 0;
     const uint32_t nd = add_cmd(p, dot, keys, nk, 0, 0, depv);
-    if (lid < nd) S(sl, SL_COLLECT + lid) = depv;
+    if (lidv() < nd) S(sl, SL_COLLECT + lidv()) = depv;
     put(S(sl, SL_CNT), (nd << 8) | (nk << 20));
     act_send(M_COLLECT, dot, (1u << n) - 1u);
   }
@@ -796,7 +804,7 @@ struct Sim : GP {
     const uint32_t nk = (uni(S(sl, SL_CNT)) >> 20) & 3u;
     const uint32_t inst = prm(P_INST);
     const uint32_t x0 = rl(pt, PT_EXEC + p);
-    if (lid == 0) {
+    if (lidv() == 0) {
       KSimArgs* k = kargs();
       for (uint32_t j = 0; j < nk; ++j)
         if (x0 + j < k->exec_cap && k->executed) k->executed[((size_t)inst * n + p) * k->exec_cap + x0 + j] = dot;
@@ -844,7 +852,7 @@ struct Sim : GP {
     const uint32_t cnt = uni(S(sl, SL_CNT));
     const uint32_t ncol = (cnt >> 8) & 0xFFu, nk = (cnt >> 20) & 3u;
     uint32_t depv = 0, nd = 0;
-    const uint32_t colv = lid < ncol ? S(sl, SL_COLLECT + lid) : 0u;
+    const uint32_t colv = lidv() < ncol ? S(sl, SL_COLLECT + lidv()) : 0u;
     if (from_self) {
       depv = colv;
       nd = ncol;
@@ -854,7 +862,7 @@ struct Sim : GP {
     if (nd > g.amax) { fail_cap(__LINE__); return; }
     set_pst(sl, p, (ps & ~3u) | ST_COLLECT);
     // the ack's deps travel in the slot: ack deps of p
-    if (lid < g.amax) S(sl, g.sl_ack + p * g.amax + lid) = lid < nd ? depv : 0u;
+    if (lidv() < g.amax) S(sl, g.sl_ack + p * g.amax + lidv()) = lidv() < nd ? depv : 0u;
     if (protocol == FX_PROTOCOL_EPAXOS && from_self) return;  // epaxos.rs:290-300
     act_send(M_COLLECT_ACK, dot, 1u << from);
   }
@@ -872,7 +880,7 @@ struct Sim : GP {
     // QuorumDeps: union + per-dep report counts over the participants' acks.
     // lane j of a participant block holds one reported dep: lanes
     // [q*amax, q*amax + amax) for process q (<= 32 lanes)
-    const uint32_t q = lid / g.amax, j = lid % g.amax;
+    const uint32_t q = lidv() / g.amax, j = lidv() % g.amax;
     uint32_t v = 0;
     if (q < n && ((part >> q) & 1u)) v = S(sl, g.sl_ack + q * g.amax + j);
     const bool valid = v != 0;
@@ -885,7 +893,7 @@ struct Sim : GP {
       const uint32_t v2 = rl(v, l2);
       if (valid && v2 == v) {
         ++cnt;
-        if (l2 < lid) first = false;
+        if (l2 < lidv()) first = false;
       }
     }
     const uint64_t um = bal(first);  // one lane per distinct dep
@@ -906,7 +914,7 @@ struct Sim : GP {
     if (first) S(sl, g.sl_value + rank) = v;
     const uint32_t c0 = uni(S(sl, SL_CNT));
     put(S(sl, SL_CNT), (c0 & ~0xFFu) | nu | (fast ? 0u : (1u << 16)));  // slow: proposer ballot set
-    if (lid == (fast ? PT_FAST : PT_SLOW) + p) ++pt;
+    if (lidv() == (fast ? PT_FAST : PT_SLOW) + p) ++pt;
     if (fast) {
       act_send(M_COMMIT, dot, (1u << n) - 1u);
     } else {
@@ -982,7 +990,7 @@ struct Sim : GP {
   // frontier + 32-bit exception window) and two logs of its frontier: one
   // entry per tick interval in which it moved (the value a tick before the
   // move reports) and its last moves with their times (Geo::rt, Geo::rc entries).
-  __device__ __forceinline__ bool gc_lane(uint32_t p) const { return (lid >> 3) == p && (lid & 7u) < n; }
+  __device__ __forceinline__ bool gc_lane(uint32_t p) const { return (lidv() >> 3) == p && (lidv() & 7u) < n; }
 
   // MCommitDot: add_to_clock (gc/clock.rs:43-48)
   __device__ __forceinline__ void h_mcommitdot(uint32_t p, uint32_t dot) {
@@ -992,7 +1000,7 @@ struct Sim : GP {
 #endif
     const uint32_t si = (dot >> FX_SEQ_BITS) - 1u, sq = dot & FX_SEQ_MASK;
     bool bad = false;
-    if (lid == p * 8u + si && sq > gf) {
+    if (lidv() == p * 8u + si && sq > gf) {
       const uint32_t off = sq - gf - 1u;
       if (off >= 32u) {
         bad = true;
@@ -1065,7 +1073,7 @@ struct Sim : GP {
     const uint32_t gc_ms = prm(P_GC);
     const uint32_t tick = (x / gc_ms + 1u) * gc_ms;
     uint32_t tv = NONE;
-    const uint32_t p = lid >> 3, q = lid & 7u;
+    const uint32_t p = lidv() >> 3, q = lidv() & 7u;
     if (p < n && q < n && p != q) {
       const uint32_t d = dpq;
       tv = x < gc_ms + d ? gc_ms + d : ((x - d) / gc_ms + 1u) * gc_ms + d;
@@ -1086,8 +1094,8 @@ struct Sim : GP {
   // stopped on it
   __device__ __forceinline__ void gc_finish(uint32_t tc, uint32_t pair, unsigned long long* st) {
     const uint32_t gc_ms = prm(P_GC);
-    if (gc_lane(lid >> 3)) {
-      uint32_t* r = gcr(lid >> 3, lid & 7u);
+    if (gc_lane(lidv() >> 3)) {
+      uint32_t* r = gcr(lidv() >> 3, lidv() & 7u);
       r[0] = gf;
       r[1] = gnt;
       r[2] = gkm;
@@ -1096,12 +1104,12 @@ struct Sim : GP {
     for (uint32_t q = 0; q < n; ++q) {
       // lane p: deliveries p -> q processed, m
       uint32_t m = 0;
-      const bool pl = lid < n && lid != q;
-      const uint32_t dq = gather(dpq, (lid * 8u + q) & 63u);  // lane p: d(p, q)
+      const bool pl = lidv() < n && lidv() != q;
+      const uint32_t dq = gather(dpq, (lidv() * 8u + q) & 63u);  // lane p: d(p, q)
       if (pl) {
         const uint32_t d = dq;
         if (tc > d) m = (tc - d - 1u) / gc_ms;
-        if (pair == lid * 8u + q && tc >= d + gc_ms && (tc - d) % gc_ms == 0) ++m;
+        if (pair == lidv() * 8u + q && tc >= d + gc_ms && (tc - d) % gc_ms == 0) ++m;
       }
       uint32_t stable = 0;
       if (!bal(pl && m == 0)) {
@@ -1110,28 +1118,28 @@ struct Sim : GP {
         tl = uni(tl);
         uint32_t cur = 0;
         bool ok = true;
-        if (lid < n) ok = gc_value_at(q, lid, tl, cur);
+        if (lidv() < n) ok = gc_value_at(q, lidv(), tl, cur);
         for (uint32_t p = 0; p < n; ++p) {
           if (p == q) continue;
           const uint32_t kl = rl(m, p) - 1u;
           uint32_t v = 0;
-          if (lid < n) {
-            ok = ok && gc_tick_value(p, lid, kl, v);
+          if (lidv() < n) {
+            ok = ok && gc_tick_value(p, lidv(), kl, v);
             cur = min(cur, v);
           }
         }
-        if (bal(lid < n && !ok)) fail_cap(__LINE__);
+        if (bal(lidv() < n && !ok)) fail_cap(__LINE__);
         for (uint32_t s2 = 0; s2 < n; ++s2) stable += rl(cur, s2);
       }
-      if (st && lid == 0) st[FX_SIM_STAT_STABLE + q] = stable;
+      if (st && lidv() == 0) st[FX_SIM_STAT_STABLE + q] = stable;
     }
   }
 
   // ===================================================== GraphExecutor
   // lane bit of a wave-uniform 64-bit mask (no per-lane 64-bit lane mask kept live)
   __device__ __forceinline__ bool mine(uint64_t m) const {
-    const uint32_t half = lid < 32u ? (uint32_t)m : (uint32_t)(m >> 32);
-    return (half >> (lid & 31u)) & 1u;
+    const uint32_t half = lidv() < 32u ? (uint32_t)m : (uint32_t)(m >> 32);
+    return (half >> (lidv() & 31u)) & 1u;
   }
   __device__ __forceinline__ uint32_t vcount_of(uint32_t d) { return uni(S(slot_find(d), SL_CNT)) & 0xFFu; }
   __device__ __forceinline__ uint32_t value_at(uint32_t d, uint32_t j) { return uni(S(slot_find(d), g.sl_value + j)); }
@@ -1167,8 +1175,8 @@ struct Sim : GP {
       return;
     }
     rput(xdot, p, sdot); rput(xrec, p, srec); rput(xwait, p, swait);
-    if ((lid & 7u) == p) {
-      const uint32_t k = lid >> 3;
+    if ((lidv() & 7u) == p) {
+      const uint32_t k = lidv() >> 3;
       if (k == PT_OCC / 8u) pt = (uint32_t)occ;
       else if (k == PT_OCC / 8u + 1u) pt = (uint32_t)(occ >> 32);
       else if (k == PT_WAIT / 8u) pt = (uint32_t)wmask;
@@ -1209,7 +1217,7 @@ struct Sim : GP {
       fr = fr + 1 + ones;
       w = win >> ones;
     }
-    if (lid == xp * 8u + si) {
+    if (lidv() == xp * 8u + si) {
       ecf = fr;
       ecw = w;
     }
@@ -1234,7 +1242,7 @@ struct Sim : GP {
     // compiler reloads or copies under a partial exec mask holds garbage in the
     // inactive lanes
     const uint32_t inst = prm(P_INST);
-    if (lid == 0) {
+    if (lidv() == 0) {
       KSimArgs* k = kargs();
       if (xk < k->exec_cap && k->executed) k->executed[((size_t)inst * n + p) * k->exec_cap + xk] = d;
     }
@@ -1276,7 +1284,7 @@ struct Sim : GP {
     const uint64_t fre = ~occ & pmask;
     if (!fre) { fail_cap(__LINE__); return -1; }
     const uint32_t sl = ctz64(fre);
-    if (lid == sl) {
+    if (lidv() == sl) {
       sdot = d;
       srec = now;  // Vertex::start_time_ms (tarjan.rs:332-348)
       swait = 0;
@@ -1293,7 +1301,7 @@ struct Sim : GP {
     missing = 0;
     idc = 1;
     const uint32_t tr = rl(stl, r);
-    if (lid == r) stl = tmk(1, 1, tep(tr));
+    if (lidv() == r) stl = tmk(1, 1, tep(tr));
     nfr = 0;
     fv = r;
     fdi = 0;
@@ -1340,7 +1348,7 @@ struct Sim : GP {
     const bool mark = in_try && missing != 0 && !emitted;
     if (mine(occ) && tid(stl) != 0) stl = tmk(0, 0, mark ? epoch : tep(stl));
     if (missing) {  // index_pending (mod.rs:525-554)
-      if (lid == root) swait = missing;
+      if (lidv() == root) swait = missing;
       wmask |= 1ull << root;
     }
     if (in_try) {
@@ -1368,15 +1376,15 @@ struct Sim : GP {
       if (tid(tx) == 0) {  // recurse (tarjan.rs:172-214)
         ++idc;
         if (idc > 127u) { fail_cap(__LINE__); return; }
-        if (lid == (uint32_t)x) stl = tmk(idc, idc, tep(tx));
-        if (lid == nfr) sfr = fv | (fdi << 8);
+        if (lidv() == (uint32_t)x) stl = tmk(idc, idc, tep(tx));
+        if (lidv() == nfr) sfr = fv | (fdi << 8);
         ++nfr;
         fv = (uint32_t)x;
         fdi = 0;
         fnc = vcount_of(rl(sdot, fv));
       } else {  // on the stack (tarjan.rs:215-225)
         const uint32_t tv = rl(stl, fv);
-        if (tid(tx) < tlow(tv) && lid == fv) stl = tmk(tid(tv), tid(tx), tep(tv));
+        if (tid(tx) < tlow(tv) && lidv() == fv) stl = tmk(tid(tv), tid(tx), tep(tv));
       }
     } else {
       const uint32_t tv = rl(stl, fv);
@@ -1395,7 +1403,7 @@ struct Sim : GP {
       fdi = fw >> 8;
       fnc = vcount_of(rl(sdot, fv));
       const uint32_t tp = rl(stl, fv);
-      if (lowv < tlow(tp) && lid == fv) stl = tmk(tid(tp), lowv, tep(tp));
+      if (lowv < tlow(tp) && lidv() == fv) stl = tmk(tid(tp), lowv, tep(tp));
     }
   }
 
@@ -1444,12 +1452,12 @@ struct Sim : GP {
     const uint32_t vc = vcount_of(d);
     deps_total += vc;
     const uint32_t dsl = slot_find(d);
-    const uint32_t depj = lid < vc ? S(dsl, g.sl_value + lid) : 0u;
+    const uint32_t depj = lidv() < vc ? S(dsl, g.sl_value + lidv()) : 0u;
     // the clock gather runs with every lane active: ds_bpermute reads 0 from a
     // lane that is inactive, and the clock words sit in lanes 8 p + s, mostly
     // outside [0, vc) (inside `&&` the call would run in the masked branch)
     const bool exd = contains_v(depj);
-    const bool keep = lid < vc && depj != d && !exd;
+    const bool keep = lidv() < vc && depj != d && !exd;
     PROF_ADD(5);
     if (!bal(keep)) {  // fast path: a singleton SCC
 #ifdef FX_SIM_PROFILE
@@ -1631,7 +1639,7 @@ struct Sim : GP {
       lat_sum += lat;
       const uint32_t region = rl(ca, c) >> 8;
       const uint32_t inst = prm(P_INST);
-      if (lid == 0) {
+      if (lidv() == 0) {
         KSimArgs* k = kargs();
         if (k->latency_log && issued - 1u < k->lat_cap)
           k->latency_log[((size_t)inst * g.C + c) * k->lat_cap + issued - 1u] = lat;
@@ -1701,7 +1709,7 @@ __global__ __launch_bounds__(64 * WPB, WPS) void k_sim(SimArgs a) {
   Sim<HM, DS, NX, GP> s;
 #pragma unroll
   for (uint32_t k = 0; k < DS; ++k) s.sdv[k] = 0;
-  s.lid = threadIdx.x & 63u;
+  s.lid_ = threadIdx.x & 63u;
   s.trace = ((uint64_t)vdiv(0) << 32) | vdiv(0);
   s.deps_total = s.trace;
   s.lat_sum = s.trace;
@@ -1715,7 +1723,7 @@ __global__ __launch_bounds__(64 * WPB, WPS) void k_sim(SimArgs a) {
   s.C = s.g.C;
   const bool has_extra = sp.extra_sim_time_ms >= 0;
   {
-    const uint32_t l = s.lid;
+    const uint32_t l = s.lidv();
     uint32_t v = 0;
     v = l == Sim<HM, DS, NX, GP>::P_SEED ? (uint32_t)sp.seed : v;
     v = l == Sim<HM, DS, NX, GP>::P_SEED + 1 ? (uint32_t)(sp.seed >> 32) : v;
@@ -1748,8 +1756,8 @@ __global__ __launch_bounds__(64 * WPB, WPS) void k_sim(SimArgs a) {
     s.synod_f = fe;  // EPaxos::allowed_faults
   }
   // ---------------------------------------------------------------- init
-  for (uint32_t i = s.lid; i < s.g.words; i += 64) smem[i] = 0;
-  for (uint32_t i = s.lid; i < s.g.R; i += 64) smem[s.g.off_free + i] = s.g.R - 1u - i;  // free stack
+  for (uint32_t i = s.lidv(); i < s.g.words; i += 64) smem[i] = 0;
+  for (uint32_t i = s.lidv(); i < s.g.R; i += 64) smem[s.g.off_free + i] = s.g.R - 1u - i;  // free stack
   s.nfree = s.g.R;
   __builtin_amdgcn_s_barrier();
 #pragma unroll
@@ -1764,19 +1772,19 @@ __global__ __launch_bounds__(64 * WPB, WPS) void k_sim(SimArgs a) {
     const uint32_t rp = sp.process_regions[p];
     // lane q < n: position of process q in p's distance order
     uint32_t pos = 0;
-    if (s.lid < n) {
-      const uint32_t rq = sp.process_regions[s.lid];
+    if (s.lidv() < n) {
+      const uint32_t rq = sp.process_regions[s.lidv()];
       const uint32_t kq = a.rank[rp * RP + rq];
       for (uint32_t q2 = 0; q2 < n; ++q2) {
         const uint32_t r2 = sp.process_regions[q2];
         const uint32_t k2 = a.rank[rp * RP + r2];
-        if (k2 < kq || (k2 == kq && q2 < s.lid)) ++pos;
+        if (k2 < kq || (k2 == kq && q2 < s.lidv())) ++pos;
       }
     }
-    const uint32_t fqm = (uint32_t)bal(s.lid < n && pos < s.fq);
-    const uint32_t wqm = (uint32_t)bal(s.lid < n && pos < s.wq);
+    const uint32_t fqm = (uint32_t)bal(s.lidv() < n && pos < s.fq);
+    const uint32_t wqm = (uint32_t)bal(s.lidv() < n && pos < s.wq);
     s.lset(s.pq, p, fqm | (wqm << 8));
-    if (s.lid >= p * 8u && s.lid < p * 8u + n) s.dpq = a.ping[rp * RP + sp.process_regions[s.lid - p * 8u]] / 2u;
+    if (s.lidv() >= p * 8u && s.lidv() < p * 8u + n) s.dpq = a.ping[rp * RP + sp.process_regions[s.lidv() - p * 8u]] / 2u;
   }
   // clients: for region in client_regions, clients_per_region each (runner.rs:143-163)
   {
@@ -1793,11 +1801,11 @@ __global__ __launch_bounds__(64 * WPB, WPS) void k_sim(SimArgs a) {
         }
       }
       for (uint32_t i = 0; i < sp.clients_per_region; ++i, ++c) {
-        if (s.lid == c) {
+        if (s.lidv() == c) {
           s.ca = best | (rc << 8);
           s.cd = a.ping[rc * RP + sp.process_regions[best]] / 2u;
         }
-        if (s.lid == 32u + c) s.cd = a.ping[sp.process_regions[best] * RP + rc] / 2u;
+        if (s.lidv() == 32u + c) s.cd = a.ping[sp.process_regions[best] * RP + rc] / 2u;
       }
     }
   }
@@ -1856,22 +1864,22 @@ __global__ __launch_bounds__(64 * WPB, WPS) void k_sim(SimArgs a) {
   }
   // ----------------------------------------------------------- outputs
   __builtin_amdgcn_s_barrier();
-  const uint32_t o_exec = gather(s.pt, (PT_EXEC + s.lid) & 63u), o_fast = gather(s.pt, (PT_FAST + s.lid) & 63u),
-                 o_slow = gather(s.pt, (PT_SLOW + s.lid) & 63u);
-  if (s.lid < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lid] = o_exec;
+  const uint32_t o_exec = gather(s.pt, (PT_EXEC + s.lidv()) & 63u), o_fast = gather(s.pt, (PT_FAST + s.lidv()) & 63u),
+                 o_slow = gather(s.pt, (PT_SLOW + s.lidv()) & 63u);
+  if (s.lidv() < n && a.executed_len) a.executed_len[(size_t)inst * n + s.lidv()] = o_exec;
   if (a.stats) {
     unsigned long long* st = a.stats + (size_t)inst * FX_SIM_STATS;
-    if (s.lid < NMAX) {
-      const bool v = s.lid < n;
-      st[FX_SIM_STAT_FAST + s.lid] = v ? o_fast : 0u;
-      st[FX_SIM_STAT_SLOW + s.lid] = v ? o_slow : 0u;
-      st[FX_SIM_STAT_STABLE + s.lid] = 0u;
-      st[FX_SIM_STAT_FAST_READS + s.lid] = 0u;  // no read-only commands on this kernel
-      st[FX_SIM_STAT_SLOW_READS + s.lid] = 0u;
+    if (s.lidv() < NMAX) {
+      const bool v = s.lidv() < n;
+      st[FX_SIM_STAT_FAST + s.lidv()] = v ? o_fast : 0u;
+      st[FX_SIM_STAT_SLOW + s.lidv()] = v ? o_slow : 0u;
+      st[FX_SIM_STAT_STABLE + s.lidv()] = 0u;
+      st[FX_SIM_STAT_FAST_READS + s.lidv()] = 0u;  // no read-only commands on this kernel
+      st[FX_SIM_STAT_SLOW_READS + s.lidv()] = 0u;
     }
     if (gc_ms && !s.err) s.gc_finish(s.now, gc_pair, st);
     const uint32_t err_site = s.prm(s.P_ERRSITE);
-    if (s.lid == 0) {
+    if (s.lidv() == 0) {
       st[FX_SIM_STAT_EVENTS] = s.events;
 #ifdef FX_SIM_PROFILE
       for (uint32_t i = 0; i < 24; ++i) st[i] = s.prof[i];
@@ -1886,8 +1894,8 @@ __global__ __launch_bounds__(64 * WPB, WPS) void k_sim(SimArgs a) {
   }
   // the instance's histogram counts held in lanes (exact: a sample either
   // went there or straight to its global bin), clamped into the bins here
-  if (s.hcv && a.chain_hist) atomicAdd(&a.chain_hist[min(s.lid, a.chain_bins - 1u)], (unsigned long long)s.hcv);
-  for (uint32_t i = s.lid; i < HD_BINS; i += 64) {
+  if (s.hcv && a.chain_hist) atomicAdd(&a.chain_hist[min(s.lidv(), a.chain_bins - 1u)], (unsigned long long)s.hcv);
+  for (uint32_t i = s.lidv(); i < HD_BINS; i += 64) {
     const uint32_t c = smem[s.g.off_hist + i];
     if (c && a.delay_hist) atomicAdd(&a.delay_hist[min(i, a.delay_bins - 1u)], (unsigned long long)c);
   }
@@ -1895,7 +1903,7 @@ __global__ __launch_bounds__(64 * WPB, WPS) void k_sim(SimArgs a) {
     const uint32_t key = s.hlk - 1u, lat = key & 0xFFFFFFu;
     atomicAdd(&a.lat_hist[(key >> 24) * a.lat_bins + min(lat, a.lat_bins - 1u)], (unsigned long long)s.hlc);
   }
-  if (s.lid == 0) a.err[inst] = s.err;
+  if (s.lidv() == 0) a.err[inst] = s.err;
 }
 
 }  // namespace sim
