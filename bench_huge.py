@@ -146,7 +146,8 @@ def main_huge(args):
         "config": {"workload": "single huge instance: 5 executors x %d Adds with cycles (BASELINE configs[4]), "
                                "shape %s" % (steps, shape), "mean_deps": round(nd_total / n_adds, 3),
                    "parallelism": "quiescent-cut decomposition on one GPU; replicas only across GPUs"},
-        "segments": int(stats.segments), "max_segment": int(stats.max_segment),
+        "segments": int(stats.segments), "single_segments": int(stats.single_segments),
+        "max_segment": int(stats.max_segment),
         "whole_streams": int(stats.whole_streams),
         "roofline": huge_roof,
         "cpu_baseline": cpu,

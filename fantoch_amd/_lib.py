@@ -102,7 +102,7 @@ class CutStats(ctypes.Structure):
     """fx_cut_stats (fx_batch_run_cut)."""
     _fields_ = [("segments", ctypes.c_uint64), ("max_segment", ctypes.c_uint32),
                 ("whole_streams", ctypes.c_uint32), ("failed_streams", ctypes.c_uint32),
-                ("tier_counts", ctypes.c_uint32 * 16)]
+                ("tier_counts", ctypes.c_uint32 * 16), ("single_segments", ctypes.c_uint64)]
 
 
 class HistBatch(ctypes.Structure):

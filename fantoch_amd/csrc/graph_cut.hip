@@ -65,6 +65,27 @@ __device__ __forceinline__ uint32_t len_of(const In& in, uint32_t s) {
   return in.lengths ? min(in.lengths[s], in.steps) : in.steps;
 }
 
+// Work item t -> (stream s, step i) of the flat kernels that read the input
+// planes.  With one tile column of streams (S <= 64; configs[4]: 5) the items
+// run in plane order: the S streams' 16-byte pieces of a 4-step tile row are
+// adjacent words, so a wave reads whole lines once.  Stream-major items (each
+// wave walking one stream's steps) read 16 bytes of each line per stream, and
+// each line came from HBM once per stream.  i may be >= steps (steps are
+// rounded up to 4).
+__device__ __forceinline__ uint64_t n_items(const In& in) {
+  return in.S <= FX_TILE_STREAMS ? (uint64_t)in.S * ((in.steps + 3u) & ~3u) : (uint64_t)in.S * in.steps;
+}
+__device__ __forceinline__ void item(const In& in, uint64_t t, uint32_t& s, uint32_t& i) {
+  if (in.S <= FX_TILE_STREAMS) {
+    const uint32_t w = 4u * in.S;
+    s = (uint32_t)(t % w) >> 2;
+    i = (uint32_t)(t / w) * 4u + (uint32_t)(t & 3u);
+  } else {
+    s = (uint32_t)(t / in.steps);
+    i = (uint32_t)(t % in.steps);
+  }
+}
+
 // position-table slot of dot d in stream s, or INF when out of the table
 __device__ __forceinline__ uint64_t pos_slot(const In& in, const uint64_t* base, const uint32_t* maxseq,
                                              uint32_t s, uint32_t d) {
@@ -148,7 +169,7 @@ __global__ void k_part_max(const uint32_t* part, uint32_t blocks, uint32_t S, ui
 }
 
 __global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad, uint32_t* part) {
-  const uint64_t total = (uint64_t)in.S * in.steps;
+  const uint64_t total = n_items(in);
   WaveMax acc;
   __shared__ uint32_t lm[SMALL_S];
   const bool small = part != nullptr;
@@ -160,7 +181,8 @@ __global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad, uint32_t* part)
   // wave-uniform trip count (the reduction needs every lane active)
   for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x; b0 < total; b0 += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t t = b0 + threadIdx.x;
-    const uint32_t s = (uint32_t)(min(t, total - 1) / in.steps), i = (uint32_t)(t % in.steps);
+    uint32_t s, i;
+    item(in, min(t, total - 1), s, i);
     const bool valid = t < total && i < len_of(in, s);
     uint32_t sq = 0;
     if (valid) {
@@ -182,9 +204,10 @@ __global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad, uint32_t* part)
 }
 
 __global__ void k_pos(In in, const uint64_t* base, const uint32_t* maxseq, uint32_t* pos, uint32_t* bad) {
-  const uint64_t total = (uint64_t)in.S * in.steps;
+  const uint64_t total = n_items(in);
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t s = (uint32_t)(t / in.steps), i = (uint32_t)(t % in.steps);
+    uint32_t s, i;
+    item(in, t, s, i);
     if (i >= len_of(in, s)) continue;
     const uint64_t slot = pos_slot(in, base, maxseq, s, in.dot[fx_index(i, s, in.steps)]);
     if (slot == ~0ull) {
@@ -197,9 +220,10 @@ __global__ void k_pos(In in, const uint64_t* base, const uint32_t* maxseq, uint3
 
 // reach(i) = max(i, position of every dep); INF for a dep never added
 __global__ void k_reach(In in, const uint64_t* base, const uint32_t* maxseq, const uint32_t* pos, uint32_t* reach) {
-  const uint64_t total = (uint64_t)in.S * in.steps;
+  const uint64_t total = n_items(in);
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t s = (uint32_t)(t / in.steps), i = (uint32_t)(t % in.steps);
+    uint32_t s, i;
+    item(in, t, s, i);
     if (i >= len_of(in, s)) continue;
     const size_t at = fx_index(i, s, in.steps);
     const uint32_t nd = FX_HDR_ND(in.hdr[at]);
@@ -208,7 +232,7 @@ __global__ void k_reach(In in, const uint64_t* base, const uint32_t* maxseq, con
       const uint64_t slot = pos_slot(in, base, maxseq, s, in.deps[j * in.pw + at]);
       r = max(r, slot == ~0ull ? INF : pos[slot]);
     }
-    reach[t] = r;
+    reach[(size_t)s * in.steps + i] = r;
   }
 }
 
@@ -391,6 +415,51 @@ __global__ void k_seglen(uint64_t nseg, const uint64_t* segbase, const uint32_t*
   }
 }
 
+// Segments one Add long (an Add whose deps all lie in the executed prefix;
+// at 2 % conflicts nine in ten segments) need no executor: the Add is a
+// singleton SCC found by the search handle_add starts from it
+// (graph/mod.rs:296-312, tarjan.rs:96-316), so it executes at its own step,
+// after the whole prefix: order row a = a | SCC start, release[a] = a.
+// k_build writes those directly, and only the longer segments form the batch:
+// per chunk of CHUNK segments the count of longer ones, then (after an
+// exclusive scan of the counts) batch index bidx[k] (INF for a single) and
+// its inverse bseg[b] = k.
+__global__ void k_multi_count(uint64_t nseg, const uint32_t* seg_start, const uint32_t* seg_end, uint32_t* ccnt) {
+  __shared__ uint32_t sh[4];
+  uint32_t cnt = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint64_t g = (uint64_t)blockIdx.x * CHUNK + threadIdx.x * 4 + k;
+    if (g < nseg && seg_end[g] != seg_start[g]) ++cnt;
+  }
+  for (uint32_t off = 32; off; off >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, off);
+  if ((threadIdx.x & 63u) == 0) sh[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) ccnt[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ void k_multi_fill(uint64_t nseg, const uint32_t* seg_start, const uint32_t* seg_end,
+                             const uint32_t* ccnt_excl, uint32_t* bidx, uint32_t* bseg) {
+  __shared__ uint32_t sh[4];
+  uint32_t m[4], cnt = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint64_t g = (uint64_t)blockIdx.x * CHUNK + threadIdx.x * 4 + k;
+    m[k] = g < nseg && seg_end[g] != seg_start[g] ? 1u : 0u;
+    cnt += m[k];
+  }
+  uint32_t run = block_excl<true>(cnt, sh) + ccnt_excl[blockIdx.x];
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint64_t g = (uint64_t)blockIdx.x * CHUNK + threadIdx.x * 4 + k;
+    if (g >= nseg) break;
+    if (m[k]) {
+      bidx[g] = run;
+      bseg[run] = (uint32_t)g;
+      ++run;
+    } else {
+      bidx[g] = INF;
+    }
+  }
+}
+
 struct Seg {
   uint32_t* dot;
   uint32_t* hdr;
@@ -413,15 +482,22 @@ __device__ __forceinline__ uint32_t seg_rank(const In& in, uint32_t s, uint32_t 
 
 __global__ void k_build(In in, const uint64_t* base, const uint32_t* maxseq, const uint32_t* pos,
                         const uint32_t* seg_of, const uint32_t* seg_start, const uint32_t* seg_end,
-                        const uint32_t* whole, Seg sg) {
-  const uint64_t total = (uint64_t)in.S * in.steps;
+                        const uint32_t* bidx, const uint32_t* whole, Seg sg, uint32_t* order, uint32_t* release) {
+  const uint64_t total = n_items(in);
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t s = (uint32_t)(t / in.steps), i = (uint32_t)(t % in.steps);
+    uint32_t s, i;
+    item(in, t, s, i);
     if (i >= len_of(in, s) || whole[s]) continue;
-    const uint32_t k = seg_of[t];
+    const uint32_t k = seg_of[(size_t)s * in.steps + i];
     const uint32_t a = seg_start[k], b = seg_end[k], j = i - a;
     const size_t at = fx_index(i, s, in.steps);
-    const size_t to = fx_index(j, k, sg.steps);
+    if (a == b) {  // a single Add: executed at its own step
+      order[at] = i | FX_ORDER_SCC_START;
+      release[at] = i;
+      continue;
+    }
+    const uint32_t bk = bidx[k];
+    const size_t to = fx_index(j, bk, sg.steps);
     const uint32_t d = in.dot[at];
     sg.dot[to] = FX_PACK_DOT(FX_DOT_SRC(d), seg_rank(in, s, a, b, FX_DOT_SRC(d), FX_DOT_SEQ(d)));
     const uint32_t h = in.hdr[at];
@@ -435,28 +511,33 @@ __global__ void k_build(In in, const uint64_t* base, const uint32_t* maxseq, con
       ++nk;
     }
     sg.hdr[to] = FX_MAKE_HDR(FX_HDR_T(h), nk, FX_HDR_KIND(h));
-    if (j == 0) sg.lengths[k] = b - a + 1u;
+    if (j == 0) sg.lengths[bk] = b - a + 1u;
   }
 }
 
-// segment outputs -> the stream's planes; a segment that did not execute
-// completely sends its stream to the whole-stream path
-__global__ void k_scatter(uint64_t nseg, uint32_t seg_steps, const uint32_t* seg_stream, const uint32_t* seg_start,
-                          const uint32_t* seg_len, const uint32_t* sorder, const uint32_t* srelease,
-                          const uint32_t* snexec, const uint32_t* serr, uint32_t steps, uint32_t* order,
-                          uint32_t* release, uint32_t* fail) {
-  const uint64_t total = nseg * seg_steps;
+// batch outputs -> the stream's planes; a segment that did not execute
+// completely sends its stream to the whole-stream path.  Items in the batch
+// planes' own order (t = plane word), so a wave reads 1 KiB of them at once
+__global__ void k_scatter(uint32_t nb, uint32_t seg_steps, const uint32_t* bseg, const uint32_t* seg_stream,
+                          const uint32_t* seg_start, const uint32_t* blen, const uint32_t* sorder,
+                          const uint32_t* srelease, const uint32_t* snexec, const uint32_t* serr, uint32_t steps,
+                          uint32_t* order, uint32_t* release, uint32_t* fail) {
+  const uint64_t total = fx_plane_words(nb, seg_steps);
+  const uint32_t steps4 = (seg_steps + 3u) >> 2;
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = t / seg_steps;
-    const uint32_t j = (uint32_t)(t % seg_steps);
-    const uint32_t len = seg_len[k];
+    const uint64_t row = t >> 8;  // (tile, 4-step block)
+    const uint32_t b = (uint32_t)(row / steps4) * 64u + ((uint32_t)(t & 255u) >> 2);
+    const uint32_t j = (uint32_t)(row % steps4) * 4u + (uint32_t)(t & 3u);
+    if (b >= nb) continue;
+    const uint32_t len = blen[b];
     if (j >= len) continue;
+    const uint32_t k = bseg[b];
     const uint32_t s = seg_stream[k], a = seg_start[k];
-    if (serr[k] != FX_OK || snexec[k] != len) {
+    if (serr[b] != FX_OK || snexec[b] != len) {
       if (j == 0) fail[s] = 1;
       continue;
     }
-    const size_t from = fx_index(j, (uint32_t)k, seg_steps);
+    const size_t from = t;  // fx_index(j, b, seg_steps)
     const size_t to = fx_index(a + j, s, steps);
     const uint32_t o = sorder[from];
     order[to] = (a + FX_ORDER_REC(o)) | (o & FX_ORDER_SCC_START);
@@ -587,8 +668,25 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
                        spart);
     if (spart) hipLaunchKernelGGL(k_part_max, dim3(S), dim3(BT), 0, hs, spart, gs, S, smax);
   }
+  // the batch: segments longer than one Add (k_multi_count)
+  uint32_t* nbatch = db.alloc<uint32_t>(1, 0);
+  uint32_t* bidx = nullptr;
+  uint32_t* bseg = nullptr;
+  if (!nbatch) return FX_ERR_HIP;
+  if (NS && NS < (1ull << 31)) {
+    const uint32_t nchS = (uint32_t)((NS + CHUNK - 1) / CHUNK);
+    uint32_t* mcnt = db.alloc<uint32_t>(nchS);
+    bidx = db.alloc<uint32_t>(NS);
+    bseg = db.alloc<uint32_t>(NS);
+    if (!mcnt || !bidx || !bseg) return FX_ERR_HIP;
+    hipLaunchKernelGGL(k_multi_count, dim3(nchS), dim3(BT), 0, hs, NS, seg_start, seg_end, mcnt);
+    chunk_excl<true>(1, nchS, mcnt, nbatch, hs);
+    hipLaunchKernelGGL(k_multi_fill, dim3(nchS), dim3(BT), 0, hs, NS, seg_start, seg_end, mcnt, bidx, bseg);
+  }
   std::vector<uint32_t> h_smax(S);
+  uint32_t h_nbatch = 0;
   (void)hipMemcpyAsync(h_smax.data(), smax, (size_t)S * 4, hipMemcpyDeviceToHost, hs);
+  (void)hipMemcpyAsync(&h_nbatch, nbatch, 4, hipMemcpyDeviceToHost, hs);
   if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
   std::vector<uint32_t> h_len(S, in.steps);
   if (in_->lengths) {
@@ -623,10 +721,12 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
   if (stats) {
     stats->segments = nseg_used;
     stats->max_segment = seg_steps;
+    stats->single_segments = nseg_used ? NS - h_nbatch : 0;
   }
   if (nseg_used) {
-    // 4. the segment batch: one stream per segment
-    const uint32_t SS = (uint32_t)NS;
+    // 4. the segment batch: one stream per segment longer than one Add (the
+    // single ones are written by k_build); NB = 0 still runs k_build
+    const uint32_t SS = std::max(h_nbatch, 1u);
     Seg sg;
     sg.steps = seg_steps;
     sg.pw = fx_plane_words(SS, seg_steps);
@@ -641,15 +741,17 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
     uint32_t* serr = db.alloc<uint32_t>(SS);
     if (!sg.dot || !sg.hdr || !sg.deps || !sg.lengths || !sorder || !srelease || !snexec || !serr) return FX_ERR_HIP;
     hipLaunchKernelGGL(k_build, dim3(grid_for(work)), dim3(BT), 0, hs, in, base, maxseq, pos, seg_of, seg_start,
-                       seg_end, whole, sg);
-    fx_stream_batch sin{sg.dot, sg.hdr, sg.deps, sg.lengths, SS, seg_steps, in.dmax, in.n};
-    fx_order_batch sout{sorder, srelease, snexec, serr};
-    const int st = run_tiered(&sin, &sout, flags, hip_stream, nullptr, stats ? stats->tier_counts : nullptr);
-    if (st == FX_ERR_HIP || st == FX_ERR_NO_DEVICE || st == FX_ERR_INVALID_ARG) return st;
-    // (per-segment failures are handled below: their streams run whole)
-    hipLaunchKernelGGL(k_scatter, dim3(grid_for((uint64_t)SS * seg_steps)), dim3(BT), 0, hs, (uint64_t)SS, seg_steps,
-                       seg_stream, seg_start, sg.lengths, sorder, srelease, snexec, serr, in.steps, out->order,
-                       out->release, fail);
+                       seg_end, bidx, whole, sg, out->order, out->release);
+    if (h_nbatch) {
+      fx_stream_batch sin{sg.dot, sg.hdr, sg.deps, sg.lengths, SS, seg_steps, in.dmax, in.n};
+      fx_order_batch sout{sorder, srelease, snexec, serr};
+      const int st = run_tiered(&sin, &sout, flags, hip_stream, nullptr, stats ? stats->tier_counts : nullptr);
+      if (st == FX_ERR_HIP || st == FX_ERR_NO_DEVICE || st == FX_ERR_INVALID_ARG) return st;
+      // (per-segment failures are handled below: their streams run whole)
+      hipLaunchKernelGGL(k_scatter, dim3(grid_for(fx_plane_words(SS, seg_steps))), dim3(BT), 0, hs, SS, seg_steps,
+                         bseg, seg_stream, seg_start, sg.lengths, sorder, srelease, snexec, serr, in.steps,
+                         out->order, out->release, fail);
+    }
   }
   // every stream that neither runs whole nor failed a segment executed all
   // its Adds — including the empty ones, which have no segment at all

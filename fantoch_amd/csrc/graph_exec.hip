@@ -750,6 +750,8 @@ __global__ __launch_bounds__(64) void k_graph_exec(KArgs a) {
 // Metrics::collect for ChainSize (one sample per SCC, mod.rs:492-493) and
 // ExecutionDelay (t(release) - t(add), mod.rs:514-518).  One 256-thread block
 // per (tile, 4-row block): thread t reads order word t of that 1 KiB granule.
+// With one tile column of streams (S <= 64; configs[4]: 5) a block takes 256
+// consecutive used words instead (4 S per 4-row block), not 4 S of 256 threads.
 // Wave-aggregated histogram increment: one atomic per distinct bin in the wave
 // (the leader lane adds the popcount of the lanes sharing its bin).  Most Adds
 // of a wave land in one or two bins (ChainSize 1, small delays), so per-lane
@@ -783,23 +785,29 @@ __global__ __launch_bounds__(256) void k_metrics(const uint32_t* __restrict__ hd
   extern __shared__ __attribute__((aligned(16))) uint32_t hist[];  // [nbc + nbd]
   const uint32_t steps4 = (steps + 3) >> 2;
   const uint32_t tiles = (S + 63) >> 6;
-  const size_t nblocks = (size_t)tiles * steps4;
+  const bool narrow = S <= 64;
+  const uint32_t w = 4u * S;  // narrow: used words per 4-row block
+  const size_t nblocks = narrow ? ((size_t)w * steps4 + 255) / 256 : (size_t)tiles * steps4;
   if (use_lds) {
     for (uint32_t q = threadIdx.x; q < nbc + nbd; q += blockDim.x) hist[q] = 0;
     __syncthreads();
   }
   const uint32_t t = threadIdx.x;
-  const uint32_t lane = t >> 2, kq = t & 3;
   // blk is block-uniform, so every wave runs the aggregated adds together
   for (size_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
-    const uint32_t tile = (uint32_t)(blk / steps4), kb = (uint32_t)(blk % steps4);
-    const uint32_t s = tile * 64 + lane;
-    const uint32_t k = kb * 4 + kq;
+    uint32_t s, k;
+    if (narrow) {
+      const size_t it = blk * 256 + t;
+      s = it < (size_t)w * steps4 ? (uint32_t)(it % w) >> 2 : S;
+      k = (uint32_t)(it / w) * 4 + (t & 3);
+    } else {
+      s = (uint32_t)(blk / steps4) * 64 + (t >> 2);
+      k = (uint32_t)(blk % steps4) * 4 + (t & 3);
+    }
     uint32_t db = kNoBin, cb = kNoBin;
     const uint32_t ne = s < S ? nexec[s] : 0;
     if (k < ne) {
-      const size_t tile_base = (size_t)tile * steps4 * 256 + (lane << 2);
-      const uint32_t o = order[tile_base + (size_t)kb * 256 + kq];
+      const uint32_t o = order[fx_index(k, s, steps)];
       const uint32_t rec = o & 0x7FFFFFFFu;
       const uint32_t rs = rec < steps ? release[fx_index(rec, s, steps)] : FX_RELEASE_NONE;
       if (rs < steps) {  // else not executed (errored stream)
@@ -1254,7 +1262,8 @@ int fx_batch_metrics(const fx_stream_batch* in, const fx_order_batch* out, const
     return FX_ERR_INVALID_ARG;
   if (device_count() <= 0) return FX_ERR_NO_DEVICE;
   const uint32_t steps4 = (in->steps + 3) >> 2;
-  const size_t nblocks = (size_t)((in->num_streams + 63) / 64) * steps4;
+  const size_t nblocks = in->num_streams <= 64 ? ((size_t)4 * in->num_streams * steps4 + 255) / 256
+                                               : (size_t)((in->num_streams + 63) / 64) * steps4;
   if (nblocks == 0) return FX_OK;
   const uint32_t grid = (uint32_t)std::min<size_t>(nblocks, 256 * 8);
   const size_t lds_bytes = (size_t)(h->nbins_chain + h->nbins_delay) * 4;

@@ -345,6 +345,12 @@ struct Big {
   }
 #endif
   uint32_t now = 0;  // ms
+  // the clock read at a cold use without a vector copy of it kept live
+  __device__ __forceinline__ uint32_t nowv() const {
+    uint32_t x = now;
+    asm volatile("" : "+s"(x));
+    return x;
+  }
   uint32_t seq = 0;  // insertion counter (C3)
   uint32_t rdraws = 0, events = 0;  // (32 bits: bounded by max_events; 64-bit counters live in LDS)
   uint64_t trace = 0;
@@ -1544,7 +1550,7 @@ struct Big {
       on_execute(sl, d, now);
     } else {
       rput(R_PST, ps | PS_INGRAPH);
-      put(RC(sl, p, R_START), now);  // Vertex::start_time_ms (tarjan.rs:332-348)
+      put(RC(sl, p, R_START), nowv());  // Vertex::start_time_ms (tarjan.rs:332-348)
       // The first search from the new vertex v enters its first dep u that is
       // neither v nor executed (deps ascend, C1).  If u is pending and the last
       // search rooted at u stopped at missing dep m with no execution at p

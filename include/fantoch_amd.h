@@ -226,7 +226,8 @@ int fx_batch_run_tiered(const fx_stream_batch* in, const fx_order_batch* out,
  * DependencyGraph (graph/mod.rs:213-642) has executed the whole prefix and
  * holds nothing pending, so each segment runs from an empty graph with its
  * prefix deps dropped and its dots renumbered per source (order-preserving).
- * All segments run as one batch through fx_batch_run_tiered and map back.
+ * Segments longer than one Add run as one batch through fx_batch_run_tiered
+ * and map back; a one-Add segment executes at its own step.
  * A stream without a usable decomposition (a dep that never arrives, a
  * segment over 4096 steps, a double index, an index-only record) or whose
  * segments do not all execute completely runs whole through
@@ -240,6 +241,9 @@ typedef struct fx_cut_stats {
                                            execute completely (capacity, or the cut
                                            argument failing: never seen so far)     */
   uint32_t tier_counts[16];             /* segment-batch streams run per tier       */
+  uint64_t single_segments;             /* segments one Add long: executed at their
+                                           own step without the batch (a singleton
+                                           SCC after the executed prefix)           */
 } fx_cut_stats;
 int fx_batch_run_cut(const fx_stream_batch* in, const fx_order_batch* out, uint32_t flags, void* hip_stream,
                      fx_cut_stats* stats);

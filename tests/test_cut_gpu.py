@@ -38,6 +38,31 @@ def test_cut_matches_oracle(case):
     st = res.cut_stats
     assert st.failed_streams == 0
     assert st.whole_streams == 0 and st.segments > planes.S
+    assert st.single_segments <= st.segments
+
+
+def test_cut_only_single_segments():
+    """Streams without dependencies: every segment is one Add long, so no
+    batch runs at all (k_build writes every row); the same outputs as the
+    oracle's.  One stream beside them with deps checks the mixed case."""
+    n = 3
+    streams = [[((1 + (k % n), 1 + k // n), [], 1) for k in range(9)] for _ in range(4)]
+    planes = fs.pack_streams(streams, n)
+    res = fd.run_batch(planes, cut=True, nbins_chain=64, nbins_delay=4096)
+    assert res.status == _lib.FX_OK
+    o_order, o_rel, o_nexec = assert_parity(planes, res)
+    chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 64, 4096)
+    assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
+    st = res.cut_stats
+    assert st.segments == 36 and st.single_segments == 36 and sum(st.tier_counts) == 0
+    # a cycle (two Adds waiting on each other) among single Adds
+    streams[1] = [((1, 1), [], 1), ((2, 1), [(3, 1)], 2), ((3, 1), [(2, 1)], 3), ((1, 2), [], 4)]
+    planes = fs.pack_streams(streams, n)
+    res = fd.run_batch(planes, cut=True)
+    assert res.status == _lib.FX_OK
+    assert_parity(planes, res)
+    st = res.cut_stats
+    assert st.segments == 3 * 9 + 3 and st.single_segments == 3 * 9 + 2
 
 
 def test_cut_ragged_lengths():
@@ -91,8 +116,11 @@ def test_config4_single_huge_instance_cut():
     assert np.all(res.nexec == planes.steps)
     chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 64, 2048)
     assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
+    st = res.cut_stats
     print("configs[4]: GPU cut driver %.3f s (incl. host<->device copies), oracle+compare %.3f s, "
-          "%d segments, longest %d" % (t_gpu, t_cpu, res.cut_stats.segments, res.cut_stats.max_segment))
+          "%d segments (%d of one Add), longest %d" % (t_gpu, t_cpu, st.segments, st.single_segments,
+                                                       st.max_segment))
+    assert 0 < st.single_segments < st.segments
 
 
 def test_config4_s5_single_huge_instance_cut():
@@ -112,7 +140,8 @@ def test_config4_s5_single_huge_instance_cut():
     chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 64, 2048)
     assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
     st = res.cut_stats
-    print("S5: %d segments, longest %d, whole streams %d" % (st.segments, st.max_segment, st.whole_streams))
+    print("S5: %d segments (%d of one Add), longest %d, whole streams %d" % (
+        st.segments, st.single_segments, st.max_segment, st.whole_streams))
     assert st.failed_streams == 0
 
 

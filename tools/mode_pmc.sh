@@ -1,12 +1,12 @@
 # Counter passes of one bench mode's dominant kernel (rocprofv3 --pmc, one
 # counter group per run, each under its own time limit; the script stops at the
 # first failing step).  usage:
-#   bash tools/mode_pmc.sh MODE KERNEL_PATTERN [bench args]
-# outputs under gpurun_out/pmc_<mode>/; summarise with tools/mode_pmc_summary.py
+#   [PMC_TAG=name] bash tools/mode_pmc.sh MODE KERNEL_PATTERN [bench args]
+# outputs under gpurun_out/pmc_<PMC_TAG or mode>/; summarise with tools/mode_pmc_summary.py
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 MODE=$1; PAT=$2; shift 2
-M=gpurun_out/pmc_$MODE; rm -rf $M; mkdir -p $M
+M=gpurun_out/pmc_${PMC_TAG:-$MODE}; rm -rf $M; mkdir -p $M
 B="bench.py --mode $MODE --steps 1 --warmup 1 --no-cpu-baseline $@"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $M/trace -o run --output-format csv -- python3 $B \
   > $M/trace.log 2>&1 || { echo "$MODE trace rc=$?"; tail -20 $M/trace.log; exit 1; }
