@@ -418,45 +418,89 @@ __global__ void k_seglen(uint64_t nseg, const uint64_t* segbase, const uint32_t*
 // Segments one Add long (an Add whose deps all lie in the executed prefix;
 // at 2 % conflicts nine in ten segments) need no executor: the Add is a
 // singleton SCC found by the search handle_add starts from it
-// (graph/mod.rs:296-312, tarjan.rs:96-316), so it executes at its own step,
+// (graph/mod.rs:244-250, tarjan.rs:96-316), so it executes at its own step,
 // after the whole prefix: order row a = a | SCC start, release[a] = a.
-// k_build writes those directly, and only the longer segments form the batch:
-// per chunk of CHUNK segments the count of longer ones, then (after an
-// exclusive scan of the counts) batch index bidx[k] (INF for a single) and
-// its inverse bseg[b] = k.
-__global__ void k_multi_count(uint64_t nseg, const uint32_t* seg_start, const uint32_t* seg_end, uint32_t* ccnt) {
-  __shared__ uint32_t sh[4];
-  uint32_t cnt = 0;
-  for (uint32_t k = 0; k < 4; ++k) {
-    const uint64_t g = (uint64_t)blockIdx.x * CHUNK + threadIdx.x * 4 + k;
-    if (g < nseg && seg_end[g] != seg_start[g]) ++cnt;
-  }
-  for (uint32_t off = 32; off; off >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, off);
-  if ((threadIdx.x & 63u) == 0) sh[threadIdx.x >> 6] = cnt;
-  __syncthreads();
-  if (threadIdx.x == 0) ccnt[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+// k_build writes those directly, and only the longer segments form the batch,
+// ordered by length class, longest first: the batch executor runs one segment
+// per lane, so a wave lasts as long as its longest segment, and neighbours of
+// like length keep its lanes busy (S5: lengths 2 to 110; the lane tier 4.8 ->
+// 2.6 ms).  It scatters k_build's writes into the batch planes (0.75 -> 1.14
+// ms); ordering only inside chunks of 1,024 segments kept them local but lost
+// more in the executor (S5 5.58 against 4.26 ms per step, same box).  Class of
+// a length L >= 2: ceil(log2 L), 1..12, 13 beyond MAX_SEG (those streams run
+// whole; their segments keep an empty batch slot).  Deterministic: within a
+// class the segments keep their id order (per-chunk class counts, an
+// exclusive scan of each class over the chunks, ranks by ballots inside a
+// chunk).
+constexpr uint32_t NCLS = 16;
+__device__ __forceinline__ uint32_t seg_class(uint64_t g, uint64_t nseg, const uint32_t* seg_start,
+                                              const uint32_t* seg_end) {
+  if (g >= nseg) return 0;
+  const uint32_t len = seg_end[g] - seg_start[g] + 1u;
+  if (len < 2) return 0;
+  return len > MAX_SEG ? 13u : 32u - (uint32_t)__builtin_clz(len - 1u);
 }
 
-__global__ void k_multi_fill(uint64_t nseg, const uint32_t* seg_start, const uint32_t* seg_end,
-                             const uint32_t* ccnt_excl, uint32_t* bidx, uint32_t* bseg) {
-  __shared__ uint32_t sh[4];
-  uint32_t m[4], cnt = 0;
+// per chunk of CHUNK segments: the count of each class (ccnt[chunk][class])
+// and of the batch's segments in all (cm[chunk])
+__global__ void k_class_count(uint64_t nseg, const uint32_t* seg_start, const uint32_t* seg_end, uint32_t nch,
+                              uint32_t* ccnt) {
+  __shared__ uint32_t cnt[NCLS];
+  if (threadIdx.x < NCLS) cnt[threadIdx.x] = 0;
+  __syncthreads();
   for (uint32_t k = 0; k < 4; ++k) {
-    const uint64_t g = (uint64_t)blockIdx.x * CHUNK + threadIdx.x * 4 + k;
-    m[k] = g < nseg && seg_end[g] != seg_start[g] ? 1u : 0u;
-    cnt += m[k];
+    const uint32_t c = seg_class((uint64_t)blockIdx.x * CHUNK + k * BT + threadIdx.x, nseg, seg_start, seg_end);
+    if (c) atomicAdd(&cnt[c], 1u);
   }
-  uint32_t run = block_excl<true>(cnt, sh) + ccnt_excl[blockIdx.x];
+  __syncthreads();
+  if (threadIdx.x < NCLS) ccnt[(size_t)threadIdx.x * nch + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// batch index of every segment (INF for a single) and its inverse.  cm: the
+// exclusive prefix of the chunks' batch counts
+__global__ void k_class_fill(uint64_t nseg, const uint32_t* seg_start, const uint32_t* seg_end, uint32_t nch,
+                             const uint32_t* ccnt, const uint32_t* ctot, uint32_t* bidx, uint32_t* bseg) {
+  __shared__ uint32_t base[NCLS], run[NCLS], cw[BT / 64][NCLS];
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  if (threadIdx.x < NCLS) {
+    uint32_t b = 0;  // longest class first
+    for (uint32_t c = threadIdx.x + 1; c < NCLS; ++c) b += ctot[c];
+    base[threadIdx.x] = b + ccnt[(size_t)threadIdx.x * nch + blockIdx.x];
+    run[threadIdx.x] = 0;
+  }
   for (uint32_t k = 0; k < 4; ++k) {
-    const uint64_t g = (uint64_t)blockIdx.x * CHUNK + threadIdx.x * 4 + k;
-    if (g >= nseg) break;
-    if (m[k]) {
-      bidx[g] = run;
-      bseg[run] = (uint32_t)g;
-      ++run;
-    } else {
-      bidx[g] = INF;
+    const uint64_t g = (uint64_t)blockIdx.x * CHUNK + k * BT + threadIdx.x;
+    const uint32_t c = seg_class(g, nseg, seg_start, seg_end);
+    if (lane < NCLS) cw[w][lane] = 0;
+    __syncthreads();
+    uint32_t rank = 0;
+    uint64_t todo = __ballot(c != 0);
+    while (todo) {
+      const uint32_t lead = __builtin_ctzll(todo);
+      const uint32_t c0 = (uint32_t)__shfl((int)c, (int)lead);
+      const uint64_t same = __ballot(c == c0);
+      if (lane == lead) cw[w][c0] = (uint32_t)__popcll(same);
+      if (c == c0) rank = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+      todo &= ~same;
     }
+    __syncthreads();
+    if (g < nseg) {
+      if (c) {
+        uint32_t b = base[c] + run[c] + rank;
+        for (uint32_t v = 0; v < w; ++v) b += cw[v][c];
+        bidx[g] = b;
+        bseg[b] = (uint32_t)g;
+      } else {
+        bidx[g] = INF;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < NCLS) {
+      uint32_t t = 0;
+      for (uint32_t v = 0; v < BT / 64; ++v) t += cw[v][threadIdx.x];
+      run[threadIdx.x] += t;
+    }
+    __syncthreads();
   }
 }
 
@@ -668,26 +712,29 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
                        spart);
     if (spart) hipLaunchKernelGGL(k_part_max, dim3(S), dim3(BT), 0, hs, spart, gs, S, smax);
   }
-  // the batch: segments longer than one Add (k_multi_count)
-  uint32_t* nbatch = db.alloc<uint32_t>(1, 0);
+  // the batch: segments longer than one Add, by chunks and, inside a chunk,
+  // longest class first (k_class_fill)
+  uint32_t* ctot = db.alloc<uint32_t>(NCLS, 0);
   uint32_t* bidx = nullptr;
   uint32_t* bseg = nullptr;
-  if (!nbatch) return FX_ERR_HIP;
+  if (!ctot) return FX_ERR_HIP;
   if (NS && NS < (1ull << 31)) {
     const uint32_t nchS = (uint32_t)((NS + CHUNK - 1) / CHUNK);
-    uint32_t* mcnt = db.alloc<uint32_t>(nchS);
+    uint32_t* ccls = db.alloc<uint32_t>((size_t)NCLS * nchS);
     bidx = db.alloc<uint32_t>(NS);
     bseg = db.alloc<uint32_t>(NS);
-    if (!mcnt || !bidx || !bseg) return FX_ERR_HIP;
-    hipLaunchKernelGGL(k_multi_count, dim3(nchS), dim3(BT), 0, hs, NS, seg_start, seg_end, mcnt);
-    chunk_excl<true>(1, nchS, mcnt, nbatch, hs);
-    hipLaunchKernelGGL(k_multi_fill, dim3(nchS), dim3(BT), 0, hs, NS, seg_start, seg_end, mcnt, bidx, bseg);
+    if (!ccls || !bidx || !bseg) return FX_ERR_HIP;
+    hipLaunchKernelGGL(k_class_count, dim3(nchS), dim3(BT), 0, hs, NS, seg_start, seg_end, nchS, ccls);
+    chunk_excl<true>(NCLS, nchS, ccls, ctot, hs);
+    hipLaunchKernelGGL(k_class_fill, dim3(nchS), dim3(BT), 0, hs, NS, seg_start, seg_end, nchS, ccls, ctot, bidx,
+                       bseg);
   }
-  std::vector<uint32_t> h_smax(S);
-  uint32_t h_nbatch = 0;
+  std::vector<uint32_t> h_smax(S), h_ctot(NCLS);
   (void)hipMemcpyAsync(h_smax.data(), smax, (size_t)S * 4, hipMemcpyDeviceToHost, hs);
-  (void)hipMemcpyAsync(&h_nbatch, nbatch, 4, hipMemcpyDeviceToHost, hs);
+  (void)hipMemcpyAsync(h_ctot.data(), ctot, NCLS * 4, hipMemcpyDeviceToHost, hs);
   if (hipStreamSynchronize(hs) != hipSuccess) return FX_ERR_HIP;
+  uint32_t h_nbatch = 0;
+  for (uint32_t c = 1; c < NCLS; ++c) h_nbatch += h_ctot[c];
   std::vector<uint32_t> h_len(S, in.steps);
   if (in_->lengths) {
     (void)hipMemcpyAsync(h_len.data(), in_->lengths, (size_t)S * 4, hipMemcpyDeviceToHost, hs);

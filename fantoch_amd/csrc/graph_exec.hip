@@ -794,7 +794,12 @@ __global__ __launch_bounds__(256) void k_metrics(const uint32_t* __restrict__ hd
   }
   const uint32_t t = threadIdx.x;
   // blk is block-uniform, so every wave runs the aggregated adds together
-  for (size_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+  // XCD-aware order (narrow batches): the hardware deals blocks to the 8 XCDs
+  // round robin; each XCD taking a contiguous eighth of every grid pass keeps
+  // the release / hdr lines its rows look up (nearby steps) in its own L2
+  const size_t b0 = narrow && gridDim.x % 8u == 0 ? (size_t)(blockIdx.x % 8u) * (gridDim.x / 8u) + blockIdx.x / 8u
+                                                  : blockIdx.x;
+  for (size_t blk = b0; blk < nblocks; blk += gridDim.x) {
     uint32_t s, k;
     if (narrow) {
       const size_t it = blk * 256 + t;
