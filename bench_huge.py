@@ -75,11 +75,13 @@ def main_huge(args):
     nd_total = int(((hdr >> 24) & 31).sum(dtype=torch.int64).item())
     n_adds = S * steps
     stats = _lib.CutStats()
+    # the segment batch's first executor tier (--tier; default FX_TIER_DEFAULT)
+    cut_flags = _lib.first_tier_flag(args.tier) if args.tier >= 0 else 0
 
     def step():
         chain.zero_()
         delay.zero_()
-        st = lib.fx_batch_run_cut(ctypes.byref(inb), ctypes.byref(outb), 0, hs, ctypes.byref(stats))
+        st = lib.fx_batch_run_cut(ctypes.byref(inb), ctypes.byref(outb), cut_flags, hs, ctypes.byref(stats))
         _lib.check(st, "fx_batch_run_cut")
         _lib.check(lib.fx_batch_metrics(ctypes.byref(inb), ctypes.byref(outb), ctypes.byref(hb), hs),
                    "fx_batch_metrics")
