@@ -524,11 +524,16 @@ __device__ __forceinline__ uint32_t seg_rank(const In& in, uint32_t s, uint32_t 
   return r;
 }
 
-// every Add of a longer segment: the rank of its dot among the segment's dots
-// of its source (rk, stream-major).  k_build takes a dep's rank at the dep's
-// position (a dep not in the prefix lies in the segment: it ends at a cut),
-// so the segment is scanned once per Add instead of once per Add and per dep
-// (S5, 3 deps per Add: k_build 1.14 ms -> k_rank 0.11 + k_build 0.29 ms)
+// Renumbering needs each dot's rank among the segment's dots of its source.
+// A segment of at most RANK_INLINE Adds is scanned by k_build itself, once
+// per Add and per dep.  For longer ones k_rank writes every Add's own rank
+// once (rk, stream-major) and k_build takes a dep's rank at the dep's
+// position (a dep outside the prefix lies in the segment: it ends at a cut):
+// S5, 3 deps per Add, k_build 1.14 ms -> k_rank 0.11 + k_build 0.29 ms.
+// (k_rank over the longer segments' batch slots instead of the stream's
+// Adds read less at 2 % but 1.45x the bytes at S5, and took 0.20 ms.)
+constexpr uint32_t RANK_INLINE = 4;
+
 __global__ void k_rank(In in, const uint32_t* seg_of, const uint32_t* seg_start, const uint32_t* seg_end,
                        const uint32_t* whole, uint32_t* rk) {
   const uint64_t total = n_items(in);
@@ -538,7 +543,7 @@ __global__ void k_rank(In in, const uint32_t* seg_of, const uint32_t* seg_start,
     if (i >= len_of(in, s) || whole[s]) continue;
     const uint32_t k = seg_of[(size_t)s * in.steps + i];
     const uint32_t a = seg_start[k], b = seg_end[k];
-    if (a == b) continue;
+    if (b - a < RANK_INLINE) continue;  // k_build ranks these itself
     const uint32_t d = in.dot[fx_index(i, s, in.steps)];
     rk[(size_t)s * in.steps + i] = seg_rank(in, s, a, b, FX_DOT_SRC(d), FX_DOT_SEQ(d));
   }
@@ -565,7 +570,8 @@ __global__ void k_build(In in, const uint64_t* base, const uint32_t* maxseq, con
     const size_t to = fx_index(j, bk, sg.steps);
     const uint32_t d = in.dot[at];
     const uint32_t* srk = rk + (size_t)s * in.steps;
-    sg.dot[to] = FX_PACK_DOT(FX_DOT_SRC(d), srk[i]);
+    const bool inl = b - a < RANK_INLINE;
+    sg.dot[to] = FX_PACK_DOT(FX_DOT_SRC(d), inl ? seg_rank(in, s, a, b, FX_DOT_SRC(d), FX_DOT_SEQ(d)) : srk[i]);
     const uint32_t h = in.hdr[at];
     const uint32_t nd = min(FX_HDR_ND(h), in.dmax);
     uint32_t nk = 0;
@@ -573,7 +579,8 @@ __global__ void k_build(In in, const uint64_t* base, const uint32_t* maxseq, con
       const uint32_t u = in.deps[x * in.pw + at];
       const uint32_t p = pos[pos_slot(in, base, maxseq, s, u)];
       if (p < a) continue;  // executed in the prefix
-      sg.deps[nk * sg.pw + to] = FX_PACK_DOT(FX_DOT_SRC(u), srk[p]);
+      sg.deps[nk * sg.pw + to] =
+          FX_PACK_DOT(FX_DOT_SRC(u), inl ? seg_rank(in, s, a, b, FX_DOT_SRC(u), FX_DOT_SEQ(u)) : srk[p]);
       ++nk;
     }
     sg.hdr[to] = FX_MAKE_HDR(FX_HDR_T(h), nk, FX_HDR_KIND(h));
@@ -817,12 +824,14 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
     if (h_nbatch) {
       fx_stream_batch sin{sg.dot, sg.hdr, sg.deps, sg.lengths, SS, seg_steps, in.dmax, in.n};
       fx_order_batch sout{sorder, srelease, snexec, serr};
-      // segments are short (S5: 2 to 110 Adds, most under 16 pending): the
-      // batch starts at the group tier unless the caller names a first tier
-      // (same box, S5 4.02 against 4.27 ms per step from FX_TIER_DEFAULT,
-      // 100 % 6.03 against 6.17 ms; the wave tier 5.27 / 8.48, wide 17.1 / 22.2)
-      const uint32_t sflags = ((flags >> FX_FLAG_TIER_SHIFT) & 15u) ? flags : flags | FX_FLAG_FIRST_TIER(FX_TIER_GROUP);
-      const int st = run_tiered(&sin, &sout, sflags, hip_stream, nullptr, stats ? stats->tier_counts : nullptr);
+      // the batch starts at FX_TIER_DEFAULT unless the caller names a first
+      // tier.  The group tier first is 4-8 % faster per step (same box: S5 3.97
+      // against 4.30 ms, 2 % 1.01 against 1.08, 100 % 6.03 against 6.17) but
+      // reads 2.2x the HBM bytes at S5 (its 8 cached deps: 2.74 GB per step
+      // against the lane tier's 0.28) and 1.3x at 2 %, so it stays opt-in
+      // (FX_FLAG_FIRST_TIER(FX_TIER_GROUP)); the wave tier 5.27 / 8.48 ms and
+      // the wide tier 17.1 / 22.2 ms are slower
+      const int st = run_tiered(&sin, &sout, flags, hip_stream, nullptr, stats ? stats->tier_counts : nullptr);
       if (st == FX_ERR_HIP || st == FX_ERR_NO_DEVICE || st == FX_ERR_INVALID_ARG) return st;
       // (per-segment failures are handled below: their streams run whole)
       hipLaunchKernelGGL(k_scatter, dim3(grid_for(fx_plane_words(SS, seg_steps))), dim3(BT), 0, hs, SS, seg_steps,
