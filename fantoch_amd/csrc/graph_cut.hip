@@ -189,7 +189,7 @@ __global__ void k_maxseq(In in, uint32_t* maxseq, uint32_t* bad, uint32_t* part)
       const size_t at = fx_index(i, s, in.steps);
       const uint32_t d = in.dot[at];
       const uint32_t src = FX_DOT_SRC(d);
-      if (src < 1 || src > in.n || FX_HDR_KIND(in.hdr[at]) != FX_KIND_ADD) bad[s] = 1;
+      if (src < 1 || src > in.n) bad[s] = 1;  // (the record kind: k_reach, which reads hdr anyway)
       sq = FX_DOT_SEQ(d);
     }
     acc.add(out, s, sq);
@@ -219,14 +219,17 @@ __global__ void k_pos(In in, const uint64_t* base, const uint32_t* maxseq, uint3
 }
 
 // reach(i) = max(i, position of every dep); INF for a dep never added
-__global__ void k_reach(In in, const uint64_t* base, const uint32_t* maxseq, const uint32_t* pos, uint32_t* reach) {
+__global__ void k_reach(In in, const uint64_t* base, const uint32_t* maxseq, const uint32_t* pos, uint32_t* reach,
+                        uint32_t* bad) {
   const uint64_t total = n_items(in);
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t s, i;
     item(in, t, s, i);
     if (i >= len_of(in, s)) continue;
     const size_t at = fx_index(i, s, in.steps);
-    const uint32_t nd = FX_HDR_ND(in.hdr[at]);
+    const uint32_t h = in.hdr[at];
+    if (FX_HDR_KIND(h) != FX_KIND_ADD) bad[s] = 1;  // an index-only or executed record: the stream runs whole
+    const uint32_t nd = FX_HDR_ND(h);
     uint32_t r = i;
     for (uint32_t j = 0; j < nd && j < in.dmax; ++j) {
       const uint64_t slot = pos_slot(in, base, maxseq, s, in.deps[j * in.pw + at]);
@@ -530,9 +533,30 @@ __device__ __forceinline__ uint32_t seg_rank(const In& in, uint32_t s, uint32_t 
 // once (rk, stream-major) and k_build takes a dep's rank at the dep's
 // position (a dep outside the prefix lies in the segment: it ends at a cut):
 // S5, 3 deps per Add, k_build 1.14 ms -> k_rank 0.11 + k_build 0.29 ms.
-// (k_rank over the longer segments' batch slots instead of the stream's
-// Adds read less at 2 % but 1.45x the bytes at S5, and took 0.20 ms.)
-constexpr uint32_t RANK_INLINE = 4;
+// k_rank walks the stream's Adds (each reads its segment bounds to skip the
+// short ones); when the longer segments hold few Adds (2 % conflicts: most
+// segments are 1-4 Adds) k_rank_slots walks only their batch slots instead
+// (a prefix of the batch, which is ordered longest class first).  At S5 the
+// slot walk read 1.45x the bytes of the Add walk and took 0.20 against 0.11 ms.
+constexpr uint32_t RANK_INLINE = 4;    // class <= 2
+constexpr uint32_t RANK_CLASS_MIN = 3;  // classes ranked by k_rank / k_rank_slots
+
+__global__ void k_rank_slots(In in, uint32_t nl, uint32_t seg_steps, const uint32_t* bseg, const uint32_t* seg_stream,
+                             const uint32_t* seg_start, const uint32_t* seg_end, const uint32_t* whole, uint32_t* rk) {
+  const uint64_t total = fx_plane_words(nl, seg_steps);
+  const uint32_t steps4 = (seg_steps + 3u) >> 2;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t row = t >> 8;  // (tile, 4-step block) of the batch planes
+    const uint32_t bb = (uint32_t)(row / steps4) * 64u + ((uint32_t)(t & 255u) >> 2);
+    const uint32_t j = (uint32_t)(row % steps4) * 4u + (uint32_t)(t & 3u);
+    if (bb >= nl) continue;
+    const uint32_t k = bseg[bb];
+    const uint32_t a = seg_start[k], b = seg_end[k], s = seg_stream[k];
+    if (j > b - a || whole[s]) continue;  // (segments over MAX_SEG belong to whole streams)
+    const uint32_t d = in.dot[fx_index(a + j, s, in.steps)];
+    rk[(size_t)s * in.steps + a + j] = seg_rank(in, s, a, b, FX_DOT_SRC(d), FX_DOT_SEQ(d));
+  }
+}
 
 __global__ void k_rank(In in, const uint32_t* seg_of, const uint32_t* seg_start, const uint32_t* seg_end,
                        const uint32_t* whole, uint32_t* rk) {
@@ -699,7 +723,7 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
   if (!base || !pos || !reach) return FX_ERR_HIP;
   (void)hipMemcpyAsync(base, h_base.data(), (size_t)S * 8, hipMemcpyHostToDevice, hs);
   hipLaunchKernelGGL(k_pos, dim3(grid_for(work)), dim3(BT), 0, hs, in, base, maxseq, pos, bad);
-  hipLaunchKernelGGL(k_reach, dim3(grid_for(work)), dim3(BT), 0, hs, in, base, maxseq, pos, reach);
+  hipLaunchKernelGGL(k_reach, dim3(grid_for(work)), dim3(BT), 0, hs, in, base, maxseq, pos, reach, bad);
   // 2. cut flags (prefix max of reach) and segment counts
   const uint32_t nch = (in.steps + CHUNK - 1) / CHUNK;
   uint32_t* cagg = db.alloc<uint32_t>((size_t)S * nch);
@@ -818,7 +842,18 @@ extern "C" int fx_batch_run_cut(const fx_stream_batch* in_, const fx_order_batch
     if (!sg.dot || !sg.hdr || !sg.deps || !sg.lengths || !sorder || !srelease || !snexec || !serr) return FX_ERR_HIP;
     uint32_t* rk = db.alloc<uint32_t>(work);
     if (!rk) return FX_ERR_HIP;
-    hipLaunchKernelGGL(k_rank, dim3(grid_for(work)), dim3(BT), 0, hs, in, seg_of, seg_start, seg_end, whole, rk);
+    // the longer segments' Adds, bounded by their class (<= 2^c each)
+    uint32_t nl = 0;
+    uint64_t nl_adds = 0;
+    for (uint32_t c = RANK_CLASS_MIN; c < NCLS; ++c) {
+      nl += h_ctot[c];
+      nl_adds += (uint64_t)h_ctot[c] << std::min(c, 12u);
+    }
+    if (nl_adds * 8 < work)
+      hipLaunchKernelGGL(k_rank_slots, dim3(grid_for(fx_plane_words(std::max(nl, 1u), seg_steps))), dim3(BT), 0, hs,
+                         in, nl, seg_steps, bseg, seg_stream, seg_start, seg_end, whole, rk);
+    else
+      hipLaunchKernelGGL(k_rank, dim3(grid_for(work)), dim3(BT), 0, hs, in, seg_of, seg_start, seg_end, whole, rk);
     hipLaunchKernelGGL(k_build, dim3(grid_for(work)), dim3(BT), 0, hs, in, base, maxseq, pos, seg_of, seg_start,
                        seg_end, bidx, whole, rk, sg, out->order, out->release);
     if (h_nbatch) {
