@@ -64,7 +64,6 @@ constexpr uint32_t TIME_LIMIT = 1u << 24;  // ms; the event key holds time << 8
 // per-instance LDS: the histogram caches, then lane tables kept out of the
 // register file (the 5-wave configs[3] build spills what does not fit): at
 // 8 p + s, p's committed GC frontier of source s + 1, its previous stable
-// frontier, the link delay p -> s
 // frontier, the link delay p -> s; and two 64-bit sums (the executor Adds'
 // deps, the client latencies)
 constexpr uint32_t L_GCF = HC_BINS + HD_BINS + 2 * HL_SLOTS, L_GPS = L_GCF + 64, L_DPQ = L_GPS + 64;
