@@ -99,6 +99,53 @@ def test_cut_unsplittable_and_errors():
     assert_parity(planes, res)
 
 
+def _segment_stream(lengths, n, seq0=None):
+    """One commit stream made of dependency-closed segments of the given
+    lengths: a segment of L > 1 Adds is a cycle (Add j waits on Add j + 1 mod
+    L, dots spread over the n sources), a segment of 1 Add has no deps."""
+    seq = dict(seq0 or {}) or {q: 0 for q in range(1, n + 1)}
+    out, t = [], 1
+    for L in lengths:
+        dots = []
+        for j in range(L):
+            src = 1 + (len(out) + j) % n
+            seq[src] += 1
+            dots.append((src, seq[src]))
+        for j in range(L):
+            deps = [dots[(j + 1) % L]] if L > 1 else []
+            out.append((dots[j], deps, t))
+            t += 1
+    return out
+
+
+@pytest.mark.parametrize("many_long", [False, True])
+def test_cut_segment_length_classes(many_long):
+    """Segments of every length class (1 to 130 Adds, cycles) in a few
+    streams: the batch ordered longest class first, ranks by k_rank_slots
+    (the longer segments hold few Adds) or by k_rank over every Add; the
+    outputs equal the oracle's."""
+    n = 5
+    rng = np.random.default_rng(17 if many_long else 16)
+    streams = []
+    for s in range(3):
+        longs = [2, 3, 4, 5, 8, 9, 16, 17, 32, 33, 64, 65, 130]
+        lengths = longs * (6 if many_long else 1) + [1] * (100 if many_long else 6000)
+        rng.shuffle(lengths)
+        streams.append(_segment_stream(lengths, n))
+    planes = fs.pack_streams(streams, n)
+    res = fd.run_batch(planes, cut=True, nbins_chain=256, nbins_delay=4096)
+    assert res.status == _lib.FX_OK
+    o_order, o_rel, o_nexec = assert_parity(planes, res)
+    assert np.all(res.nexec == planes.lengths)
+    chain, delay = oracle_hists(planes, o_order, o_rel, o_nexec, 256, 4096)
+    assert np.array_equal(res.chain, chain) and np.array_equal(res.delay, delay)
+    st = res.cut_stats
+    assert st.whole_streams == 0 and st.failed_streams == 0
+    assert st.segments == 3 * len(lengths)
+    assert st.single_segments == 3 * lengths.count(1)
+    assert st.max_segment == 130
+
+
 def test_config4_single_huge_instance_cut():
     """BASELINE configs[4]: one instance, five executors each fed a
     10^6-Add commit stream with cycles; bit-exact with the oracle and timed
