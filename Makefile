@@ -33,6 +33,10 @@ $(OBJDIR)/%.o: fantoch_amd/csrc/% $(HDRS)
 # one wait state a VALU write of the same VGPR needs (sim_wave.hip prm, fixed
 # in round 4; tests/test_sim_poison.py's zero fill catches it deterministically).
 # max-ilp / min-reg / max-occupancy / memory-clause: 418 - 423 M (round 3).
+# Round 6, same box, two runs each (profiles/r06_sim_sched_ab.txt): iterative-ILP
+# 428.9 / 429.2 / 429.6 M; max-ilp 430.1 / 430.4 / 429.9; iterative-ILP with
+# -amdgpu-set-wave-priority 431.5 / 431.0 / 429.8; max-ilp with it 427.2 / 426.9;
+# iterative-minreg 428.6: within noise, so the schedule the tests ran on stays.
 SIM_SCHED := -mllvm -amdgpu-sched-strategy=iterative-ilp
 # the large-instance simulator and the wide executor tiers under the iterative
 # ILP scheduler: configs[3] simulator 99.1 -> 103.1 M, dense executor 66.7 ->
